@@ -1,0 +1,157 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-2 XL (1.5 B) training throughput at sequence length 2048.
+
+Metric (BASELINE.json): samples/sec for the whole node.  Synthetic token data, random-init
+weights, bf16 compute with fp32 master weights + fused AdamW, full training step
+(forward, backward, gradient all-reduce over RCCL, optimizer step) through the smp API:
+``smp.init`` -> ``smp.DistributedModel`` -> ``smp.DistributedOptimizer`` -> ``@smp.step``.
+
+Single GPU:  python bench.py
+N GPUs:      python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+                 --master-port P bench.py --gpus N
+Scaling is weak: the per-GPU micro-batch is fixed, global batch = mbs x microbatches x N/(pp*tp).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="gpt2-xl")
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--mbs", type=int, default=8, help="per-GPU micro-batch size")
+    ap.add_argument("--microbatches", type=int, default=1)
+    ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-flash", action="store_true")
+    ap.add_argument("--activation-checkpointing", action="store_true")
+    ap.add_argument("--shard-optimizer-state", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import smdistributed_modelparallel_amd.torch as smp
+    from smdistributed_modelparallel_amd.models import GPT_CONFIGS, build_gpt, gpt_inputs
+    from smdistributed_modelparallel_amd.models.gpt import train_flops_per_token
+
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    cfg = {
+        "pipeline_parallel_degree": args.pp,
+        "tensor_parallel_degree": args.tp,
+        "microbatches": args.microbatches,
+        "ddp": world > 1 or args.tp > 1,
+        "bf16": True,
+        "amd_fused_attention": not args.no_flash,
+        "shard_optimizer_state": args.shard_optimizer_state,
+    }
+    if args.pp > 1:
+        cfg["auto_partition"] = True
+    smp.init(cfg)
+    torch.manual_seed(1234 + smp.dp_rank())
+    mc = GPT_CONFIGS[args.model]
+    with smp.model_creation(tensor_parallelism=args.tp > 1, dtype=torch.float32):
+        model = build_gpt(args.model, dropout=args.dropout, num_positions=max(args.seq, mc["num_positions"]))
+    model = smp.DistributedModel(model)
+    if args.activation_checkpointing:
+        for layer in model.get_module().transformer.seq_layers:
+            smp.set_activation_checkpointing(layer)
+    decay, no_decay = [], []
+    for n, p in model.get_module().named_parameters():
+        (no_decay if (p.dim() < 2 or "bias" in n or "norm" in n) else decay).append(p)
+    inner = torch.optim.AdamW([{"params": decay, "weight_decay": 0.1}, {"params": no_decay, "weight_decay": 0.0}],
+                              lr=1e-4, betas=(0.9, 0.95), eps=1e-8)
+    opt = smp.DistributedOptimizer(inner)
+
+    @smp.step
+    def train_step(model, ids, mask, labels):
+        loss, _ = model((ids, mask, None, None, labels))
+        model.backward(loss)
+        return loss
+
+    dev = torch.device("cuda", smp.local_rank()) if torch.cuda.is_available() else torch.device("cpu")
+    batch = args.mbs * args.microbatches
+    g = torch.Generator(device=dev)
+    g.manual_seed(42 + smp.rank())
+    data = [gpt_inputs(batch, args.seq, mc["vocab_size"], dev, generator=g) for _ in range(2)]
+
+    def one(i):
+        ids, mask, _, _, labels = data[i % len(data)]
+        opt.zero_grad()
+        out = train_step(model, ids, mask, labels)
+        opt.step()
+        return out
+
+    for i in range(args.warmup):
+        out = one(i)
+    loss_val = float(out.reduce_mean()) if out is not None and smp.pp_rank() == 0 else float("nan")
+
+    def sync():
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.barrier()
+
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = one(i)
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt / args.steps * 1000.0
+    # scaled-batch TP: every data-parallel rank (TP ranks included) consumes its own batch
+    global_batch = batch * smp.dp_size()
+    samples_per_s = global_batch * args.steps / dt
+    tokens_per_s = samples_per_s * args.seq
+    flops = train_flops_per_token(args.model, args.seq) * tokens_per_s
+    if smp.rank() == 0:
+        par = f"pp{args.pp}xtp{args.tp}xdp{max(1, world // (args.pp * args.tp))}"
+        rec = {
+            "metric": "samples/sec (whole node) GPT-2 XL seq2048",
+            "value": round(samples_per_s, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic",
+            "config": {
+                "model": args.model,
+                "global_batch": global_batch,
+                "seq_len": args.seq,
+                "parallelism": par,
+                "micro_batch_per_gpu": args.mbs,
+                "microbatches": args.microbatches,
+                "flash_attention": not args.no_flash,
+                "dropout": args.dropout,
+            },
+            "tokens_per_s": round(tokens_per_s, 1),
+            "model_tflops_per_gpu": round(flops / world / 1e12, 1),
+            "final_loss": round(loss_val, 4),
+        }
+        print(json.dumps(rec), flush=True)
+    smp.barrier()
+
+
+if __name__ == "__main__":
+    main()

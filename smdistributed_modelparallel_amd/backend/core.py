@@ -1,0 +1,275 @@
+"""Process topology, native runtime bring-up and coordinated shutdown.
+
+Reference parity: `smp/backend/core.py:165-562` (rank/size/group queries, world-size
+validation, ExitHook, shutdown on exit).  MPI is replaced by the launcher environment
+(``torchrun``: RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE) and the native mailbox
+is wired up through a key-value store rendezvous (the torch.distributed TCPStore).
+"""
+import atexit
+import os
+import socket
+import sys
+
+from .collectives import CollectiveCommunicator, CommGroup
+from .exceptions import InvalidEnvironmentError, NotInitializedError, WorkerSizeError
+from .logger import get_logger
+from .native import runtime
+from .topology import Ranker
+
+logger = get_logger()
+
+
+class ExitHook:
+    """Intercepts sys.exit/excepthook so shutdown can report a consistent status
+    (reference `core.py:165-188`)."""
+
+    def __init__(self):
+        self.exit_code = None
+        self.exception = None
+        self._orig_exit = None
+        self._orig_excepthook = None
+
+    def hook(self):
+        self._orig_exit = sys.exit
+        self._orig_excepthook = sys.excepthook
+        sys.exit = self.exit
+        sys.excepthook = self.exc_handler
+
+    def unhook(self):
+        if self._orig_exit is not None:
+            sys.exit = self._orig_exit
+            sys.excepthook = self._orig_excepthook
+
+    def exit(self, code=0):
+        self.exit_code = code
+        self._orig_exit(code)
+
+    def exc_handler(self, exc_type, exc, *args):
+        self.exception = exc
+        self._orig_excepthook(exc_type, exc, *args)
+
+
+def _env_int(*names, default=None):
+    for n in names:
+        v = os.environ.get(n)
+        if v is not None and v != "":
+            return int(v)
+    return default
+
+
+def _local_ip(master_addr):
+    if master_addr in ("127.0.0.1", "localhost"):
+        return "127.0.0.1"
+    try:
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        s.connect((master_addr, 9))
+        ip = s.getsockname()[0]
+        s.close()
+        return ip
+    except OSError:
+        return "127.0.0.1"
+
+
+class ModelParallelCore:
+    def __init__(self):
+        self.cfg = None
+        self.ranker = None
+        self.mailbox = None
+        self.comm = None
+        self.timeline = None
+        self.exit_hook = None
+        self._initialized = False
+        self._rank = 0
+        self._size = 1
+        self._local_rank = 0
+        self._local_size = 1
+
+    # ----------------------------------------------------------- lifecycle
+    @property
+    def initialized(self):
+        return self._initialized
+
+    def read_environment(self):
+        self._rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", default=0)
+        self._size = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", default=1)
+        self._local_rank = _env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", default=self._rank)
+        self._local_size = _env_int("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", default=self._size)
+        if self._rank >= self._size or self._local_rank >= self._local_size:
+            raise InvalidEnvironmentError(
+                f"inconsistent launcher environment: rank {self._rank}/{self._size}, "
+                f"local {self._local_rank}/{self._local_size}"
+            )
+
+    def _validate_worker_size(self, cfg):
+        pp, tp = cfg.pipeline_parallel_degree, cfg.tensor_parallel_degree
+        if self._size % (pp * tp) != 0:
+            raise WorkerSizeError(
+                f"World size {self._size} must be divisible by pipeline_parallel_degree x "
+                f"tensor_parallel_degree = {pp * tp}."
+            )
+        if cfg.zero2d_enabled():
+            if self._size % cfg.sharded_data_parallel_degree != 0:
+                raise WorkerSizeError(
+                    f"World size {self._size} must be divisible by sharded_data_parallel_degree "
+                    f"{cfg.sharded_data_parallel_degree}."
+                )
+        dp = self._size // pp
+        if dp > 1 and not (cfg.ddp or cfg.horovod or cfg.zero2d_enabled()):
+            raise WorkerSizeError(
+                f"World size {self._size} implies data parallelism of degree {dp // tp}; enable 'ddp' in the config."
+            )
+
+    def initialize(self, cfg, store, device_count=None):
+        """`store` is a torch.distributed Store shared by all ranks."""
+        self.cfg = cfg
+        self.read_environment()
+        self._validate_worker_size(cfg)
+        if device_count is not None and device_count > 0 and self._local_size > device_count:
+            raise InvalidEnvironmentError(
+                f"{self._local_size} processes on this node but only {device_count} GPUs are visible."
+            )
+        pp, tp = cfg.pipeline_parallel_degree, cfg.tensor_parallel_degree
+        rdp = self._size // (pp * tp)
+        self.ranker = Ranker(cfg.placement_strategy, rdp, pp, tp)
+
+        rt = runtime()
+        self.mailbox = rt.Mailbox(self._rank, self._size)
+        host = _local_ip(os.environ.get("MASTER_ADDR", "127.0.0.1"))
+        port = self.mailbox.listen("0.0.0.0" if host != "127.0.0.1" else "127.0.0.1")
+        store.set(f"smp/mailbox/{self._rank}", f"{host}:{port}")
+        hosts, ports = [], []
+        for r in range(self._size):
+            h, p = store.get(f"smp/mailbox/{r}").decode().rsplit(":", 1)
+            hosts.append(h)
+            ports.append(int(p))
+        self.mailbox.connect(hosts, ports, float(os.environ.get("SMP_CONNECT_TIMEOUT", "300")))
+        self.comm = CollectiveCommunicator(self, self.mailbox)
+
+        self.timeline = rt.Timeline(self._rank)
+        tl = os.environ.get("SMP_TIMELINE_FILE")
+        if tl:
+            self.timeline.set_output(tl.replace("{rank}", str(self._rank)))
+
+        if cfg.zero2d_enabled():
+            cfg.construct_zero2d_config_dict(self)
+
+        self.exit_hook = ExitHook()
+        self.exit_hook.hook()
+        atexit.register(self.shutdown)
+        self._initialized = True
+
+    def shutdown(self):
+        if not self._initialized:
+            return
+        self._initialized = False
+        success = True
+        if self.exit_hook is not None:
+            success = self.exit_hook.exception is None and self.exit_hook.exit_code in (None, 0)
+            self.exit_hook.unhook()
+        try:
+            if self.timeline is not None:
+                self.timeline.flush()
+            if self.mailbox is not None:
+                if success:
+                    self.mailbox.flush()
+                self.mailbox.shutdown()
+        except Exception as e:  # pragma: no cover - best effort at exit
+            logger.debug(f"shutdown: {e}")
+
+    def _check(self):
+        if not self._initialized:
+            raise NotInitializedError()
+
+    # ------------------------------------------------------------- queries
+    def rank(self):
+        return self._rank
+
+    def size(self):
+        return self._size
+
+    def local_rank(self):
+        return self._local_rank
+
+    def local_size(self):
+        return self._local_size
+
+    def pp_rank(self):
+        return self.ranker.get_pp_rank(self._rank)
+
+    def tp_rank(self):
+        return self.ranker.get_tp_rank(self._rank)
+
+    def rdp_rank(self):
+        return self.ranker.get_rdp_rank(self._rank)
+
+    def dp_rank(self):
+        return self.ranker.get_dp_rank(self._rank)
+
+    def mp_rank(self):
+        return self.ranker.get_mp_rank(self._rank)
+
+    def pp_size(self):
+        return self.ranker.size_map["P"]
+
+    def tp_size(self):
+        return self.ranker.size_map["T"]
+
+    def rdp_size(self):
+        return self.ranker.size_map["D"]
+
+    def dp_size(self):
+        return self.ranker.size_map["D"] * self.ranker.size_map["T"]
+
+    def mp_size(self):
+        return self.ranker.size_map["P"] * self.ranker.size_map["T"]
+
+    def get_pp_group(self):
+        return self.ranker.get_pp_group(self._rank)
+
+    def get_tp_group(self):
+        return self.ranker.get_tp_group(self._rank)
+
+    def get_rdp_group(self):
+        return self.ranker.get_rdp_group(self._rank)
+
+    def get_dp_group(self):
+        return self.ranker.get_dp_group(self._rank)
+
+    def get_mp_group(self):
+        return self.ranker.get_mp_group(self._rank)
+
+    def get_group_ranks(self, group):
+        if group == CommGroup.WORLD:
+            return list(range(self._size))
+        return {
+            CommGroup.PP_GROUP: self.get_pp_group,
+            CommGroup.TP_GROUP: self.get_tp_group,
+            CommGroup.RDP_GROUP: self.get_rdp_group,
+            CommGroup.DP_GROUP: self.get_dp_group,
+            CommGroup.MP_GROUP: self.get_mp_group,
+        }[group]()
+
+    def pp_rank_to_rank(self, pp_rank):
+        return self.ranker.translate(pp_rank, self.tp_rank(), self.rdp_rank())
+
+    def is_in_same_instance(self, other_rank):
+        return (other_rank // self._local_size) == (self._rank // self._local_size)
+
+    def instance_id(self):
+        return self._rank // self._local_size
+
+    def barrier(self):
+        self.comm.barrier(CommGroup.WORLD)
+
+    def timeline_start_step(self, step):
+        if self.timeline is not None:
+            self.timeline.start_step(step)
+
+    def timeline_end_step(self):
+        if self.timeline is not None:
+            self.timeline.end_step()
+
+    def timeline_record_pipeline_event(self, mb, label):
+        if self.timeline is not None and self.timeline.enabled:
+            self.timeline.mark(mb, label)
+

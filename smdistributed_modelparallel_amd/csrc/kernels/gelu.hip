@@ -1,0 +1,177 @@
+// Fused bias + tanh-GeLU forward/backward (K17 of SURVEY §2.6; the reference runs this
+// as TorchScript, `smp/torch/nn/gelu.py:29-64`) and a column-sum kernel for bias grads.
+//
+// Elementwise and HBM-bound: 16-byte vectors (8 bf16) per lane, bias broadcast over the
+// last dim, fp32 math.  The backward recomputes tanh from the saved pre-activation
+// (x + bias is never materialised).
+#include "common.h"
+#include "kernels.h"
+
+namespace smpk {
+namespace {
+
+constexpr float kC0 = 0.7978845608028654f;  // sqrt(2/pi)
+constexpr float kC1 = 0.044715f;
+
+__device__ __forceinline__ float gelu_f(float x) {
+  const float u = kC0 * (x + kC1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float u = kC0 * (x + kC1 * x * x * x);
+  const float t = tanhf(u);
+  const float du = kC0 * (1.f + 3.f * kC1 * x * x);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
+                                                            T* __restrict__ y, int64_t rows, int64_t cols) {
+  constexpr int N = Vec16<T>::N;
+  const int64_t total = rows * cols;
+  if (VEC) {
+    for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * N; i < total;
+         i += static_cast<int64_t>(gridDim.x) * 256 * N) {
+      Vec16<T> a = load16(x + i);
+      const int64_t c = i % cols;
+      Vec16<T> bb;
+      if (bias) bb = load16(bias + c);
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float v = to_f32(a.v[j]) + (bias ? to_f32(bb.v[j]) : 0.f);
+        o.v[j] = from_f32<T>(gelu_f(v));
+      }
+      store16(y + i, o);
+    }
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
+         i += static_cast<int64_t>(gridDim.x) * 256) {
+      float v = to_f32(x[i]) + (bias ? to_f32(bias[i % cols]) : 0.f);
+      y[i] = from_f32<T>(gelu_f(v));
+    }
+  }
+}
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const T* __restrict__ bias, T* __restrict__ dx,
+                                                            int64_t rows, int64_t cols) {
+  constexpr int N = Vec16<T>::N;
+  const int64_t total = rows * cols;
+  if (VEC) {
+    for (int64_t i = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * N; i < total;
+         i += static_cast<int64_t>(gridDim.x) * 256 * N) {
+      Vec16<T> a = load16(x + i);
+      Vec16<T> d = load16(dy + i);
+      const int64_t c = i % cols;
+      Vec16<T> bb;
+      if (bias) bb = load16(bias + c);
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float v = to_f32(a.v[j]) + (bias ? to_f32(bb.v[j]) : 0.f);
+        o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad(v));
+      }
+      store16(dx + i, o);
+    }
+  } else {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
+         i += static_cast<int64_t>(gridDim.x) * 256) {
+      float v = to_f32(x[i]) + (bias ? to_f32(bias[i % cols]) : 0.f);
+      dx[i] = from_f32<T>(to_f32(dy[i]) * gelu_grad(v));
+    }
+  }
+}
+
+// Column sums: grid (ceil(cols/64), parts); 64 columns x 4 row lanes per block.
+template <typename T>
+__global__ void __launch_bounds__(256) col_sum_partial(const T* __restrict__ x, float* __restrict__ part,
+                                                       int64_t rows, int64_t cols, int64_t rows_per_part) {
+  __shared__ float s[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + cl;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
+  const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
+  float a = 0.f;
+  if (c < cols)
+    for (int64_t r = r0 + rl; r < r1; r += 4) a += to_f32(x[r * cols + c]);
+  s[rl][cl] = a;
+  __syncthreads();
+  if (rl == 0 && c < cols) part[static_cast<int64_t>(blockIdx.y) * cols + c] = s[0][cl] + s[1][cl] + s[2][cl] + s[3][cl];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) col_sum_final(const float* __restrict__ part, T* __restrict__ out, int parts,
+                                                     int64_t cols) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float a = 0.f;
+  for (int p = 0; p < parts; ++p) a += part[p * cols + c];
+  out[c] = from_f32<T>(a);
+}
+
+inline int elt_grid(int64_t total, int per_thread) {
+  int64_t b = (total / per_thread + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return static_cast<int>(b);
+}
+
+}  // namespace
+
+int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s) {
+  const int64_t total = rows * cols;
+  if (total <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    constexpr int N = Vec16<T>::N;
+    const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                                          reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
+    if (vec)
+      bias_gelu_fwd_kernel<T, true><<<elt_grid(total, N), 256, 0, s>>>(
+          static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
+    else
+      bias_gelu_fwd_kernel<T, false><<<elt_grid(total, 1), 256, 0, s>>>(
+          static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
+                  hipStream_t s) {
+  const int64_t total = rows * cols;
+  if (total <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    constexpr int N = Vec16<T>::N;
+    const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+                                          reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) &
+                                         15) == 0;
+    if (vec)
+      bias_gelu_bwd_kernel<T, true><<<elt_grid(total, N), 256, 0, s>>>(
+          static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(dx), rows,
+          cols);
+    else
+      bias_gelu_bwd_kernel<T, false><<<elt_grid(total, 1), 256, 0, s>>>(
+          static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(dx), rows,
+          cols);
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+// workspace: parts * cols floats with parts = min(256, ceil(rows / 64)).
+int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  int64_t parts = (rows + 63) / 64;
+  if (parts > 256) parts = 256;
+  const int64_t rpp = (rows + parts - 1) / parts;
+  SMPK_DISPATCH(dt, T, {
+    dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(parts));
+    col_sum_partial<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), workspace, rows, cols, rpp);
+    col_sum_final<T><<<static_cast<int>((cols + 255) / 256), 256, 0, s>>>(workspace, static_cast<T*>(out),
+                                                                        static_cast<int>(parts), cols);
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace smpk

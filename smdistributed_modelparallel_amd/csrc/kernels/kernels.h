@@ -1,0 +1,127 @@
+// Host-side launcher API of the gfx950 kernels.  Pure C++ (no torch types) so the
+// kernels are reusable and their translation units compile quickly; the torch binding
+// layer (bindings.cpp) validates tensors and forwards raw pointers + the current stream.
+// Every launcher returns 0 on success or a hipError_t / negative code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smpk {
+
+enum DType : int { F32 = 0, F16 = 1, BF16 = 2 };
+
+// ---------------------------------------------------------------- optimizers (optim.hip)
+// Fused Adam/AdamW over one contiguous range. param may be null (master is the param).
+int fused_adam(int param_dt, void* param, int grad_dt, const void* grad, float* master, float* exp_avg,
+               float* exp_avg_sq, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+               float bias_c1, float bias_c2, float grad_scale, int adamw_mode, hipStream_t s);
+int fused_sgd(int param_dt, void* param, int grad_dt, const void* grad, float* master, float* mom, int64_t n,
+              float lr, float momentum, float dampening, float weight_decay, int nesterov, int first_run,
+              float grad_scale, hipStream_t s);
+int fused_adagrad(int param_dt, void* param, int grad_dt, const void* grad, float* master, float* sum, int64_t n,
+                  float lr, float eps, float weight_decay, float grad_scale, hipStream_t s);
+// LAMB stage 1: update = adam_direction + wd * p  (written into `update`), m/v updated.
+int lamb_stage1(int grad_dt, const void* grad, const float* master, float* exp_avg, float* exp_avg_sq,
+                float* update, int64_t n, float beta1, float beta2, float eps, float weight_decay, float bias_c1,
+                float bias_c2, float grad_scale, hipStream_t s);
+// LAMB stage 2: p -= lr * trust * update, trust from per-range norms (device scalars).
+int lamb_stage2(int param_dt, void* param, float* master, const float* update, int64_t n, float lr,
+                const float* p_norm_sq, const float* u_norm_sq, int use_trust, hipStream_t s);
+// sum of squares of x (any dtype) * scale^2 accumulated into *out (fp32, atomic).
+int sumsq(int dt, const void* x, int64_t n, float scale, float* out, hipStream_t s);
+// *out = max(*out, 1 if any element non-finite).
+int nonfinite(int dt, const void* x, int64_t n, float* out, hipStream_t s);
+// y = a * x + b * y (elementwise, same dtype) ; y may equal x.
+int axpby(int dt, const void* x, void* y, int64_t n, float a, float b, hipStream_t s);
+// copy with cast: dst(dt_dst) = src(dt_src) * scale
+int cast_copy(int dt_src, const void* src, int dt_dst, void* dst, int64_t n, float scale, hipStream_t s);
+
+// ------------------------------------------------------------------ norms (layernorm.hip)
+// y = (x - mean) * rstd * w + b ; optional residual add: x = x + r written to x_out first.
+int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
+                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);
+int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
+                  const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
+                  int part_rows, const void* dres, hipStream_t s);
+int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
+                         int64_t cols, hipStream_t s);
+// Distributed-LN pieces (hidden sharded across TP): apply with global stats, local sums.
+int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const void* b, const float* mean,
+                          const float* var, void* y, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);
+int layernorm_local_sums(int dt, const void* x, const float* mean, hipStream_t s);
+int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned);
+
+// ------------------------------------------------------------- elementwise (gelu.hip)
+// y = gelu_tanh(x + bias) ; bias broadcast over the last dim (may be null).
+int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s);
+// dx = dy * gelu'(x + bias) ; dbias partial sums per row-chunk (fp32) when dbias_part != null.
+int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
+                  hipStream_t s);
+// Column sums of a [rows, cols] matrix into fp32 partials then final (for bias grads).
+int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s);
+
+// --------------------------------------------------------------- softmax (softmax.hip)
+int scaled_masked_softmax_fwd(int dt, const void* x, const uint8_t* mask, void* y, int64_t batch, int64_t heads,
+                              int64_t sq, int64_t sk, int64_t mask_batch, float scale, hipStream_t s);
+int scaled_upper_triang_softmax_fwd(int dt, const void* x, void* y, int64_t attn_batches, int64_t sq, int64_t sk,
+                                    float scale, hipStream_t s);
+int scaled_softmax_bwd(int dt, const void* dy, const void* y, void* dx, int64_t rows, int64_t cols, float scale,
+                       hipStream_t s);
+
+// ------------------------------------------------------------------------ rope (rope.hip)
+// In-place rotary embedding on x [b, s, h, d] using rotary_dim, style 0 = GPT-J
+// (interleaved pairs), 1 = NeoX (half rotation). cos/sin tables [s, rotary_dim/2] fp32.
+int rope_apply(int dt, void* x, const float* cos_t, const float* sin_t, int64_t b, int64_t s_len, int64_t h,
+               int64_t d, int64_t rotary_dim, int64_t stride_b, int64_t stride_s, int64_t stride_h, int style,
+               int inverse, int64_t pos_offset, hipStream_t s);
+
+// -------------------------------------------------------------- attention (attention.hip)
+// Flash-style attention, bf16/fp16 in, fp32 softmax stats. q,k,v,o: [b, h, s, d] with
+// explicit strides (elements); lse: [b, h, sq] fp32.
+struct AttnParams {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  int64_t b, h, sq, sk, d;
+  int64_t q_sb, q_sh, q_ss;
+  int64_t k_sb, k_sh, k_ss;
+  int64_t v_sb, v_sh, v_ss;
+  int64_t o_sb, o_sh, o_ss;
+  float scale;
+  int causal;
+  int window;  // >0: local attention window (GPT-Neo)
+};
+struct AttnBwdParams {
+  AttnParams f;
+  const void* dout;
+  int64_t do_sb, do_sh, do_ss;
+  void* dq;
+  void* dk;
+  void* dv;
+  int64_t dq_sb, dq_sh, dq_ss;
+  int64_t dk_sb, dk_sh, dk_ss;
+  int64_t dv_sb, dv_sh, dv_ss;
+  float* delta;  // [b, h, sq] workspace
+  float* dq_acc;  // [b, h, sq, d] fp32 workspace
+};
+int attention_fwd(int dt, const AttnParams& p, hipStream_t s);
+int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);
+
+// ------------------------------------------------------- cross entropy (cross_entropy.hip)
+// Per-row: lse over [vocab_start, vocab_end) local shard; returns local max / sumexp /
+// target logit (target may be outside the shard -> 0). Fused fwd writes softmax stats;
+// bwd writes dlogits = (softmax - onehot) * grad.
+int xent_fwd_stats(int dt, const void* logits, const int64_t* target, int64_t rows, int64_t vocab, int64_t vocab_start,
+                   float* row_max, float* row_sumexp, float* row_target_logit, int64_t ignore_index, hipStream_t s);
+int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row_lse, const float* grad_rows,
+             void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s);
+
+// ---------------------------------------------------------------- pack / unpack (pack.hip)
+// Generic strided 4-D copy: dst[i0,i1,i2,i3] = src[...] with element strides (for the
+// split/merge-axis all-to-all and allgatherv packing).
+int strided_copy4(int elem_bytes, const void* src, void* dst, const int64_t* sizes, const int64_t* src_strides,
+                  const int64_t* dst_strides, hipStream_t s);
+
+}  // namespace smpk

@@ -1,0 +1,416 @@
+// Fused LayerNorm forward/backward (K9/K10/K11 of SURVEY §2.6) and the distributed-LN
+// "apply with global statistics" piece (K6).
+//
+// One wave64 per row: every lane keeps VPT 16-byte vectors of its row in registers, so
+// x is read once, mean/variance come from two wave reductions (exact two-pass variance
+// on the register copy) and y is written once.  4 rows per 256-thread block.  An
+// optional residual input is added in the same pass and the sum written out
+// (pre-LN transformer: h = h + f(h); ln(h) in one kernel).
+// Rows wider than the register budget fall back to a block-per-row streaming kernel.
+//
+// Backward: dx per row in registers; dgamma/dbeta accumulated per lane across the rows a
+// block owns, combined across the block's waves in LDS and written as fp32 partials,
+// then reduced by a column kernel (deterministic, no atomics).
+#include "common.h"
+#include "kernels.h"
+
+namespace smpk {
+namespace {
+
+constexpr int kRowsPerBlock = 4;
+
+template <typename T, typename W, int VPT>
+__global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const T* __restrict__ res,
+                                                  T* __restrict__ x_out, const W* __restrict__ w,
+                                                  const W* __restrict__ b, T* __restrict__ y,
+                                                  float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                  int64_t rows, int cols, float eps) {
+  constexpr int N = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * cols;
+  float v[VPT][N];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = (k * 64 + lane) * N;
+    if (c < cols) {
+      Vec16<T> a = load16(xr + c);
+      if (res != nullptr) {
+        Vec16<T> r = load16(res + row * cols + c);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          v[k][j] = to_f32(a.v[j]) + to_f32(r.v[j]);
+          a.v[j] = from_f32<T>(v[k][j]);
+        }
+        store16(x_out + row * cols + c, a);
+#pragma unroll
+        for (int j = 0; j < N; ++j) v[k][j] = to_f32(a.v[j]);  // normalise the rounded sum
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) v[k][j] = to_f32(a.v[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) sum += v[k][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) v[k][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(sum) / cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = (k * 64 + lane) * N;
+    if (c < cols) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float d = v[k][j] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / cols + eps);
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = (k * 64 + lane) * N;
+    if (c < cols) {
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        float g = w ? to_f32(w[c + j]) : 1.f;
+        float bb = b ? to_f32(b[c + j]) : 0.f;
+        o.v[j] = from_f32<T>((v[k][j] - mean) * rstd * g + bb);
+      }
+      store16(y + row * cols + c, o);
+    }
+  }
+}
+
+// Generic fallback: one block per row, streaming (any width, any alignment).
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) ln_fwd_stream(const T* __restrict__ x, const T* __restrict__ res,
+                                                     T* __restrict__ x_out, const W* __restrict__ w,
+                                                     const W* __restrict__ b, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int64_t rows, int cols, float eps) {
+  __shared__ float smem[16];
+  const int64_t row = blockIdx.x;
+  const T* xr = x + row * cols;
+  float sum = 0.f;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    float a = to_f32(xr[c]);
+    if (res != nullptr) {
+      T s = from_f32<T>(a + to_f32(res[row * cols + c]));
+      x_out[row * cols + c] = s;
+      a = to_f32(s);
+    }
+    sum += a;
+  }
+  const T* src = res != nullptr ? x_out + row * cols : xr;
+  const float mean = block_sum(sum, smem) / cols;
+  float sq = 0.f;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    const float d = to_f32(src[c]) - mean;
+    sq += d * d;
+  }
+  const float rstd = rsqrtf(block_sum(sq, smem) / cols + eps);
+  if (threadIdx.x == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    float g = w ? to_f32(w[c]) : 1.f;
+    float bb = b ? to_f32(b[c]) : 0.f;
+    y[row * cols + c] = from_f32<T>((to_f32(src[c]) - mean) * rstd * g + bb);
+  }
+}
+
+template <typename T, typename W, int VPT>
+__global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, const T* __restrict__ x,
+                                                  const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                  float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                  int64_t rows, int cols, const T* __restrict__ dres) {
+  constexpr int N = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  float dwacc[VPT][N], dbacc[VPT][N];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k)
+#pragma unroll
+    for (int j = 0; j < N; ++j) dwacc[k][j] = dbacc[k][j] = 0.f;
+
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + wid; row < rows;
+       row += static_cast<int64_t>(gridDim.x) * kRowsPerBlock) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[VPT][N], g[VPT][N];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int c = (k * 64 + lane) * N;
+      if (c < cols) {
+        Vec16<T> a = load16(x + row * cols + c);
+        Vec16<T> d = load16(dy + row * cols + c);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const float dyv = to_f32(d.v[j]);
+          xh[k][j] = (to_f32(a.v[j]) - mean) * rstd;
+          const float ww = w ? to_f32(w[c + j]) : 1.f;
+          g[k][j] = dyv * ww;
+          s1 += g[k][j];
+          s2 += g[k][j] * xh[k][j];
+          dwacc[k][j] += dyv * xh[k][j];
+          dbacc[k][j] += dyv;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+#pragma unroll
+    for (int k = 0; k < VPT; ++k) {
+      const int c = (k * 64 + lane) * N;
+      if (c < cols) {
+        Vec16<T> o;
+        Vec16<T> r;
+        if (dres != nullptr) r = load16(dres + row * cols + c);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          float v = rstd * (g[k][j] - s1 - xh[k][j] * s2);
+          if (dres != nullptr) v += to_f32(r.v[j]);
+          o.v[j] = from_f32<T>(v);
+        }
+        store16(dx + row * cols + c, o);
+      }
+    }
+  }
+  // combine the block's 4 waves through LDS (waves take turns: LDS = 2 x cols fp32),
+  // then write one partial row per block
+  extern __shared__ float lds[];  // [2][cols]
+  if (dw_part == nullptr) return;
+  for (int r = 0; r < kRowsPerBlock; ++r) {
+    if (wid == r) {
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int c = (k * 64 + lane) * N;
+        if (c < cols) {
+#pragma unroll
+          for (int j = 0; j < N; ++j) {
+            if (r == 0) {
+              lds[c + j] = dwacc[k][j];
+              lds[cols + c + j] = dbacc[k][j];
+            } else {
+              lds[c + j] += dwacc[k][j];
+              lds[cols + c + j] += dbacc[k][j];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    dw_part[static_cast<int64_t>(blockIdx.x) * cols + c] = lds[c];
+    if (db_part) db_part[static_cast<int64_t>(blockIdx.x) * cols + c] = lds[cols + c];
+  }
+}
+
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) ln_bwd_stream(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                     float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                     int64_t rows, int cols, const T* __restrict__ dres) {
+  // one block per row; dw/db partial per row (parts == rows) -- only used for odd shapes
+  __shared__ float smem[16];
+  const int64_t row = blockIdx.x;
+  const float mean = mean_in[row], rstd = rstd_in[row];
+  float s1 = 0.f, s2 = 0.f;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    const float dyv = to_f32(dy[row * cols + c]);
+    const float xh = (to_f32(x[row * cols + c]) - mean) * rstd;
+    const float gg = dyv * (w ? to_f32(w[c]) : 1.f);
+    s1 += gg;
+    s2 += gg * xh;
+    if (dw_part) dw_part[row * cols + c] = dyv * xh;
+    if (db_part) db_part[row * cols + c] = dyv;
+  }
+  s1 = block_sum(s1, smem) / cols;
+  s2 = block_sum(s2, smem) / cols;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    const float dyv = to_f32(dy[row * cols + c]);
+    const float xh = (to_f32(x[row * cols + c]) - mean) * rstd;
+    const float gg = dyv * (w ? to_f32(w[c]) : 1.f);
+    float v = rstd * (gg - s1 - xh * s2);
+    if (dres) v += to_f32(dres[row * cols + c]);
+    dx[row * cols + c] = from_f32<T>(v);
+  }
+}
+
+template <typename W>
+__global__ void __launch_bounds__(256) ln_bwd_reduce_kernel(const float* __restrict__ dw_part,
+                                                            const float* __restrict__ db_part, W* __restrict__ dw,
+                                                            W* __restrict__ db, int parts, int64_t cols) {
+  // 256 threads = 64 columns x 4 part-lanes; coalesced over columns.
+  __shared__ float sw[4][64], sb[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + cl;
+  float a = 0.f, b = 0.f;
+  if (c < cols) {
+    for (int p = pl; p < parts; p += 4) {
+      a += dw_part[p * cols + c];
+      if (db_part) b += db_part[p * cols + c];
+    }
+  }
+  sw[pl][cl] = a;
+  sb[pl][cl] = b;
+  __syncthreads();
+  if (pl == 0 && c < cols) {
+    a = sw[0][cl] + sw[1][cl] + sw[2][cl] + sw[3][cl];
+    b = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
+    if (dw) dw[c] = from_f32<W>(a);
+    if (db) db[c] = from_f32<W>(b);
+  }
+}
+
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) ln_apply_stats(const T* __restrict__ x, const W* __restrict__ w,
+                                                      const W* __restrict__ b, const float* __restrict__ mean,
+                                                      const float* __restrict__ var, T* __restrict__ y,
+                                                      float* __restrict__ rstd_out, int64_t rows, int cols,
+                                                      float eps) {
+  const int64_t row = blockIdx.x;
+  const float m = mean[row];
+  const float r = rsqrtf(var[row] + eps);
+  if (threadIdx.x == 0 && rstd_out) rstd_out[row] = r;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    const float g = w ? to_f32(w[c]) : 1.f;
+    const float bb = b ? to_f32(b[c]) : 0.f;
+    y[row * cols + c] = from_f32<T>((to_f32(x[row * cols + c]) - m) * r * g + bb);
+  }
+}
+
+template <typename T>
+bool vec_ok(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+}
+
+}  // namespace
+
+int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
+                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s) {
+  if (rows <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    SMPK_DISPATCH(wdt, W, {
+      constexpr int N = Vec16<T>::N;
+      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(y) &&
+                           (residual == nullptr || (vec_ok<T>(residual) && vec_ok<T>(x_out)));
+      const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
+      const int grid = static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock);
+      const T* xx = static_cast<const T*>(x);
+      const T* rr = static_cast<const T*>(residual);
+      T* xo = static_cast<T*>(x_out);
+      const W* ww = static_cast<const W*>(w);
+      const W* bb = static_cast<const W*>(b);
+      T* yy = static_cast<T*>(y);
+      const int c = static_cast<int>(cols);
+      if (aligned && vpt <= 1) {
+        ln_fwd_reg<T, W, 1><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+      } else if (aligned && vpt <= 2) {
+        ln_fwd_reg<T, W, 2><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+      } else if (aligned && vpt <= 4) {
+        ln_fwd_reg<T, W, 4><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+      } else if (aligned && vpt <= 8) {
+        ln_fwd_reg<T, W, 8><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+      } else {
+        ln_fwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+      }
+    });
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+// Number of partial rows the backward will produce for (rows, cols): callers size
+// dw_part/db_part as [parts, cols] fp32.
+static inline int ln_bwd_parts(int64_t rows, int64_t cols, bool reg_path) {
+  if (!reg_path) return static_cast<int>(rows);
+  int64_t blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
+  if (blocks > 1024) blocks = 1024;
+  return static_cast<int>(blocks);
+}
+
+int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean, const float* rstd,
+                  void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols, int part_rows,
+                  const void* dres, hipStream_t s) {
+  if (rows <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    SMPK_DISPATCH(wdt, W, {
+      constexpr int N = Vec16<T>::N;
+      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(dy) && vec_ok<T>(dx) &&
+                           (dres == nullptr || vec_ok<T>(dres));
+      const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
+      const bool reg = aligned && vpt <= 8;
+      const int parts = ln_bwd_parts(rows, cols, reg);
+      if (part_rows != parts) return -2;  // caller must size partials with layernorm_bwd_parts
+      const T* dyy = static_cast<const T*>(dy);
+      const T* xx = static_cast<const T*>(x);
+      const W* ww = static_cast<const W*>(w);
+      T* dxx = static_cast<T*>(dx);
+      const T* dr = static_cast<const T*>(dres);
+      const int c = static_cast<int>(cols);
+      const size_t lds = static_cast<size_t>(2) * cols * sizeof(float);
+      if (reg && vpt <= 1) {
+        ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+      } else if (reg && vpt <= 2) {
+        ln_bwd_reg<T, W, 2><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+      } else if (reg && vpt <= 4) {
+        ln_bwd_reg<T, W, 4><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+      } else if (reg) {
+        ln_bwd_reg<T, W, 8><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+      } else {
+        ln_bwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part,
+                                                                   rows, c, dr);
+      }
+    });
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
+                         int64_t cols, hipStream_t s) {
+  SMPK_DISPATCH(wdt, W, {
+    ln_bwd_reduce_kernel<W><<<static_cast<int>((cols + 63) / 64), 256, 0, s>>>(
+        dw_part, db_part, static_cast<W*>(dw), static_cast<W*>(db), parts, cols);
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const void* b, const float* mean,
+                          const float* var, void* y, float* rstd, int64_t rows, int64_t cols, float eps,
+                          hipStream_t s) {
+  if (rows <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    SMPK_DISPATCH(wdt, W, {
+      ln_apply_stats<T, W><<<static_cast<int>(rows), 256, 0, s>>>(
+          static_cast<const T*>(x), static_cast<const W*>(w), static_cast<const W*>(b), mean, var, static_cast<T*>(y),
+          rstd, rows, static_cast<int>(cols), eps);
+    });
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int layernorm_local_sums(int, const void*, const float*, hipStream_t) { return -1; }
+
+// exported helper so bindings can size partial buffers
+int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned) {
+  const int N = dt == F32 ? 4 : 8;
+  const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
+  return ln_bwd_parts(rows, cols, aligned && (cols % N == 0) && vpt <= 8);
+}
+
+}  // namespace smpk

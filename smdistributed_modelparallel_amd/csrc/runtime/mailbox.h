@@ -1,0 +1,106 @@
+// Control-plane transport of the runtime: a full-mesh TCP mailbox.
+//
+// Replaces the reference's MPI object channel + listener thread (N1b/N1d in SURVEY §2.1;
+// call sites smp/backend/collectives.py:237-324 and smp/torch/server_comm.py:60-348).
+//
+// Every message carries (src, transaction id, channel). Channel USER messages are
+// matched by (src, tid) against explicit receives; channel SERVER messages are
+// unsolicited and go to a FIFO the pipeline server drains (the reference's
+// "server=True" routing).  One receiver thread multiplexes all peer sockets with
+// poll(2); one sender thread per peer drains an outgoing queue so a Python send never
+// blocks the caller on a slow peer (async send semantics of smp_async_send).
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <utility>
+#include <vector>
+
+namespace smprt {
+
+enum Channel : uint8_t { USER = 0, SERVER = 1 };
+
+struct Message {
+  int32_t src = -1;
+  int64_t tid = 0;
+  uint8_t channel = USER;
+  std::string payload;
+};
+
+struct TransportStats {
+  uint64_t msgs_sent = 0, msgs_recv = 0, bytes_sent = 0, bytes_recv = 0;
+};
+
+class Mailbox {
+ public:
+  Mailbox(int rank, int world);
+  ~Mailbox();
+
+  // Bind a listening socket on `host` (port chosen by the kernel); returns the port.
+  int listen(const std::string& host);
+  // Connect the full mesh. `hosts`/`ports` are indexed by rank.
+  void connect(const std::vector<std::string>& hosts, const std::vector<int>& ports,
+               double timeout_s);
+
+  void send(int dst, int64_t tid, uint8_t channel, std::string payload);
+  // Multi-destination send of one payload (smp_async_bcast).
+  void broadcast(const std::vector<int>& dsts, int64_t tid, uint8_t channel,
+                 const std::string& payload);
+
+  // Matched receive. timeout_s < 0 waits forever. Throws on timeout/shutdown.
+  std::string recv(int src, int64_t tid, double timeout_s);
+  bool poll(int src, int64_t tid);
+
+  // Unsolicited (server channel) messages.
+  bool has_server_message();
+  // Returns false on timeout.
+  bool next_server_message(Message* out, double timeout_s);
+
+  // Wait until every queued outgoing message has been written to its socket.
+  void flush();
+  void shutdown();
+  TransportStats stats();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+ private:
+  struct Peer {
+    int fd = -1;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::shared_ptr<const std::string>> outq;  // framed messages
+    std::thread sender;
+    bool writing = false;
+  };
+
+  void recv_loop();
+  void send_loop(int peer);
+  void deliver(Message&& m);
+  std::shared_ptr<const std::string> frame(int64_t tid, uint8_t channel, const std::string& p);
+
+  int rank_, world_;
+  int listen_fd_ = -1;
+  std::vector<std::unique_ptr<Peer>> peers_;
+  std::thread receiver_;
+  std::atomic<bool> stop_{false};
+  int wake_pipe_[2] = {-1, -1};
+
+  std::mutex in_mu_;
+  std::condition_variable in_cv_;
+  std::map<std::pair<int, int64_t>, std::deque<std::string>> matched_;
+  std::deque<Message> server_q_;
+  std::string error_;
+
+  std::mutex stats_mu_;
+  TransportStats stats_;
+};
+
+}  // namespace smprt

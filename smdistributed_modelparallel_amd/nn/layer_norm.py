@@ -1,0 +1,118 @@
+"""LayerNorm modules.
+
+* ``FusedLayerNorm`` / ``MixedFusedLayerNorm``: the HIP fused LayerNorm (apex replacement,
+  reference `smp/torch/nn/layer_norm.py:140-152`).
+* ``DistributedLayerNorm``: LayerNorm over a hidden dimension sharded across the TP group
+  (``optimize="memory"`` layout; reference `layer_norm.py:24-135`): forward all-reduces the
+  per-row mean and variance (fp32), backward all-reduces the two per-row partial sums.
+"""
+import numbers
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops.layernorm import add_layer_norm, layer_norm
+from .utils import get_local_channels, get_start_pos_for_slicing, tp_group, tp_size
+
+
+class FusedLayerNorm(nn.Module):
+    def __init__(self, normalized_shape, eps=1e-5, elementwise_affine=True, device=None, dtype=None):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.normalized_shape = tuple(normalized_shape)
+        self.eps = eps
+        self.elementwise_affine = elementwise_affine
+        n = 1
+        for s in self.normalized_shape:
+            n *= s
+        if elementwise_affine:
+            self.weight = nn.Parameter(torch.ones(n, device=device, dtype=dtype))
+            self.bias = nn.Parameter(torch.zeros(n, device=device, dtype=dtype))
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        shape = x.shape
+        y = layer_norm(x.reshape(-1, self.weight.numel() if self.weight is not None else shape[-1]), self.weight,
+                       self.bias, self.eps)
+        return y.view(shape)
+
+    def forward_add(self, x, residual):
+        """(LN(x + residual), x + residual) in one kernel."""
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
+
+    def extra_repr(self):
+        return f"{self.normalized_shape}, eps={self.eps}, elementwise_affine={self.elementwise_affine}"
+
+
+class MixedFusedLayerNorm(FusedLayerNorm):
+    """fp32 input with low-precision affine params; output in the param dtype."""
+
+    def forward(self, x):
+        y = super().forward(x)
+        return y.to(self.weight.dtype) if self.weight is not None else y
+
+
+class _DistLNStats(torch.autograd.Function):
+    """Global mean/var over a TP-sharded last dim (fp32), with the matching backward."""
+
+    @staticmethod
+    def forward(ctx, x, full_dim, group):
+        xf = x.float()
+        s1 = xf.sum(-1, keepdim=True)
+        if group is not None:
+            dist.all_reduce(s1, group=group)
+        mean = s1 / full_dim
+        s2 = (xf - mean).pow(2).sum(-1, keepdim=True)
+        if group is not None:
+            dist.all_reduce(s2, group=group)
+        var = s2 / full_dim
+        ctx.save_for_backward(xf, mean)
+        ctx.full_dim, ctx.group = full_dim, group
+        return mean, var
+
+    @staticmethod
+    def backward(ctx, gmean, gvar):
+        xf, mean = ctx.saved_tensors
+        n = ctx.full_dim
+        if ctx.group is not None:
+            # every rank's local y depends on the shared statistics: sum their grads
+            g = torch.cat([gmean, gvar], dim=-1).contiguous()
+            dist.all_reduce(g, group=ctx.group)
+            gmean, gvar = g[..., :1], g[..., 1:]
+        # d mean / dx = 1/n ; d var / dx = 2 (x - mean) / n  (the mean term sums to zero)
+        gx = gmean / n + gvar * 2.0 * (xf - mean) / n
+        return gx, None, None
+
+
+class DistributedLayerNorm(nn.Module):
+    """LayerNorm whose normalised dim is split across the TP group (uneven splits ok)."""
+
+    def __init__(self, normalized_shape, eps=1e-5, elementwise_affine=True, device=None, dtype=None):
+        super().__init__()
+        if isinstance(normalized_shape, numbers.Integral):
+            normalized_shape = (normalized_shape,)
+        self.full_dim = normalized_shape[-1]
+        self.local_dim = get_local_channels(self.full_dim)
+        self.start = get_start_pos_for_slicing(self.full_dim)
+        self.eps = eps
+        self.elementwise_affine = elementwise_affine
+        if elementwise_affine:
+            self.weight = nn.Parameter(torch.ones(self.local_dim, device=device, dtype=dtype))
+            self.bias = nn.Parameter(torch.zeros(self.local_dim, device=device, dtype=dtype))
+            self.weight._smp_scaled_batch = True
+            self.bias._smp_scaled_batch = True
+        else:
+            self.register_parameter("weight", None)
+            self.register_parameter("bias", None)
+
+    def forward(self, x):
+        group = tp_group() if tp_size() > 1 else None
+        mean, var = _DistLNStats.apply(x, self.full_dim, group)
+        y = (x.float() - mean) * torch.rsqrt(var + self.eps)
+        if self.weight is not None:
+            y = y * self.weight.float() + self.bias.float()
+        return y.to(x.dtype)

@@ -1,0 +1,578 @@
+"""Tensor-parallel transformer family: ``DistributedTransformerLMHead``,
+``DistributedTransformer``, ``DistributedTransformerLayer``, ``DistributedAttentionLayer``,
+``DistributedTransformerOutputLayer``.
+
+Reference parity (`smp/torch/nn/transformer.py:184-1835`): same constructor keys and
+defaults (``_KEYS``), scaled-batch TP semantics (each tp_rank owns a different local batch;
+the first layer of a stage all-gathers the batch over the TP group, head/channel-parallel
+math runs on the TP-group batch, the last layer of a stage narrows back), Megatron-style
+column/row parallel GEMMs with forward/backward all-reduces, bias of row-parallel layers
+only on tp_rank 0, uneven head splits, pre/post/single-pre LayerNorm, GPT-J/NeoX parallel
+attention output, rotary embeddings (GPT-J interleaved / NeoX half), GPT-Neo local
+attention windows, query-key layer scaling / ``scale_attn_by_layer_idx``, fp32 attention,
+fused bias-GeLU, vocab-parallel embedding + cross entropy, tied LM head, ``prescaled_batch``
+sequence sharding at the model ends.
+
+MI355X choices:
+* Q, K and V live in ONE fused ``[3 * local_heads * head_dim, hidden]`` weight so the
+  projection is a single large hipBLASLt GEMM; its output is consumed in
+  ``[b, s, 3, heads, d]`` layout by the attention kernel without a permute copy.
+* attention is the flash-style HIP kernel (no ``[s, s]`` scores, no 2048 cap);
+* LayerNorm, residual-add+LayerNorm, bias+GeLU and the LM-head cross entropy are fused
+  HIP kernels (see ``ops/``).
+"""
+import math
+import warnings
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..backend.exceptions import SMPInvalidArgumentError
+from ..ops.attention import attention as attention_op
+from ..ops.cross_entropy import cross_entropy
+from ..ops.gelu import bias_gelu
+from ..ops.rope import apply_rotary
+from ..torch.state_mod import state
+from .layer_norm import FusedLayerNorm
+from .utils import (
+    allgather_for_tp,
+    bwd_allreduce_for_tp,
+    fwd_allreduce_for_tp,
+    get_local_channels,
+    get_merge_shapes,
+    init_weight_,
+    mark_scaled_batch,
+    mark_tp,
+    narrow_for_tp,
+    shard_sequence,
+    tp_group,
+    tp_rank,
+    tp_size,
+    unshard_sequence,
+)
+
+_LAYER_KEYS = OrderedDict(
+    [
+        ("num_attention_heads", 32),
+        ("attention_head_size", 32),
+        ("hidden_size", 1024),
+        ("intermediate_size", 4096),
+        ("attention_dropout_prob", 0.1),
+        ("hidden_dropout_prob", 0.1),
+        ("activation", "gelu"),
+        ("layernorm_epsilon", 1e-5),
+        ("initializer_range", 0.02),
+        ("use_normal_initialization", False),
+        ("causal_mask_size", None),
+        ("add_cross_attention", False),
+        ("pre_layernorm", False),
+        ("post_layernorm", True),
+        ("attention_in_fp32", False),
+        ("query_key_layer_scaling", False),
+        ("fp32_residual_addition", False),
+        ("fused_softmax", True),
+        ("fused_bias_gelu", False),
+        ("_scale_qkv_fan_out", False),
+        ("_precision_test", False),
+        ("rotary_dim", None),
+        ("rotary_emb_base", None),
+        ("gpt_neox_type_rotary", False),
+        ("parallel_attn_output", False),
+        ("use_qkv_bias", True),
+        ("use_attn_dense_bias", True),
+        ("window_size", None),
+        ("single_pre_layernorm", False),
+        ("scale_attention_scores", True),
+        ("scale_attn_by_layer_idx", False),
+        ("mask_value", -1e4),
+    ]
+)
+
+
+def parse_args(obj, args, kwargs, keys):
+    cfg = OrderedDict()
+    names = list(keys.keys())
+    if len(args) > len(names):
+        raise SMPInvalidArgumentError(f"too many positional arguments for {type(obj).__name__}")
+    for i, a in enumerate(args):
+        cfg[names[i]] = a
+    for k, v in kwargs.items():
+        if k not in keys:
+            raise SMPInvalidArgumentError(f"unknown argument {k} for {type(obj).__name__}")
+        if k in cfg:
+            raise SMPInvalidArgumentError(f"duplicate argument {k}")
+        cfg[k] = v
+    for k, d in keys.items():
+        if k not in cfg:
+            cfg[k] = d
+        setattr(obj, k, cfg[k])
+    return cfg
+
+
+def _subset(cfg, keys):
+    return {k: cfg[k] for k in keys if k in cfg}
+
+
+def _param_dtype():
+    if state.initialized and state.cfg._fp16_param_init:
+        return torch.float16
+    return None
+
+
+class DistributedModule(nn.Module):
+    """Base of every smp.nn distributed module (reference `nn/dist_module.py:5-32`)."""
+
+    def can_distribute(self, *args, **kwargs):
+        return True
+
+    def can_shard_activation_offloading(self):
+        return True
+
+
+class _Dropout(nn.Module):
+    def __init__(self, p):
+        super().__init__()
+        self.p = p
+
+    def forward(self, x):
+        if self.p == 0.0 or not self.training:
+            return x
+        return F.dropout(x, self.p, True)
+
+
+def _activation(x, kind, bias=None, fused=False):
+    if kind == "gelu":
+        return bias_gelu(x, bias)
+    if bias is not None:
+        x = x + bias
+    if kind == "relu":
+        return F.relu(x)
+    if kind == "gelu_exact":
+        return F.gelu(x)
+    raise SMPInvalidArgumentError(f"unsupported activation {kind}")
+
+
+# =========================================================== attention layer
+class DistributedAttentionLayer(DistributedModule):
+    _KEYS = OrderedDict(
+        [(k, v) for k, v in _LAYER_KEYS.items()
+         if k not in ("intermediate_size", "activation", "fused_bias_gelu", "parallel_attn_output",
+                      "single_pre_layernorm", "add_cross_attention")]
+        + [("cross_attention", False)]
+    )
+
+    def __init__(self, *args, layer_idx=0, **kwargs):
+        super().__init__()
+        parse_args(self, args, kwargs, self._KEYS)
+        self.layer_idx = layer_idx
+        self.local_heads = get_local_channels(self.num_attention_heads)
+        lh, d, h = self.local_heads, self.attention_head_size, self.hidden_size
+        self.local_attn = lh * d
+        self.full_attn = self.num_attention_heads * d
+        dtype = _param_dtype()
+        n_proj = 1 if self.cross_attention else 3
+        self.qkv_weight = nn.Parameter(torch.empty(n_proj * lh * d, h, dtype=dtype))
+        self.qkv_bias = nn.Parameter(torch.zeros(n_proj * lh * d, dtype=dtype)) if self.use_qkv_bias else None
+        if self.cross_attention:
+            self.kv_weight = nn.Parameter(torch.empty(2 * lh * d, h, dtype=dtype))
+            self.kv_bias = nn.Parameter(torch.zeros(2 * lh * d, dtype=dtype)) if self.use_qkv_bias else None
+        self.dense_weight = nn.Parameter(torch.empty(h, lh * d, dtype=dtype))
+        self.dense_bias = (
+            nn.Parameter(torch.zeros(h, dtype=dtype)) if (self.use_attn_dense_bias and tp_rank() == 0) else None
+        )
+        if self.pre_layernorm:
+            self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+        if self.post_layernorm:
+            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+        self.dropout = _Dropout(self.hidden_dropout_prob)
+        self.input_layer = True
+        self.output_layer = True
+        self.reset_parameters()
+        for p in self.parameters():
+            mark_scaled_batch(p)
+        mark_tp(self.qkv_weight, 0, n_proj)
+        if self.qkv_bias is not None:
+            mark_tp(self.qkv_bias, 0, n_proj)
+        if self.cross_attention:
+            mark_tp(self.kv_weight, 0, 2)
+            if self.kv_bias is not None:
+                mark_tp(self.kv_bias, 0, 2)
+        mark_tp(self.dense_weight, 1)
+        if self.dense_bias is not None:
+            mark_tp(self.dense_bias, None, rank0_only=True)
+
+    def reset_parameters(self):
+        r, normal = self.initializer_range, self.use_normal_initialization
+        h = self.hidden_size
+        fan_out_qkv = self.full_attn * (3 if self._scale_qkv_fan_out else 1)
+        init_weight_(self.qkv_weight, h, fan_out_qkv, r, normal)
+        if self.cross_attention:
+            init_weight_(self.kv_weight, h, self.full_attn, r, normal)
+        init_weight_(self.dense_weight, self.full_attn, h, r, normal)
+        with torch.no_grad():
+            for b in (self.qkv_bias, getattr(self, "kv_bias", None), self.dense_bias):
+                if b is not None:
+                    b.zero_()
+
+    # ------------------------------------------------------------------ core
+    def _scale(self):
+        s = 1.0 / math.sqrt(self.attention_head_size) if self.scale_attention_scores else 1.0
+        if self.scale_attn_by_layer_idx:
+            s = s / float(self.layer_idx + 1)
+        return s
+
+    def core(self, a, mask=None, cross_states=None, cross_mask=None):
+        """a: [B, s, h] (already normalised). Returns the dense output after the TP
+        all-reduce (bias included), [B, s, h]."""
+        a = bwd_allreduce_for_tp(a)
+        B, s, _ = a.shape
+        lh, d = self.local_heads, self.attention_head_size
+        if self.cross_attention:
+            q = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, lh, d)
+            c = bwd_allreduce_for_tp(cross_states)
+            kv = F.linear(c, self.kv_weight, self.kv_bias).view(B, c.shape[1], 2, lh, d)
+            k, v = kv[:, :, 0], kv[:, :, 1]
+            causal, mask = False, cross_mask
+        else:
+            qkv = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
+            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+            causal = self.causal_mask_size is not None
+        if self.rotary_dim:
+            base = self.rotary_emb_base or 10000
+            q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
+            k = apply_rotary(k, self.rotary_dim, base, self.gpt_neox_type_rotary)
+        ctx = attention_op(
+            q, k, v, causal=causal, mask=mask, scale=self._scale(),
+            dropout_p=self.attention_dropout_prob, window=self.window_size, training=self.training,
+            attention_in_fp32=self.attention_in_fp32,
+            use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
+        )
+        ctx = ctx.reshape(B, s, lh * d)
+        out = F.linear(ctx, self.dense_weight, self.dense_bias)
+        return fwd_allreduce_for_tp(out)
+
+    def forward(self, inputs):
+        if self.cross_attention:
+            hidden, mask, cross_states, cross_mask = inputs
+        else:
+            hidden, mask = inputs[0], inputs[1]
+            cross_states = cross_mask = None
+        if tp_size() > 1 and self.input_layer and not _prescaled():
+            hidden = allgather_for_tp(hidden, 0)
+            mask = _gather_mask(mask)
+        a = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
+        out = self.dropout(self.core(a, mask, cross_states, cross_mask)) + hidden
+        if self.post_layernorm:
+            out = self.layernorm(out)
+        if tp_size() > 1 and self.output_layer and not _prescaled():
+            out = narrow_for_tp(out, 0)
+        return (out,) + tuple(inputs[1:])
+
+
+def _prescaled():
+    return state.initialized and state.cfg.prescaled_batch
+
+
+def _gather_mask(mask):
+    if mask is None or not torch.is_tensor(mask) or mask.dim() == 0 or mask.shape[0] == 1:
+        return mask
+    return allgather_for_tp(mask, 0)
+
+
+# ============================================================== output (MLP)
+class DistributedTransformerOutputLayer(DistributedModule):
+    _KEYS = OrderedDict(
+        [(k, _LAYER_KEYS[k]) for k in ("hidden_size", "intermediate_size", "hidden_dropout_prob", "activation",
+                                       "layernorm_epsilon", "initializer_range", "use_normal_initialization",
+                                       "pre_layernorm", "post_layernorm", "fp32_residual_addition",
+                                       "fused_bias_gelu", "_precision_test")]
+    )
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        parse_args(self, args, kwargs, self._KEYS)
+        self.local_inter = get_local_channels(self.intermediate_size)
+        h, li = self.hidden_size, self.local_inter
+        dtype = _param_dtype()
+        self.dense1_weight = nn.Parameter(torch.empty(li, h, dtype=dtype))
+        self.dense1_bias = nn.Parameter(torch.zeros(li, dtype=dtype))
+        self.dense2_weight = nn.Parameter(torch.empty(h, li, dtype=dtype))
+        self.dense2_bias = nn.Parameter(torch.zeros(h, dtype=dtype)) if tp_rank() == 0 else None
+        if self.pre_layernorm:
+            self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+        if self.post_layernorm:
+            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+        self.dropout = _Dropout(self.hidden_dropout_prob)
+        self.input_layer = True
+        self.output_layer = True
+        self.reset_parameters()
+        for p in self.parameters():
+            mark_scaled_batch(p)
+        mark_tp(self.dense1_weight, 0)
+        mark_tp(self.dense1_bias, 0)
+        mark_tp(self.dense2_weight, 1)
+        if self.dense2_bias is not None:
+            mark_tp(self.dense2_bias, None, rank0_only=True)
+
+    def reset_parameters(self):
+        r, normal = self.initializer_range, self.use_normal_initialization
+        init_weight_(self.dense1_weight, self.hidden_size, self.intermediate_size, r, normal)
+        init_weight_(self.dense2_weight, self.intermediate_size, self.hidden_size, r, normal)
+        with torch.no_grad():
+            self.dense1_bias.zero_()
+            if self.dense2_bias is not None:
+                self.dense2_bias.zero_()
+
+    def core(self, m):
+        m = bwd_allreduce_for_tp(m)
+        x = F.linear(m, self.dense1_weight)
+        x = _activation(x, self.activation, self.dense1_bias)
+        out = F.linear(x, self.dense2_weight, self.dense2_bias)
+        return fwd_allreduce_for_tp(out)
+
+    def forward(self, hidden):
+        if tp_size() > 1 and self.input_layer and not _prescaled():
+            hidden = allgather_for_tp(hidden, 0)
+        m = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
+        out = self.dropout(self.core(m)) + hidden
+        if self.post_layernorm:
+            out = self.layernorm(out)
+        if tp_size() > 1 and self.output_layer and not _prescaled():
+            out = narrow_for_tp(out, 0)
+        return out
+
+
+# ========================================================== transformer layer
+class DistributedTransformerLayer(DistributedModule):
+    _KEYS = _LAYER_KEYS
+
+    def __init__(self, *args, layer_idx=0, **kwargs):
+        super().__init__()
+        cfg = parse_args(self, args, kwargs, self._KEYS)
+        if not (self.pre_layernorm or self.post_layernorm or self.single_pre_layernorm):
+            raise SMPInvalidArgumentError("one of pre_layernorm / post_layernorm / single_pre_layernorm must be True")
+        self.layer_idx = layer_idx
+        attn_cfg = {k: cfg[k] for k in DistributedAttentionLayer._KEYS if k in cfg}
+        out_cfg = {k: cfg[k] for k in DistributedTransformerOutputLayer._KEYS if k in cfg}
+        if self.single_pre_layernorm:
+            attn_cfg["pre_layernorm"] = True
+            out_cfg["pre_layernorm"] = False
+        if self.parallel_attn_output:
+            # GPT-J / NeoX: h + attn(ln1(h)) + mlp(ln2(h))  (single_pre_layernorm: shared ln)
+            attn_cfg["post_layernorm"] = False
+            out_cfg["post_layernorm"] = False
+        self.attention = DistributedAttentionLayer(layer_idx=layer_idx, **attn_cfg)
+        if self.add_cross_attention:
+            cross_cfg = dict(attn_cfg, cross_attention=True, causal_mask_size=None, rotary_dim=None)
+            self.cross_attention = DistributedAttentionLayer(layer_idx=layer_idx, **cross_cfg)
+        self.output = DistributedTransformerOutputLayer(**out_cfg)
+        self.input_layer = True
+        self.output_layer = True
+
+    def forward(self, inputs):
+        hidden, mask = inputs[0], inputs[1]
+        if tp_size() > 1 and self.input_layer and not _prescaled():
+            hidden = allgather_for_tp(hidden, 0)
+            mask = _gather_mask(mask)
+        at, out = self.attention, self.output
+        if self.parallel_attn_output:
+            a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
+            attn = at.core(a, mask)
+            m = a if self.single_pre_layernorm else (out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden)
+            mlp = out.core(m)
+            hidden = hidden + at.dropout(attn) + out.dropout(mlp)
+        else:
+            a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
+            attn = at.dropout(at.core(a, mask))
+            if at.post_layernorm:
+                hidden = at.layernorm(attn + hidden)
+                m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
+            elif out.pre_layernorm and hasattr(out.pre_layernorm_module, "forward_add"):
+                # fused: residual add + LayerNorm in one HIP kernel
+                m, hidden = out.pre_layernorm_module.forward_add(attn, hidden)
+            else:
+                hidden = attn + hidden
+                m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
+            if self.add_cross_attention:
+                ca = self.cross_attention
+                c_in = ca.pre_layernorm_module(hidden) if ca.pre_layernorm else hidden
+                hidden = ca.dropout(ca.core(c_in, None, inputs[2], inputs[3])) + hidden
+                if ca.post_layernorm:
+                    hidden = ca.layernorm(hidden)
+                m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
+            hidden = out.dropout(out.core(m)) + hidden
+            if out.post_layernorm:
+                hidden = out.layernorm(hidden)
+        if tp_size() > 1 and self.output_layer and not _prescaled():
+            hidden = narrow_for_tp(hidden, 0)
+        return (hidden,) + tuple(inputs[1:])
+
+
+# ================================================================ transformer
+class DistributedTransformer(DistributedModule):
+    _KEYS = OrderedDict([("num_layers", 12)] + list(_LAYER_KEYS.items()) + [("attention_layers_type", None),
+                                                                         ("_output_full_batch", False)])
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        cfg = parse_args(self, args, kwargs, self._KEYS)
+        layer_cfg = {k: cfg[k] for k in _LAYER_KEYS}
+        layers = []
+        for i in range(self.num_layers):
+            lc = dict(layer_cfg)
+            if self.attention_layers_type is not None:
+                kind = self.attention_layers_type[i]
+                lc["window_size"] = self.window_size if kind == "local" else None
+            else:
+                lc["window_size"] = self.window_size
+            layers.append(DistributedTransformerLayer(layer_idx=i, **lc))
+        self.seq_layers = nn.Sequential(*layers)
+        self.update_layer_boundaries()
+
+    def update_layer_boundaries(self, partition_of=None):
+        """Mark the first/last layer of every pipeline stage (where the TP batch
+        all-gather / narrow happen). `partition_of(module)` gives the stage."""
+        layers = list(self.seq_layers)
+        for i, layer in enumerate(layers):
+            p = partition_of(layer) if partition_of else 0
+            prev = partition_of(layers[i - 1]) if (partition_of and i > 0) else p
+            nxt = partition_of(layers[i + 1]) if (partition_of and i + 1 < len(layers)) else p
+            layer.input_layer = i == 0 or prev != p
+            layer.output_layer = (i == len(layers) - 1 and not self._output_full_batch) or nxt != p
+            for sub in (layer.attention, layer.output):
+                sub.input_layer = False
+                sub.output_layer = False
+
+    def forward(self, inputs):
+        return self.seq_layers(inputs)
+
+
+# ================================================================ LM head model
+class DistributedTransformerLMHead(DistributedModule):
+    _KEYS = OrderedDict(
+        [("num_layers", 12)]
+        + [(k, v) for k, v in _LAYER_KEYS.items() if k != "mask_value"]
+        + [
+            ("vocab_size", 30522),
+            ("num_positions", 1024),
+            ("embedding_dropout_prob", 0.1),
+            ("mask_value", -1e4),
+            ("num_token_types", 0),
+            ("add_lm_head", True),
+            ("distribute_embedding", False),
+            ("use_positional_embedding", True),
+            ("use_lm_head_bias", False),
+            ("attention_layers_type", None),
+            ("final_layernorm", False),
+            ("tie_input_output_embedding", True),
+        ]
+    )
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        cfg = parse_args(self, args, kwargs, self._KEYS)
+        if not (self.pre_layernorm or self.post_layernorm or self.single_pre_layernorm):
+            raise SMPInvalidArgumentError("one of pre_layernorm / post_layernorm / single_pre_layernorm must be True")
+        if self.causal_mask_size is not None and self.num_positions > self.causal_mask_size:
+            raise SMPInvalidArgumentError("causal_mask_size must be >= num_positions")
+        if self.distribute_embedding and self.parallel_attn_output:
+            warnings.warn("distribute_embedding is not supported with parallel_attn_output; disabling it")
+            self.distribute_embedding = False
+        dtype = _param_dtype()
+        h = self.hidden_size
+        if self.distribute_embedding:
+            from .embedding import DistributedEmbedding
+
+            self.word_embedding = DistributedEmbedding(self.vocab_size, h, initializer_range=self.initializer_range,
+                                                       vocab_parallel=True)
+        else:
+            self.word_embedding = nn.Embedding(self.vocab_size, h, dtype=dtype)
+            with torch.no_grad():
+                self.word_embedding.weight.normal_(0.0, self.initializer_range)
+        if self.use_positional_embedding:
+            self.position_embedding = nn.Embedding(self.num_positions, h, dtype=dtype)
+            with torch.no_grad():
+                self.position_embedding.weight.normal_(0.0, self.initializer_range)
+        if self.num_token_types > 0:
+            self.token_type_embedding = nn.Embedding(self.num_token_types, h, dtype=dtype)
+        self.dropout = _Dropout(self.embedding_dropout_prob)
+        tcfg = {k: cfg[k] for k in DistributedTransformer._KEYS if k in cfg}
+        tcfg["_output_full_batch"] = self.distribute_embedding
+        self.transformer = DistributedTransformer(**tcfg)
+        if self.final_layernorm:
+            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+        if self.add_lm_head:
+            if self.distribute_embedding:
+                self.lm_head_weight_local = None  # tied to the vocab-parallel embedding shard
+            else:
+                self.lm_head = nn.Linear(h, self.vocab_size, bias=self.use_lm_head_bias, dtype=dtype)
+                if self.tie_input_output_embedding:
+                    self.lm_head.weight = self.word_embedding.weight
+
+    def forward(self, inputs):
+        if self.add_cross_attention:
+            input_ids, attention_mask, token_type_ids, position_ids, cross_states, cross_mask, labels = inputs
+        else:
+            input_ids, attention_mask, token_type_ids, position_ids, labels = inputs
+            cross_states = cross_mask = None
+        B, s = input_ids.shape[0], input_ids.shape[1]
+        device = input_ids.device
+        position_ids = torch.arange(0, s, dtype=torch.long, device=device).unsqueeze(0).expand(B, -1)
+        mask = None
+        if self.causal_mask_size is None and attention_mask is not None:
+            mask = (attention_mask.view(B, -1) == 0).view(B, 1, 1, -1).expand(B, 1, s, s)
+
+        prescaled = _prescaled() and tp_size() > 1
+        if prescaled and not self.distribute_embedding:
+            input_ids, position_ids, token_type_ids = shard_sequence(input_ids, position_ids, token_type_ids,
+                                                                     bwd_allgather=False)
+        hidden = self.word_embedding(input_ids)
+        if self.use_positional_embedding:
+            hidden = hidden + self.position_embedding(position_ids)
+        if token_type_ids is not None:
+            if self.num_token_types <= 0:
+                raise SMPInvalidArgumentError("token_type_ids provided but num_token_types == 0")
+            hidden = hidden + self.token_type_embedding(token_type_ids)
+        with state.fork_tp_rng() if prescaled else _nullctx():
+            hidden = self.dropout(hidden)
+        if prescaled and not self.distribute_embedding:
+            (hidden,) = unshard_sequence(s, hidden)
+
+        tx_in = (hidden, mask, cross_states, cross_mask) if self.add_cross_attention else (hidden, mask)
+        hidden = self.transformer(tx_in)[0]
+        if self.final_layernorm:
+            hidden = self.layernorm(hidden)
+
+        if self.distribute_embedding:
+            hidden = bwd_allreduce_for_tp(hidden)
+            logits = F.linear(hidden, self.word_embedding.weight)
+            if labels is None:
+                return self.word_embedding.gather_vocab(logits)
+            if not _prescaled():
+                labels = allgather_for_tp(labels, 0)
+            shift_logits = logits[..., :-1, :]
+            shift_labels = labels[..., 1:]
+            rows = cross_entropy(shift_logits, shift_labels, vocab_start=self.word_embedding.vocab_start_idx,
+                                 group=tp_group() if tp_size() > 1 else None, reduction="none")
+            return rows.mean(), shift_logits
+
+        if prescaled:
+            (hidden,) = shard_sequence(hidden, shift=-1)
+        logits = self.lm_head(hidden) if self.add_lm_head else hidden
+        if labels is None:
+            return logits
+        # shift labels (not logits): position t predicts token t+1; the last position is
+        # ignored.  Same loss as slicing logits[..., :-1, :] without copying [B, s, V].
+        shift_labels = F.pad(labels[..., 1:], (0, 1), value=-100)
+        loss = cross_entropy(logits, shift_labels, ignore_index=-100)
+        return loss, logits
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

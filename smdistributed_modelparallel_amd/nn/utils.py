@@ -1,0 +1,336 @@
+"""Tensor-parallel building blocks: channel splits, parameter scopes and the autograd
+collectives used by the distributed modules.
+
+Reference parity (`smp/torch/nn/utils.py:45-844`):
+* ``get_local_channels(n)``: the first ``n % tp`` ranks get one extra channel;
+  ``get_start_pos_for_slicing`` gives each rank's offset (uneven splits supported);
+* collectives with forward/backward pairs: all-reduce (f/g), all-gather <-> narrow,
+  reduce-scatter <-> all-gather, all-to-all (scatter-and-merge), sequence shard/unshard;
+  uneven splits are padded to the largest shard for RCCL and un-padded after;
+* ``parameter_creation_scope`` marks parameters created in distributed modules as
+  scaled-batch parameters and initialises them *as if unsharded* (fan-in/fan-out of the
+  full layer, or N(0, initializer_range)).
+
+With tp_size == 1 every collective is an identity (no RCCL calls).
+"""
+import math
+from contextlib import contextmanager
+
+import torch
+import torch.distributed as dist
+
+from ..torch.state_mod import state
+
+
+# --------------------------------------------------------------------- topology
+def tp_size():
+    return state.core.tp_size() if state.initialized else 1
+
+
+def tp_rank():
+    return state.core.tp_rank() if state.initialized else 0
+
+
+def tp_group():
+    return state.pgs.tp if state.initialized else None
+
+
+def get_local_channels(num_channels, rank=None):
+    size = tp_size()
+    rank = tp_rank() if rank is None else rank
+    base, rem = divmod(num_channels, size)
+    return base + (1 if rank < rem else 0)
+
+
+def get_start_pos_for_slicing(num_channels, rank=None):
+    rank = tp_rank() if rank is None else rank
+    return sum(get_local_channels(num_channels, r) for r in range(rank))
+
+
+def get_merge_shapes(num_channels):
+    return [get_local_channels(num_channels, r) for r in range(tp_size())]
+
+
+# -------------------------------------------------------------- raw collectives
+def _pad_to(x, dim, n):
+    if x.size(dim) == n:
+        return x
+    pad_shape = list(x.shape)
+    pad_shape[dim] = n - x.size(dim)
+    return torch.cat([x, x.new_zeros(pad_shape)], dim=dim)
+
+
+def _allgather(x, dim, sizes=None):
+    """Concatenate every TP rank's x along dim (uneven sizes allowed)."""
+    ws = tp_size()
+    if ws == 1:
+        return x
+    group = tp_group()
+    x = x.contiguous()
+    if sizes is None:
+        sizes = [x.size(dim)] * ws
+    mx = max(sizes)
+    xp = _pad_to(x, dim, mx).movedim(dim, 0).contiguous()
+    out = xp.new_empty((ws * mx,) + tuple(xp.shape[1:]))
+    dist.all_gather_into_tensor(out, xp, group=group)
+    if any(s != mx for s in sizes):
+        out = torch.cat([p[:s] for p, s in zip(out.split(mx, dim=0), sizes)], dim=0)
+    return out.movedim(0, dim).contiguous() if dim != 0 else out
+
+
+def _reduce_scatter(x, dim, sizes=None):
+    """Sum over TP ranks, keep this rank's slice along dim."""
+    ws = tp_size()
+    if ws == 1:
+        return x
+    group = tp_group()
+    if sizes is None:
+        assert x.size(dim) % ws == 0, "reduce_scatter requires divisible size or explicit sizes"
+        sizes = [x.size(dim) // ws] * ws
+    mx = max(sizes)
+    parts = list(x.split(sizes, dim=dim))
+    padded = [_pad_to(p, dim, mx).movedim(dim, 0) for p in parts]
+    inp = torch.cat(padded, dim=0).contiguous()
+    out = inp.new_empty((mx,) + tuple(inp.shape[1:]))
+    dist.reduce_scatter_tensor(out, inp, group=group)
+    out = out[: sizes[tp_rank()]]
+    return out.movedim(0, dim).contiguous()
+
+
+def _allreduce(x):
+    if tp_size() == 1:
+        return x
+    x = x.contiguous()
+    dist.all_reduce(x, group=tp_group())
+    return x
+
+
+def _narrow(x, dim, sizes=None):
+    ws = tp_size()
+    if ws == 1:
+        return x
+    if sizes is None:
+        n = x.size(dim) // ws
+        return x.narrow(dim, tp_rank() * n, n).contiguous()
+    start = sum(sizes[: tp_rank()])
+    return x.narrow(dim, start, sizes[tp_rank()]).contiguous()
+
+
+def _all_to_all(x, split_dim, merge_dim, split_sizes=None, merge_sizes=None):
+    """Split x along split_dim into tp pieces (piece r -> rank r); concatenate received
+    pieces along merge_dim (uneven merge sizes allowed) -- `scatter_and_merge`."""
+    ws = tp_size()
+    if ws == 1:
+        return x
+    if split_sizes is None:
+        split_sizes = [x.size(split_dim) // ws] * ws
+    pieces = [p.contiguous() for p in x.split(split_sizes, dim=split_dim)]
+    me = tp_rank()
+    out_shapes = []
+    for r in range(ws):
+        s = list(pieces[me].shape)
+        if merge_sizes is not None:
+            s[merge_dim] = merge_sizes[r]
+        else:
+            s[merge_dim] = x.size(merge_dim)
+        out_shapes.append(s)
+    outs = [x.new_empty(s) for s in out_shapes]
+    # each received piece r has this rank's split slice and rank r's merge extent
+    dist.all_to_all(outs, pieces, group=tp_group())
+    return torch.cat(outs, dim=merge_dim)
+
+
+# ------------------------------------------------------------ autograd wrappers
+class _FwdAllreduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return _allreduce(x.clone() if tp_size() > 1 else x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _BwdAllreduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return _allreduce(g.clone() if tp_size() > 1 else g)
+
+
+class _Allgather(torch.autograd.Function):
+    """fwd all-gather along dim; bwd narrow (each rank keeps its own slice)."""
+
+    @staticmethod
+    def forward(ctx, x, dim, sizes):
+        ctx.dim, ctx.sizes = dim, sizes
+        return _allgather(x, dim, sizes)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _narrow(g, ctx.dim, ctx.sizes), None, None
+
+
+class _FusedAllgather(torch.autograd.Function):
+    """fwd all-gather; bwd reduce-scatter (the gathered tensor feeds rank-local math)."""
+
+    @staticmethod
+    def forward(ctx, x, dim, sizes):
+        ctx.dim, ctx.sizes = dim, sizes
+        return _allgather(x, dim, sizes)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _reduce_scatter(g, ctx.dim, ctx.sizes), None, None
+
+
+class _Narrow(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dim, sizes):
+        ctx.dim, ctx.sizes = dim, sizes
+        return _narrow(x, dim, sizes)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _allgather(g, ctx.dim, ctx.sizes), None, None
+
+
+class _ReduceScatter(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dim, sizes):
+        ctx.dim, ctx.sizes = dim, sizes
+        return _reduce_scatter(x, dim, sizes)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _allgather(g, ctx.dim, ctx.sizes), None, None
+
+
+class _ScatterAndMerge(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, split_dim, merge_dim, split_sizes, merge_sizes):
+        ctx.args = (split_dim, merge_dim, split_sizes, merge_sizes)
+        ctx.in_merge = x.size(merge_dim)
+        return _all_to_all(x, split_dim, merge_dim, split_sizes, merge_sizes)
+
+    @staticmethod
+    def backward(ctx, g):
+        split_dim, merge_dim, split_sizes, merge_sizes = ctx.args
+        # reverse: split along merge_dim by merge_sizes, merge along split_dim by split_sizes
+        back = _all_to_all(g, merge_dim, split_dim, merge_sizes, split_sizes)
+        return back, None, None, None, None
+
+
+def fwd_allreduce_for_tp(x):
+    return _FwdAllreduce.apply(x) if tp_size() > 1 else x
+
+
+def bwd_allreduce_for_tp(x):
+    return _BwdAllreduce.apply(x) if tp_size() > 1 else x
+
+
+def allgather_for_tp(x, dim, sizes=None):
+    return _Allgather.apply(x, dim, sizes) if tp_size() > 1 else x
+
+
+def fused_allgather_for_tp(x, dim, merge_shapes=None):
+    return _FusedAllgather.apply(x, dim, merge_shapes) if tp_size() > 1 else x
+
+
+def narrow_for_tp(x, dim, sizes=None):
+    return _Narrow.apply(x, dim, sizes) if tp_size() > 1 else x
+
+
+def reduce_scatter_for_tp(x, dim, split_shapes=None):
+    return _ReduceScatter.apply(x, dim, split_shapes) if tp_size() > 1 else x
+
+
+def scatter_and_merge_for_tp(x, split_dim, merge_dim, split_shapes=None, merge_shapes=None):
+    return _ScatterAndMerge.apply(x, split_dim, merge_dim, split_shapes, merge_shapes) if tp_size() > 1 else x
+
+
+def shard_sequence(*tensors, dim=1, shift=0, bwd_allgather=True):
+    """prescaled_batch: keep this rank's contiguous chunk of the sequence dimension."""
+    if tp_size() == 1:
+        return tensors
+    out = []
+    for t in tensors:
+        if t is None:
+            out.append(None)
+            continue
+        sizes = get_merge_shapes(t.size(dim))
+        if bwd_allgather and t.requires_grad:
+            out.append(narrow_for_tp(t, dim, sizes))
+        else:
+            out.append(_narrow(t, dim, sizes))
+    return tuple(out)
+
+
+def unshard_sequence(seq_length, *tensors, dim=1):
+    if tp_size() == 1:
+        return tensors
+    sizes = get_merge_shapes(seq_length)
+    return tuple(allgather_for_tp(t, dim, sizes) if t is not None else None for t in tensors)
+
+
+# ---------------------------------------------------------- parameter creation
+class _ScopeState:
+    active = []
+
+
+@contextmanager
+def parameter_creation_scope(module, scaled_batch=True, dtype=None, use_normal=False, initializer_range=0.02,
+                             fan_in=None, fan_out=None):
+    """Parameters created inside are (optionally) scaled-batch and initialised as if
+    unsharded.  `fan_in` / `fan_out` override the fans seen by nn.init (full layer dims)."""
+    _ScopeState.active.append(
+        dict(module=module, scaled_batch=scaled_batch, dtype=dtype, use_normal=use_normal,
+             initializer_range=initializer_range, fan_in=fan_in, fan_out=fan_out)
+    )
+    try:
+        yield
+    finally:
+        _ScopeState.active.pop()
+
+
+def mark_scaled_batch(param, scaled=True):
+    param._smp_scaled_batch = scaled
+    param._smp_distributed = True
+    return param
+
+
+def is_scaled_batch(param):
+    return getattr(param, "_smp_scaled_batch", False)
+
+
+def mark_tp(param, axis, groups=1, rank0_only=False):
+    """Record how a parameter is split across the TP group, for checkpoint merge/slice:
+    `axis` the sharded dim (None = replicated), `groups` > 1 when the full tensor is
+    `groups` concatenated blocks each sharded separately (fused QKV), `rank0_only` for
+    row-parallel biases that exist only on tp_rank 0."""
+    param._smp_tp_axis = axis
+    param._smp_tp_groups = groups
+    param._smp_tp_rank0_only = rank0_only
+    return param
+
+
+def init_weight_(w, full_in, full_out, initializer_range=0.02, use_normal=False):
+    """Initialise a (possibly sharded) [out, in] weight as nn.Linear of the full shape."""
+    with torch.no_grad():
+        if use_normal:
+            w.normal_(0.0, initializer_range)
+        else:
+            bound = 1.0 / math.sqrt(full_in) if full_in > 0 else 0.0
+            # kaiming_uniform(a=sqrt(5)) on the full layer == U(-1/sqrt(fan_in), 1/sqrt(fan_in))
+            w.uniform_(-bound, bound)
+    return w
+
+
+def init_bias_(b, full_in):
+    with torch.no_grad():
+        bound = 1.0 / math.sqrt(full_in) if full_in > 0 else 0.0
+        b.uniform_(-bound, bound)
+    return b

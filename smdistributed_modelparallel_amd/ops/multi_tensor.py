@@ -1,0 +1,127 @@
+"""Fused optimizer / reduction kernels over flat contiguous ranges (K12-K16, K20).
+
+GPU: one HIP kernel per call.  CPU: reference PyTorch math (test target).
+"""
+import math
+
+import torch
+
+from ._ext import ext
+
+
+def fused_adam_(param_lowp, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0,
+                adamw=True, bias_correction=True):
+    """Updates master/m/v in place (fp32) and writes param_lowp (if given) in the same pass."""
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    if master.is_cuda:
+        ext().fused_adam(param_lowp, grad, master, m, v, lr, beta1, beta2, eps, weight_decay, bc1, bc2,
+                         grad_scale, adamw)
+        return
+    g = grad.float() * grad_scale
+    if adamw:
+        master.mul_(1.0 - lr * weight_decay)
+    else:
+        g = g + weight_decay * master
+    m.mul_(beta1).add_(g, alpha=1.0 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    master.addcdiv_(m, denom, value=-lr / bc1)
+    if param_lowp is not None:
+        param_lowp.copy_(master)
+
+
+def fused_sgd_(param_lowp, grad, master, mom, lr, momentum, dampening, weight_decay, nesterov, first, grad_scale=1.0):
+    if master.is_cuda:
+        ext().fused_sgd(param_lowp, grad, master, mom, lr, momentum, dampening, weight_decay, nesterov, first,
+                        grad_scale)
+        return
+    g = grad.float() * grad_scale + weight_decay * master
+    if momentum != 0.0:
+        if first:
+            mom.copy_(g)
+        else:
+            mom.mul_(momentum).add_(g, alpha=1.0 - dampening)
+        g = g + momentum * mom if nesterov else mom
+    master.add_(g, alpha=-lr)
+    if param_lowp is not None:
+        param_lowp.copy_(master)
+
+
+def fused_adagrad_(param_lowp, grad, master, state_sum, lr, eps, weight_decay, grad_scale=1.0):
+    if master.is_cuda:
+        ext().fused_adagrad(param_lowp, grad, master, state_sum, lr, eps, weight_decay, grad_scale)
+        return
+    g = grad.float() * grad_scale + weight_decay * master
+    state_sum.addcmul_(g, g)
+    master.addcdiv_(g, state_sum.sqrt().add_(eps), value=-lr)
+    if param_lowp is not None:
+        param_lowp.copy_(master)
+
+
+def lamb_stage1_(grad, master, m, v, update, beta1, beta2, eps, weight_decay, step, grad_scale=1.0,
+                 bias_correction=True):
+    bc1 = 1.0 - beta1 ** step if bias_correction else 1.0
+    bc2 = 1.0 - beta2 ** step if bias_correction else 1.0
+    if master.is_cuda:
+        ext().lamb_stage1(grad, master, m, v, update, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale)
+        return
+    g = grad.float() * grad_scale
+    m.mul_(beta1).add_(g, alpha=1.0 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1.0 - beta2)
+    update.copy_((m / bc1) / ((v / bc2).sqrt() + eps) + weight_decay * master)
+
+
+def lamb_stage2_(param_lowp, master, update, lr, p_norm_sq, u_norm_sq, use_trust=True):
+    if master.is_cuda:
+        ext().lamb_stage2(param_lowp, master, update, lr, p_norm_sq, u_norm_sq, use_trust)
+        return
+    trust = 1.0
+    if use_trust:
+        a, b = float(p_norm_sq.sqrt()), float(u_norm_sq.sqrt())
+        trust = a / b if (a > 0 and b > 0) else 1.0
+    master.add_(update, alpha=-lr * trust)
+    if param_lowp is not None:
+        param_lowp.copy_(master)
+
+
+def sumsq(x, out=None, scale=1.0):
+    """Accumulates sum(x^2) * scale^2 into `out` (fp32 1-element tensor) and returns it."""
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    if x.numel() == 0:
+        return out
+    if x.is_cuda:
+        ext().sumsq_(x.contiguous(), out, scale)
+    else:
+        out += (x.float() * scale).pow(2).sum()
+    return out
+
+
+def nonfinite_flag(x, out=None):
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=x.device)
+    if x.numel() == 0:
+        return out
+    if x.is_cuda:
+        ext().nonfinite_(x.contiguous(), out)
+    else:
+        if not torch.isfinite(x).all():
+            out.fill_(1.0)
+    return out
+
+
+def axpby_(x, y, a, b):
+    if y.is_cuda:
+        ext().axpby_(x, y, a, b)
+    else:
+        y.mul_(b).add_(x, alpha=a)
+    return y
+
+
+def cast_copy_(src, dst, scale=1.0):
+    if dst.is_cuda:
+        ext().cast_copy_(src, dst, scale)
+    else:
+        dst.copy_(src.float() * scale if scale != 1.0 else src)
+    return dst

@@ -1,0 +1,55 @@
+"""Rotary position embeddings (K18): GPT-J interleaved pairs and GPT-NeoX half rotation
+(reference `smp/torch/nn/transformer.py:114-182,1565-1615`).
+
+x layout ``[b, s, h, d]``; only the first ``rotary_dim`` channels rotate.  cos/sin
+tables are built once per (seq, dim, base, device) in fp32 (precomputed tables rather
+than on-device trig, per the elementwise guidance for CDNA).
+"""
+import torch
+
+_cache = {}
+
+
+def rope_tables(seq_len, rotary_dim, base, device, offset=0):
+    key = (seq_len + offset, rotary_dim, base, device)
+    t = _cache.get(key)
+    if t is None:
+        inv = 1.0 / (base ** (torch.arange(0, rotary_dim, 2, dtype=torch.float32, device=device) / rotary_dim))
+        pos = torch.arange(seq_len + offset, dtype=torch.float32, device=device)
+        f = torch.outer(pos, inv)
+        t = (f.cos(), f.sin())
+        _cache[key] = t
+    cos, sin = t
+    return cos[offset: offset + seq_len], sin[offset: offset + seq_len]
+
+
+def _rotate_every_two(x):
+    x1 = x[..., ::2]
+    x2 = x[..., 1::2]
+    return torch.stack((-x2, x1), dim=-1).flatten(-2)
+
+
+def _rotate_half(x):
+    h = x.shape[-1] // 2
+    return torch.cat((-x[..., h:], x[..., :h]), dim=-1)
+
+
+def apply_rotary(x, rotary_dim, base=10000, neox_style=False, offset=0):
+    """Returns a new tensor with rotary applied (autograd-friendly)."""
+    if rotary_dim is None or rotary_dim == 0:
+        return x
+    b, s, h, d = x.shape
+    cos, sin = rope_tables(s, rotary_dim, base, x.device, offset)
+    rot, rest = x[..., :rotary_dim], x[..., rotary_dim:]
+    if neox_style:
+        c = torch.cat((cos, cos), dim=-1).view(1, s, 1, rotary_dim)
+        sn = torch.cat((sin, sin), dim=-1).view(1, s, 1, rotary_dim)
+        out = rot.float() * c + _rotate_half(rot.float()) * sn
+    else:
+        c = cos.repeat_interleave(2, dim=-1).view(1, s, 1, rotary_dim)
+        sn = sin.repeat_interleave(2, dim=-1).view(1, s, 1, rotary_dim)
+        out = rot.float() * c + _rotate_every_two(rot.float()) * sn
+    out = out.to(x.dtype)
+    if rest.shape[-1] == 0:
+        return out
+    return torch.cat((out, rest), dim=-1)

@@ -1,0 +1,382 @@
+"""``smp.DistributedOptimizer``.
+
+Reference parity (`smp/torch/optimizers/optimizer.py:437-549`, `fp16/fp16.py`): wraps any
+torch optimizer; with fp16/bf16 keeps fp32 master weights (Bit16_Optimizer semantics),
+unscales fp16 gradients with a static or dynamic loss scale and skips overflowing steps
+(overflow decision shared across the model-parallel group), ``clip_master_grads``
+(global L2 norm across model-parallel ranks), optimizer-state sharding
+(``shard_optimizer_state``: each data-parallel rank updates only its slice, then
+parameters are all-gathered), local/full state dicts, param name <-> index maps.
+
+MI355X design: the optimizer works on *domains* -- contiguous ranges of the model's flat
+parameter/gradient buffers (`parallel/flat.py`), one per gradient bucket (or this rank's
+chunk of each bucket when sharded).  For Adam/AdamW/SGD/Adagrad/LAMB the whole update
+(unscale + clip + moment update + fp32 master update + low-precision param write-back)
+is ONE fused HIP kernel per domain.  Any other torch optimizer runs through the same
+domains as fp32 "virtual parameters" (the reference's name for sharded master slices).
+"""
+import torch
+import torch.distributed as dist
+
+from ..backend.exceptions import SMPInvalidArgumentError
+from ..backend.logger import get_logger
+from ..ops import multi_tensor as mt
+from ..torch.state_mod import state
+from .loss_scaler import DynamicLossScaler, LossScaler, any_overflow
+
+logger = get_logger()
+
+
+def _kind_of(opt):
+    name = type(opt).__name__
+    if name in ("AdamW",):
+        return "adamw"
+    if name in ("Adam",):
+        return "adamw" if opt.defaults.get("decoupled_weight_decay", False) else "adam"
+    if name == "FusedAdam":
+        return "adamw" if getattr(opt, "adam_w_mode", True) else "adam"
+    if name == "SGD" or name == "FusedSGD":
+        return "sgd"
+    if name == "Adagrad" or name == "FusedAdagrad":
+        return "adagrad"
+    if name == "FusedLAMB":
+        return "lamb"
+    return "generic"
+
+
+class _Domain:
+    __slots__ = ("key", "start", "end", "group_index", "master", "m", "v", "upd", "vparam", "params")
+
+    def __init__(self, key, start, end, group_index, params):
+        self.key, self.start, self.end, self.group_index, self.params = key, start, end, group_index, params
+        self.master = self.m = self.v = self.upd = self.vparam = None
+
+    @property
+    def numel(self):
+        return self.end - self.start
+
+
+class DistributedOptimizer:
+    def __init__(self, optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None):
+        if state.model is None:
+            raise SMPInvalidArgumentError("create smp.DistributedModel before smp.DistributedOptimizer")
+        self.optimizer = optimizer
+        model = state.model
+        model_params = set(model.module.parameters())
+        for g in optimizer.param_groups:
+            for p in g["params"]:
+                if p not in model_params:
+                    raise SMPInvalidArgumentError("optimizer contains a parameter that is not part of the model")
+        self._orig_param_groups = [dict(g, params=list(g["params"])) for g in optimizer.param_groups]
+        cfg = state.cfg
+        self.fp16 = cfg.fp16 or cfg.fp16_params
+        self.bf16 = cfg.bf16
+        if self.fp16:
+            self.loss_scaler = DynamicLossScaler(**(dynamic_loss_args or {})) if dynamic_loss_scale else \
+                LossScaler(static_loss_scale)
+        else:
+            self.loss_scaler = LossScaler(1.0)
+        self.kind = _kind_of(optimizer)
+        self.domains = []
+        self._step_count = [0] * len(optimizer.param_groups)
+        self._clip_coef = None
+        self._built = False
+        self.overflow = False
+        state.optimizer = self
+        if model.partitioned:
+            self._on_model_partitioned()
+        if state.loaded_optimizer_state is not None:
+            self._deferred_load = state.loaded_optimizer_state
+        else:
+            self._deferred_load = None
+
+    # ----------------------------------------------------------------- props
+    @property
+    def loss_scale(self):
+        return self.loss_scaler.loss_scale
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    @property
+    def defaults(self):
+        return self.optimizer.defaults
+
+    @property
+    def state(self):
+        return self.optimizer.state
+
+    # ----------------------------------------------------------------- build
+    def _on_model_partitioned(self):
+        model = state.model
+        if not self._built:
+            model._relayout_for_optimizer([g["params"] for g in self._orig_param_groups])
+        self._build_domains()
+        self._built = True
+        if getattr(self, "_deferred_load", None) is not None:
+            self.load_state_dict(self._deferred_load)
+            self._deferred_load = None
+            state.loaded_optimizer_state = None
+
+    def _group_index_of(self):
+        idx = {}
+        for gi, g in enumerate(self._orig_param_groups):
+            for p in g["params"]:
+                idx.setdefault(p, gi)
+        return idx
+
+    def _build_domains(self):
+        model = state.model
+        gidx = self._group_index_of()
+        self.domains = []
+        lowp = self.fp16 or self.bf16
+        for key, flat in model.flat_groups.items():
+            red = model.reducers[key]
+            for b in flat.buckets:
+                gis = {gidx.get(p, 0) for p in b.params}
+                gi = min(gis)
+                if red.shard and red.group_size > 1:
+                    s, e = red.shard_range(b)
+                else:
+                    s, e = b.start, b.end
+                d = _Domain(key, s, e, gi, b.params)
+                dev = flat.data.device
+                if lowp or flat.data.dtype != torch.float32:
+                    d.master = flat.data[s:e].float().clone()
+                else:
+                    d.master = flat.data[s:e]  # fp32 model: the parameters are the master copy
+                if self.kind in ("adam", "adamw", "lamb"):
+                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev)
+                    d.v = torch.zeros(e - s, dtype=torch.float32, device=dev)
+                elif self.kind in ("sgd",):
+                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev)
+                elif self.kind == "adagrad":
+                    init = self.optimizer.param_groups[gi].get("initial_accumulator_value", 0.0)
+                    d.v = torch.full((e - s,), float(init), dtype=torch.float32, device=dev)
+                if self.kind == "lamb":
+                    d.upd = torch.empty(e - s, dtype=torch.float32, device=dev)
+                self.domains.append(d)
+        if self.kind == "generic":
+            # inner optimizer sees fp32 virtual parameters (one per domain)
+            groups = [[] for _ in self.optimizer.param_groups]
+            for d in self.domains:
+                vp = torch.nn.Parameter(d.master, requires_grad=True)
+                d.vparam = vp
+                groups[d.group_index].append(vp)
+            self.optimizer.state.clear()
+            for gi, g in enumerate(self.optimizer.param_groups):
+                g["params"] = groups[gi]
+
+    def virtual_named_parameters(self):
+        for i, d in enumerate(self.domains):
+            yield f"{d.key}/domain{i}", d.vparam if d.vparam is not None else d.master
+
+    # ------------------------------------------------------------------ step
+    def zero_grad(self, set_to_none=False):
+        model = state.model
+        for flat in model.flat_groups.values():
+            flat.zero_grad()
+        if self.kind == "generic":
+            for d in self.domains:
+                if d.vparam is not None:
+                    d.vparam.grad = None
+
+    def _grad_range(self, d):
+        return state.model.flat_groups[d.key].grad[d.start:d.end]
+
+    def _param_range(self, d):
+        return state.model.flat_groups[d.key].data[d.start:d.end]
+
+    def _model_parallel_group(self):
+        cfg = state.cfg
+        if cfg.shard_optimizer_state or cfg.zero2d_enabled():
+            return state.pgs.world
+        return state.pgs.mp
+
+    def _check_overflow(self):
+        grads = [self._grad_range(d) for d in self.domains]
+        return any_overflow(grads, self._model_parallel_group() if state.core.mp_size() > 1 or
+                            state.cfg.shard_optimizer_state else None)
+
+    def clip_master_grads(self, max_norm, norm_type=2):
+        """Global L2 norm of the (unscaled) gradients across all ranks holding distinct
+        gradients; records the clip coefficient applied inside the next step."""
+        if norm_type != 2:
+            raise SMPInvalidArgumentError("only L2 norm clipping is supported")
+        dev = state.device
+        acc = torch.zeros(1, dtype=torch.float32, device=dev)
+        core = state.core
+        inv = 1.0 / self.loss_scale
+        for d in self.domains:
+            # replicated (non-TP) params are identical on every tp_rank: count them once
+            if d.key == "default" and core.tp_size() > 1 and core.tp_rank() != 0:
+                continue
+            mt.sumsq(self._grad_range(d), acc, scale=inv)
+        if state.cfg.shard_optimizer_state and core.dp_size() > 1:
+            if core.tp_size() > 1:
+                dist.all_reduce(acc, group=state.pgs.world)
+            else:
+                dist.all_reduce(acc, group=state.pgs.world)
+        elif core.mp_size() > 1:
+            dist.all_reduce(acc, group=state.pgs.mp)
+        norm = acc.sqrt()
+        coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0)
+        self._clip_coef = coef
+        return norm
+
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        inv_scale = 1.0 / self.loss_scale
+        if self.fp16:
+            self.overflow = self._check_overflow()
+            if self.loss_scaler.dynamic:
+                self.loss_scaler.update_scale(self.overflow)
+            if self.overflow:
+                logger.info(f"gradient overflow: skipping step, loss scale -> {self.loss_scale}")
+                self._clip_coef = None
+                return loss
+        gscale = inv_scale
+        if self._clip_coef is not None:
+            # one scalar host read per step (the coefficient is already all-reduced)
+            gscale = gscale * float(self._clip_coef.item())
+            self._clip_coef = None
+        lowp = self.fp16 or self.bf16
+        for gi in range(len(self.optimizer.param_groups)):
+            self._step_count[gi] += 1
+        if self.kind == "generic":
+            self._generic_step(gscale, lowp)
+        else:
+            for d in self.domains:
+                self._fused_step(d, gscale, lowp)
+        self._allgather_shards()
+        return loss
+
+    def _hp(self, gi):
+        return self.optimizer.param_groups[gi]
+
+    def _fused_step(self, d, gscale, lowp):
+        g = self._hp(d.group_index)
+        step = self._step_count[d.group_index]
+        grad = self._grad_range(d)
+        plow = self._param_range(d) if (lowp or d.master.data_ptr() != self._param_range(d).data_ptr()) else None
+        lr = float(g["lr"])
+        wd = float(g.get("weight_decay", 0.0))
+        if self.kind in ("adam", "adamw"):
+            b1, b2 = g.get("betas", (0.9, 0.999))
+            mt.fused_adam_(plow, grad, d.master, d.m, d.v, lr, float(b1), float(b2), float(g.get("eps", 1e-8)), wd,
+                           step, gscale, adamw=self.kind == "adamw", bias_correction=g.get("bias_correction", True))
+        elif self.kind == "sgd":
+            mom = float(g.get("momentum", 0.0))
+            mt.fused_sgd_(plow, grad, d.master, d.m if mom != 0.0 else None, lr, mom, float(g.get("dampening", 0.0)),
+                          wd, bool(g.get("nesterov", False)), step == 1, gscale)
+        elif self.kind == "adagrad":
+            mt.fused_adagrad_(plow, grad, d.master, d.v, lr, float(g.get("eps", 1e-10)), wd, gscale)
+        elif self.kind == "lamb":
+            b1, b2 = g.get("betas", (0.9, 0.999))
+            mt.lamb_stage1_(grad, d.master, d.m, d.v, d.upd, float(b1), float(b2), float(g.get("eps", 1e-6)), wd,
+                            step, gscale, bias_correction=g.get("bias_correction", True))
+            # per-parameter trust ratios inside the domain
+            flat = state.model.flat_groups[d.key]
+            for p in d.params:
+                o = flat.offsets[p]
+                s, e = max(o, d.start), min(o + p.numel(), d.end)
+                if s >= e:
+                    continue
+                ms, upd = d.master[s - d.start:e - d.start], d.upd[s - d.start:e - d.start]
+                pn = mt.sumsq(ms)
+                un = mt.sumsq(upd)
+                pl = plow[s - d.start:e - d.start] if plow is not None else None
+                mt.lamb_stage2_(pl, ms, upd, lr, pn, un, use_trust=g.get("use_nvlamb", False) or wd != 0.0)
+
+    def _generic_step(self, gscale, lowp):
+        for d in self.domains:
+            gr = torch.empty_like(d.master)
+            mt.cast_copy_(self._grad_range(d), gr, gscale)
+            d.vparam.grad = gr
+        self.optimizer.step()
+        for d in self.domains:
+            if d.master.data_ptr() != self._param_range(d).data_ptr():
+                mt.cast_copy_(d.master, self._param_range(d))
+
+    def _allgather_shards(self):
+        model = state.model
+        for r in model.reducers.values():
+            if r.shard and r.group_size > 1:
+                r.allgather_params()
+
+    # ----------------------------------------------------------- state dicts
+    def local_optimizer_state_dict(self):
+        return {
+            "kind": self.kind,
+            "domains": [
+                {k: (getattr(d, k).detach().cpu() if getattr(d, k) is not None else None)
+                 for k in ("master", "m", "v")} | {"key": d.key, "start": d.start, "end": d.end}
+                for d in self.domains
+            ],
+            "step_count": list(self._step_count),
+            "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.optimizer.param_groups],
+            "inner": self.optimizer.state_dict() if self.kind == "generic" else None,
+        }
+
+    def local_fp16_state_dict(self):
+        return {"loss_scaler": self.loss_scaler.state_dict(), "fp16": self.fp16, "bf16": self.bf16}
+
+    def local_state_dict(self):
+        d = self.local_optimizer_state_dict()
+        d["fp16_state"] = self.local_fp16_state_dict()
+        return d
+
+    def state_dict(self):
+        return self.local_state_dict()
+
+    def load_local_optimizer_state_dict(self, sd):
+        if len(sd["domains"]) != len(self.domains):
+            raise SMPInvalidArgumentError("optimizer state does not match the current partition/sharding layout")
+        for d, s in zip(self.domains, sd["domains"]):
+            for k in ("master", "m", "v"):
+                t = getattr(d, k)
+                if t is not None and s.get(k) is not None:
+                    t.copy_(s[k].to(t.device))
+            lowp = self.fp16 or self.bf16
+            if lowp:
+                mt.cast_copy_(d.master, self._param_range(d))
+        self._step_count = list(sd.get("step_count", self._step_count))
+        for g, saved in zip(self.optimizer.param_groups, sd.get("param_groups", [])):
+            for k, v in saved.items():
+                g[k] = v
+        if self.kind == "generic" and sd.get("inner") is not None:
+            self.optimizer.load_state_dict(sd["inner"])
+        self._allgather_shards()
+
+    def load_local_fp16_state_dict(self, sd):
+        self.loss_scaler.load_state_dict(sd["loss_scaler"])
+
+    def load_state_dict(self, sd):
+        if not self._built:
+            self._deferred_load = sd
+            return
+        self.load_local_optimizer_state_dict(sd)
+        if "fp16_state" in sd:
+            self.load_local_fp16_state_dict(sd["fp16_state"])
+
+    def load_optimizer_checkpoint(self, sd):
+        self.load_state_dict(sd)
+
+    def param_name_to_index(self):
+        names = {p: n for n, p in state.model.module.named_parameters()}
+        out, i = {}, 0
+        for g in self._orig_param_groups:
+            for p in g["params"]:
+                out[names.get(p)] = i
+                i += 1
+        return out
+
+    def param_index_to_name(self):
+        return {v: k for k, v in self.param_name_to_index().items()}
+
+    def add_param_group(self, group):
+        raise SMPInvalidArgumentError("add_param_group after wrapping in DistributedOptimizer is not supported")
+
+    def __getstate__(self):
+        raise TypeError("DistributedOptimizer is not picklable; use smp.save_checkpoint")

@@ -1,0 +1,145 @@
+"""Bucketed, backward-overlapped gradient reduction over RCCL.
+
+Reference behaviour (native ``smplib.Reducer`` + ``GradCounter``, N1f/N1g;
+`smp/torch/ddp_model.py:43-632`, `allreduce/ddp.py`, `allreduce/scaler.py:32-42`):
+
+* scaled-batch (tensor-parallel) parameters are averaged over the RDP group and
+  additionally divided by ``microbatches x tp_size``; every other parameter is averaged
+  over the full DP group and divided by ``microbatches``
+  (``average_grads_across_microbatches``);
+* a bucket is reduced as soon as every parameter in it has its *final* gradient -- for a
+  single-stage model that is the last microbatch's backward; for pipeline stages the
+  native ``GradCounter`` decides;
+* ``backward_passes_per_step`` / ``require_backward_grad_sync`` gate the reduction;
+* DDP comm hooks can replace the all-reduce.
+
+MI355X design: buckets are contiguous slices of one flat gradient buffer
+(`parallel/flat.py`), launched strictly in bucket order (identical collective order on
+every rank) as asynchronous RCCL all-reduces -- or reduce-scatters when optimizer state
+is sharded -- that overlap the rest of backward on RCCL's own stream.  The default bucket
+cap is sized for ring all-reduce over xGMI (7 x ~153 GB/s links): ~200 MB keeps each ring
+step long enough to amortise launch latency while leaving >10 buckets of overlap for a
+1.5 B-parameter model.
+"""
+import torch
+import torch.distributed as dist
+
+from ..backend.logger import get_logger
+
+logger = get_logger()
+
+
+class BucketReducer:
+    def __init__(self, flat, group, group_size, divisor, overlap=True, shard=False, comm_hook=None,
+                 name="default"):
+        self.flat = flat
+        self.group = group
+        self.group_size = group_size
+        self.divisor = float(divisor)
+        self.overlap = overlap
+        self.shard = shard  # reduce-scatter instead of all-reduce (ZeRO-1)
+        self.comm_hook = comm_hook
+        self.name = name
+        self.final = False  # current backward produces final grads
+        self.sync_enabled = True
+        self.next_launch = 0
+        self._hooks = []
+        self._launched_any = False
+        self.group_rank = dist.get_rank(group) if (group is not None and dist.is_initialized()) else 0
+        if overlap:
+            self._install_hooks()
+
+    # ------------------------------------------------------------------ hooks
+    def _install_hooks(self):
+        for p in self.flat.params():
+            if p.requires_grad:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks.clear()
+
+    def _on_grad(self, p):
+        if not (self.final and self.sync_enabled):
+            return
+        b = self.flat.bucket_of.get(p)
+        if b is None:
+            return
+        b.ready += 1
+        if b.ready == len(b.params):
+            self._launch_ready()
+
+    def _launch_ready(self):
+        buckets = self.flat.buckets
+        while self.next_launch < len(buckets) and buckets[self.next_launch].ready >= len(buckets[self.next_launch].params):
+            self._launch(buckets[self.next_launch])
+            self.next_launch += 1
+
+    # ------------------------------------------------------------- collectives
+    def _launch(self, b):
+        if b.launched:
+            return
+        b.launched = True
+        buf = self.flat.grad[b.start : b.end]
+        scale = 1.0 / (self.divisor * self.group_size)
+        if scale != 1.0:
+            buf.mul_(scale)
+        if self.group is None or self.group_size == 1:
+            b.work = None
+            return
+        if self.comm_hook is not None:
+            b.work = self.comm_hook(b, buf)
+            return
+        if self.shard:
+            n = b.numel // self.group_size
+            out = buf[self.group_rank * n : (self.group_rank + 1) * n]
+            b.work = dist.reduce_scatter_tensor(out, buf, group=self.group, async_op=True)
+        else:
+            b.work = dist.all_reduce(buf, group=self.group, async_op=True)
+
+    # ------------------------------------------------------------------ step
+    def prepare_for_backward(self):
+        self.flat.rebind_grads()
+        for b in self.flat.buckets:
+            b.ready = 0
+            b.work = None
+            b.launched = False
+        self.next_launch = 0
+
+    def set_final(self, final):
+        self.final = final and self.overlap
+
+    def synchronize(self):
+        """Launch whatever is left (unused params / non-overlapped mode) and wait."""
+        if not self.sync_enabled:
+            return
+        for b in self.flat.buckets:
+            if not b.launched:
+                self._launch(b)
+        self.next_launch = len(self.flat.buckets)
+        for b in self.flat.buckets:
+            if b.work is not None:
+                if hasattr(b.work, "wait"):
+                    b.work.wait()
+                b.work = None
+
+    def shard_range(self, b):
+        n = b.numel // self.group_size
+        return b.start + self.group_rank * n, b.start + (self.group_rank + 1) * n
+
+    def allgather_params(self, async_op=False):
+        """After a sharded optimizer step: every rank's chunk of each bucket -> everyone."""
+        works = []
+        if self.group is None or self.group_size == 1:
+            return works
+        for b in self.flat.buckets:
+            buf = self.flat.data[b.start : b.end]
+            n = b.numel // self.group_size
+            chunk = buf[self.group_rank * n : (self.group_rank + 1) * n]
+            works.append(dist.all_gather_into_tensor(buf, chunk, group=self.group, async_op=True))
+        if not async_op:
+            for w in works:
+                w.wait()
+            return []
+        return works

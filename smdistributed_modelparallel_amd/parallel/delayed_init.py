@@ -1,0 +1,65 @@
+"""Delayed parameter initialisation.
+
+Reference behaviour (`smp/torch/parameter.py:23-36`): parameters created inside
+``smp.delay_param_initialization()`` are not materialised at construction; after
+partitioning only the *local* ones are allocated (on the device) and initialised, so a
+model larger than host memory can be built.  Implementation: construction happens on
+the ``meta`` device; at post-partition each local module with meta parameters is
+allocated with ``to_empty`` on the device and re-initialised by its own
+``reset_parameters`` (or the module's ``_init_weights`` for HF-style models), non-local
+meta parameters become empty tensors.
+"""
+from contextlib import contextmanager
+
+import torch
+
+from ..torch.state_mod import state
+
+
+@contextmanager
+def delay_param_initialization(enabled=True):
+    if not enabled:
+        yield
+        return
+    state.delay_param_initialization_enabled = True
+    try:
+        with torch.device("meta"):
+            yield
+    finally:
+        state.delay_param_initialization_enabled = False
+
+
+def _has_meta(m):
+    return any(p.is_meta for p in m.parameters(recurse=False)) or any(
+        b is not None and b.is_meta for b in m.buffers(recurse=False))
+
+
+def materialize_local(model):
+    root = model.module
+    mm = state.module_manager
+    device = state.device
+    me = state.core.pp_rank()
+    for m in root.modules():
+        if not _has_meta(m):
+            continue
+        local = mm.get_partition(m) == me or mm.get_partition(m) is None
+        for name, p in list(m._parameters.items()):
+            if p is None or not p.is_meta:
+                continue
+            if local:
+                p.data = torch.empty(p.shape, dtype=p.dtype, device=device)
+            else:
+                p.data = torch.empty(0, dtype=p.dtype, device=device)
+        for name, b in list(m._buffers.items()):
+            if b is not None and b.is_meta:
+                m._buffers[name] = torch.zeros(b.shape, dtype=b.dtype, device=device) if local else \
+                    torch.empty(0, dtype=b.dtype, device=device)
+        if local:
+            init = state.param_initializers.get(m)
+            with torch.no_grad():
+                if init is not None:
+                    init(m)
+                elif hasattr(m, "reset_parameters") and callable(m.reset_parameters):
+                    m.reset_parameters()
+                elif hasattr(root, "_init_weights"):
+                    root._init_weights(m)

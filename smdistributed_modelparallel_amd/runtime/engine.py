@@ -1,0 +1,529 @@
+"""Pipeline execution engine.
+
+What it does (reference behaviour, `smp/torch/server.py`, `worker.py`, `ops.py`,
+`patches/execution.py`, `sequential.py`): pp_rank 0 runs the user's step function per
+microbatch; whenever a module owned by another pipeline stage is called, the call becomes
+a request to that stage, the caller's coroutine is suspended and the server keeps
+scheduling other microbatches -- the pipeline schedule emerges from the task priorities
+(``interleaved`` / ``simple`` with the ``active_microbatches`` cap).  ``nn.Sequential``
+stacks are executed as chains that hop stage to stage directly (child-to-child) and only
+return to the caller at the end.
+
+How it is built here (our design, not the reference's):
+
+* **Coroutines are greenlets**, not OS threads handing a condition variable back and
+  forth: one OS thread, zero lock hand-offs, deterministic interleaving.
+* **Backward is segmented and asynchronous.** A remote call saves (requester side) the
+  tensors it sent and (executor side) its outputs and its input leaves.  Autograd hooks
+  (`RemoteOutput.backward`) and input-leaf gradients turn into backward *messages* to
+  whichever rank holds the next segment; every segment runs
+  ``torch.autograd.backward(saved, grads, retain_graph=True)`` -- gradients are linear,
+  so partial segments compose exactly.  No backward function ever blocks.
+* **Termination is an ack tree** (Dijkstra-Scholten): every backward message is acked
+  once the work it spawned has been acked; the microbatch root on pp_rank 0 completes
+  when its own children are acked.  This replaces the reference's real/dummy/sequential
+  receive counting (`module_manager.py:360-720`, `server.py:162-252`).
+* Microbatch state is freed when pp_rank 0 broadcasts the microbatch-end message, which
+  also carries the step outputs to every stage (`MicrobatchEndResult` semantics).
+"""
+import itertools
+
+import torch
+from greenlet import greenlet
+
+from ..backend.exceptions import PipelineParallelBWDError, SMPRuntimeError
+from ..backend.logger import get_logger
+from .pipeline import MbStatus, create_pipeline
+from .serialization import stubify, unstubify
+
+logger = get_logger()
+
+
+class RemoteOutput(torch.autograd.Function):
+    """Outputs of a module executed on another stage (reference ``SMPParentRecv``).
+
+    Forward is an identity on the received tensors; backward ships the output
+    gradients to the stage that holds the producing graph segment."""
+
+    @staticmethod
+    def forward(ctx, engine, holder, key, mb, *tensors):
+        ctx.set_materialize_grads(False)
+        ctx.engine, ctx.holder, ctx.key, ctx.mb = engine, holder, key, mb
+        return tuple(t.view_as(t) for t in tensors)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        if any(g is not None for g in grads):
+            ctx.engine._send_bwd(ctx.holder, ("out", ctx.key), ctx.mb, list(grads))
+        return (None, None, None, None) + (None,) * len(grads)
+
+
+class _Token:
+    __slots__ = ("pending", "ack_to", "remote_token", "mb", "done")
+
+    def __init__(self, ack_to, remote_token, mb):
+        self.pending = 0
+        self.ack_to = ack_to
+        self.remote_token = remote_token
+        self.mb = mb
+        self.done = False
+
+
+class _Worker:
+    __slots__ = ("g", "mb", "kind", "result", "exc", "wait_key")
+
+    def __init__(self, g, mb, kind):
+        self.g, self.mb, self.kind = g, mb, kind
+        self.result = None
+        self.exc = None
+        self.wait_key = None
+
+
+class _MbState:
+    __slots__ = ("sent", "leaves", "out")
+
+    def __init__(self):
+        self.sent = {}
+        self.leaves = {}
+        self.out = {}
+
+
+class PipelineEngine:
+    def __init__(self, state):
+        self.state = state
+        self._ids = itertools.count()
+        self.reset_step()
+
+    # ------------------------------------------------------------- plumbing
+    @property
+    def core(self):
+        return self.state.core
+
+    def reset_step(self):
+        self.mbstate = {}
+        self.tokens = {}
+        self.waiting = {}  # wait key -> worker
+        self.workers = []
+        self.results = {}
+        self.pipeline = None
+        self._cur_token = None
+        self._stop = False
+        self._root_tokens = {}
+        self._local_q = []
+
+    def _new_id(self):
+        return (self.core.rank(), next(self._ids))
+
+    def _mb(self, mb):
+        s = self.mbstate.get(mb)
+        if s is None:
+            s = self.mbstate[mb] = _MbState()
+        return s
+
+    def _pp_peer(self, pp_rank):
+        return self.core.pp_rank_to_rank(pp_rank)
+
+    def _send(self, dst, msg):
+        stubbed, tensors = stubify(msg)
+        self.state.transport.send(dst, stubbed, tensors)
+
+    def _broadcast_pp(self, msg):
+        me = self.core.rank()
+        for r in self.core.get_pp_group():
+            if r != me:
+                self._send(r, msg)
+
+    # ============================================================== run_step
+    def run_step(self, step_fn, mb_inputs):
+        model = self.state.model
+        if self.core.pp_size() == 1:
+            return self._run_local(step_fn, mb_inputs)
+        model._ensure_partitioned(step_fn, mb_inputs)
+        return self._run_pipelined(step_fn, mb_inputs)
+
+    def _run_local(self, step_fn, mb_inputs):
+        outs = []
+        n = len(mb_inputs)
+        model = self.state.model
+        for mb, (a, k) in enumerate(mb_inputs):
+            self.state.microbatch = mb
+            model._begin_microbatch(mb, n)
+            outs.append(step_fn.run_microbatch(mb, a, k))
+        return outs
+
+    # ------------------------------------------------------------ pipelined
+    def _run_pipelined(self, step_fn, mb_inputs):
+        self.reset_step()
+        cfg = self.state.cfg
+        n = cfg.microbatches
+        self.num_mb = n
+        leader = self.core.pp_rank() == 0
+        self.server = greenlet.getcurrent()
+        self.step_fn = step_fn
+        self.mb_inputs = mb_inputs
+        if leader:
+            self.pipeline = create_pipeline(cfg.pipeline, n, cfg.active_microbatches)
+        try:
+            self._serve(leader)
+        finally:
+            self.state.transport.drain()
+        outs = [self.results[i] for i in range(n)]
+        self.reset_step()
+        return outs
+
+    def _serve(self, leader):
+        timeout = 0.05
+        while not self._stop:
+            progressed = False
+            while self._local_q:
+                result_id, payload = self._local_q.pop(0)
+                self._resume(self.waiting.pop(("res", result_id)), payload)
+                progressed = True
+            while True:
+                m = self.state.transport.poll(0.0)
+                if m is None:
+                    break
+                self._dispatch(*m)
+                progressed = True
+                if self._stop:
+                    return
+            if leader:
+                if self.pipeline.is_done():
+                    self._stop = True
+                    return
+                act = self.pipeline.next_action()
+                if act is not None:
+                    kind, mb = act
+                    if kind == "fwd":
+                        self._start_microbatch(mb)
+                    else:
+                        self.pipeline.set_status(mb, MbStatus.BWD)
+                        self._resume(self.waiting.pop(("bwd_start", mb)), None)
+                    progressed = True
+            if not progressed:
+                m = self.state.transport.poll(timeout)
+                if m is not None:
+                    self._dispatch(*m)
+
+    # ----------------------------------------------------------- coroutines
+    def _spawn(self, fn, mb, kind, *args):
+        w = _Worker(None, mb, kind)
+
+        def run():
+            try:
+                w.result = fn(*args)
+            except BaseException as e:  # noqa: B902 - re-raised in the server
+                w.exc = e
+            return ("exit", w)
+
+        w.g = greenlet(run, parent=self.server)
+        self.workers.append(w)
+        self._resume(w, None)
+
+    def _resume(self, worker, value):
+        ret = worker.g.switch(value)
+        self._after_switch(worker, ret)
+
+    def _after_switch(self, worker, ret):
+        kind, payload = ret
+        if kind == "exit":
+            self.workers.remove(worker)
+            if worker.exc is not None:
+                self._abort(worker.exc)
+            if worker.kind == "root":
+                self._finish_microbatch(worker.mb, worker.result)
+        elif kind == "wait":
+            worker.wait_key = payload
+            self.waiting[payload] = worker
+            if payload[0] == "bwd_start":
+                self.pipeline.set_status(payload[1], MbStatus.READY_FOR_BWD)
+                self.state.model._mark_fwd_pass_done(payload[1])
+
+    def _suspend(self, key):
+        """Called from a worker: yield to the server until `key` is satisfied."""
+        st = self.state
+        saved = (torch.is_grad_enabled(), st.microbatch, self._cur_token)
+        cur = greenlet.getcurrent()
+        worker = next((w for w in self.workers if w.g is cur), None)
+        if worker is None:
+            raise SMPRuntimeError("remote call outside of a pipeline worker")
+        value = self.server.switch(("wait", key))
+        torch.set_grad_enabled(saved[0])
+        st.microbatch = saved[1]
+        self._cur_token = saved[2]
+        return value
+
+    def _abort(self, exc):
+        try:
+            self._broadcast_pp(("abort", repr(exc)))
+        except Exception:  # pragma: no cover
+            pass
+        raise exc
+
+    # ------------------------------------------------------------- dispatch
+    def _dispatch(self, src, stubbed, tensors):
+        kind = stubbed[0]
+        if kind == "fwd":
+            self._spawn(self._exec_fwd, stubbed[2], "fwd", src, stubbed, tensors)
+        elif kind == "res":
+            _, result_id, mb, out_stubbed, holder, out_key, grad_enabled = stubbed
+            w = self.waiting.pop(("res", result_id))
+            self._resume(w, (out_stubbed, tensors, holder, out_key))
+        elif kind == "bwd":
+            _, key, mb, grads_stubbed, remote_token = stubbed
+            grads = unstubify(grads_stubbed, tensors)
+            self._process_bwd(src, key, mb, grads, remote_token)
+        elif kind == "ack":
+            self._ack(stubbed[1])
+        elif kind == "mbdone":
+            _, mb, out_stubbed = stubbed
+            self.results[mb] = unstubify(out_stubbed, tensors)
+            self.mbstate.pop(mb, None)
+            self.state.model._on_microbatch_done(mb)
+            if len(self.results) == self.num_mb:
+                self._stop = True
+        elif kind == "abort":
+            raise SMPRuntimeError(f"peer pipeline stage (rank {src}) failed: {stubbed[1]}")
+        else:
+            raise SMPRuntimeError(f"unknown pipeline message {kind}")
+
+    # ----------------------------------------------------------- microbatch
+    def _start_microbatch(self, mb):
+        self.pipeline.set_status(mb, MbStatus.FWD)
+        a, k = self.mb_inputs[mb]
+        self.state.model._begin_microbatch(mb, self.num_mb)
+
+        def run():
+            self.state.microbatch = mb
+            return self.step_fn.run_microbatch(mb, a, k)
+
+        self._spawn(run, mb, "root")
+
+    def _finish_microbatch(self, mb, out):
+        self.pipeline.mark_done(mb)
+        self.results[mb] = out
+        self.mbstate.pop(mb, None)
+        self.state.model._on_microbatch_done(mb)
+        self._broadcast_pp(("mbdone", mb, out))
+
+    # ------------------------------------------------------- forward (remote)
+    def remote_module_call(self, module, args, kwargs):
+        mm = self.state.module_manager
+        name = mm.get_module_name(module)
+        owner = self._pp_peer(mm.get_partition(module))
+        return self._remote_call(owner, ("module", name), (args, kwargs))
+
+    def remote_chain_call(self, seq, start, inp):
+        mm = self.state.module_manager
+        name = mm.get_module_name(seq)
+        child = list(seq.children())[start]
+        owner = self._pp_peer(mm.get_partition(child))
+        return self._remote_call(owner, ("chain", name, start), ((inp,), {}))
+
+    def _remote_call(self, owner, target, payload):
+        st = self.state
+        mb = st.microbatch
+        rid = self._new_id()
+        grad_enabled = torch.is_grad_enabled()
+        stubbed, tensors = stubify(payload)
+        if grad_enabled:
+            sent = [t for t in tensors if t.requires_grad]
+            if sent:
+                self._mb(mb).sent[rid] = sent
+        st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled), tensors)
+        out_stubbed, out_tensors, holder, out_key = self._suspend(("res", rid))
+        return self._materialize_outputs(out_stubbed, out_tensors, holder, out_key, mb, grad_enabled)
+
+    def _materialize_outputs(self, out_stubbed, tensors, holder, out_key, mb, grad_enabled):
+        _, stubs = _stubs_of(out_stubbed)
+        rg_idx = [s.index for s in stubs if s.requires_grad] if grad_enabled else []
+        if rg_idx:
+            tensors = list(tensors)
+            ins = []
+            for i in rg_idx:
+                t = tensors[i].detach()
+                t.requires_grad_(True)
+                ins.append(t)
+            wrapped = RemoteOutput.apply(self, holder, out_key, mb, *ins)
+            for i, w in zip(rg_idx, wrapped):
+                tensors[i] = w
+        return unstubify(out_stubbed, tensors)
+
+    def _exec_fwd(self, src, msg, tensors):
+        _, rid, mb, target, stubbed, reply_to, result_id, grad_enabled = msg
+        st = self.state
+        st.microbatch = mb
+        torch.set_grad_enabled(grad_enabled)
+        _, stubs = _stubs_of(stubbed)
+        tensors = list(tensors)
+        if grad_enabled:
+            leaves = []
+            for s in stubs:
+                if s.requires_grad:
+                    t = tensors[s.index].detach()
+                    t.requires_grad_(True)
+                    tensors[s.index] = t
+                    leaves.append(t)
+            if leaves:
+                self._mb(mb).leaves[rid] = (leaves, src)
+        args, kwargs = unstubify(stubbed, tensors)
+        mm = st.module_manager
+        if target[0] == "module":
+            module = mm.get_module(target[1])
+            out = st.model._call_local(module, args, kwargs)
+            self._send_result(reply_to, result_id, mb, out, rid, grad_enabled)
+        else:
+            seq = mm.get_module(target[1])
+            self.run_chain(seq, target[2], args[0], reply_to, result_id, mb, rid, grad_enabled)
+
+    def run_chain(self, seq, start, h, reply_to, result_id, mb, rid, grad_enabled):
+        """Execute seq's children from `start` while they are local; hand the rest to the
+        next stage directly (child-to-child)."""
+        mm = self.state.module_manager
+        children = list(seq.children())
+        me = self.core.pp_rank()
+        i = start
+        j = i
+        while j < len(children) and mm.get_partition(children[j]) == me:
+            j += 1
+        h = self.state.model._run_local_chain(seq, children, i, j, h)
+        if j == len(children):
+            self._send_result(reply_to, result_id, mb, h, rid, grad_enabled)
+            return
+        nxt = self._pp_peer(mm.get_partition(children[j]))
+        rid2 = self._new_id()
+        stubbed, tensors = stubify(((h,), {}))
+        if grad_enabled:
+            sent = [t for t in tensors if t.requires_grad]
+            if sent:
+                self._mb(mb).sent[rid2] = sent
+        self.state.transport.send(
+            nxt, ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled),
+            tensors,
+        )
+
+    def _send_result(self, reply_to, result_id, mb, out, rid, grad_enabled):
+        stubbed, tensors = stubify(out)
+        if grad_enabled:
+            rg = [t for t in tensors if t.requires_grad]
+            if rg:
+                self._mb(mb).out[rid] = rg
+        msg = ("res", result_id, mb, stubbed, self.core.rank(), rid, grad_enabled)
+        if reply_to == self.core.rank():
+            # local delivery (a chain came back to its requester's stage): queue it for the
+            # server loop -- a worker must never resume another worker directly.
+            det = [t.detach() for t in tensors]
+            self._local_q.append((result_id, (stubbed, det, self.core.rank(), rid)))
+        else:
+            self.state.transport.send(reply_to, msg, tensors)
+
+    # --------------------------------------------------------------- backward
+    def backward_root(self, tensors, grads):
+        """model.backward() on pp_rank 0 inside a microbatch worker."""
+        mb = self.state.microbatch
+        self._suspend(("bwd_start", mb))
+        tid = self._new_token(None, None, mb)
+        self._root_tokens[mb] = tid
+        self._run_backward(tid, mb, tensors, grads)
+        self._maybe_finish(tid)
+        if not self.tokens.get(tid, _DONE).done:
+            self._suspend(("bwd_done", mb))
+
+    def _new_token(self, ack_to, remote_token, mb):
+        tid = next(self._ids)
+        self.tokens[tid] = _Token(ack_to, remote_token, mb)
+        return tid
+
+    def _send_bwd(self, holder, key, mb, grads):
+        parent = self._cur_token
+        if parent is None:
+            raise PipelineParallelBWDError("remote backward outside of a tracked backward segment")
+        self.tokens[parent].pending += 1
+        self._send(holder, ("bwd", key, mb, grads, parent))
+
+    def _run_backward(self, tid, mb, tensors, grads):
+        pairs = [(t, g) for t, g in zip(tensors, grads) if g is not None and t.requires_grad]
+        prev = self._cur_token
+        self._cur_token = tid
+        try:
+            if pairs:
+                with torch.enable_grad():
+                    torch.autograd.backward([t for t, _ in pairs], [g for _, g in pairs], retain_graph=True)
+            self._flush_leaf_grads(mb)
+        finally:
+            self._cur_token = prev
+
+    def _flush_leaf_grads(self, mb):
+        s = self.mbstate.get(mb)
+        if s is None:
+            return
+        for rid, (leaves, provider) in s.leaves.items():
+            gs = [l.grad for l in leaves]
+            if any(g is not None for g in gs):
+                for l in leaves:
+                    l.grad = None
+                self._send_bwd(provider, ("in", rid), mb, gs)
+
+    def _process_bwd(self, src, key, mb, grads, remote_token):
+        s = self._mb(mb)
+        kind, rid = key
+        saved = s.sent.get(rid) if kind == "in" else s.out.get(rid)
+        if saved is None:
+            raise PipelineParallelBWDError(f"no saved tensors for {key} (mb {mb}) on rank {self.core.rank()}")
+        tid = self._new_token(src, remote_token, mb)
+        self.state.microbatch = mb
+        self._run_backward(tid, mb, saved, grads)
+        self._maybe_finish(tid)
+
+    def _ack(self, tid):
+        t = self.tokens[tid]
+        t.pending -= 1
+        self._maybe_finish(tid)
+
+    def _maybe_finish(self, tid):
+        t = self.tokens[tid]
+        if t.pending > 0 or t.done:
+            return
+        t.done = True
+        del self.tokens[tid]
+        if t.ack_to is not None:
+            self._send(t.ack_to, ("ack", t.remote_token))
+        else:
+            w = self.waiting.pop(("bwd_done", t.mb), None)
+            if w is not None:
+                self._resume(w, None)
+
+
+class _DoneSentinel:
+    done = True
+
+
+_DONE = _DoneSentinel()
+
+
+def _stubs_of(stubbed):
+    from .serialization import TensorStub
+
+    found = []
+
+    def walk(o, memo):
+        if isinstance(o, TensorStub):
+            found.append(o)
+            return
+        oid = id(o)
+        if oid in memo:
+            return
+        memo.add(oid)
+        if isinstance(o, (list, tuple, set)):
+            for x in o:
+                walk(x, memo)
+        elif isinstance(o, dict):
+            for x in o.values():
+                walk(x, memo)
+        elif hasattr(o, "__dict__") and not isinstance(o, type):
+            for x in vars(o).values():
+                walk(x, memo)
+
+    walk(stubbed, set())
+    uniq = {s.index: s for s in found}
+    return stubbed, [uniq[i] for i in sorted(uniq)]

@@ -1,0 +1,591 @@
+"""``smp.DistributedModel``.
+
+Reference parity (`smp/torch/model.py:79-1608`): wraps a user module; casts to fp16/bf16
+(Bit16 module); replaces TP-marked modules with their distributed counterparts (checking
+the total parameter count); partitions modules across pipeline stages (manual or auto,
+only global rank 0 traces, the partition is sent to every rank, the main module is
+partition 0); after partitioning moves only local modules to the device, disables and
+releases non-local parameters, creates the gradient reducers (scaled-batch params over
+RDP, others over DP), broadcasts parameters over the data-parallel groups and runs
+post-partition hooks; ``backward`` casts the loss to fp32 and scales it for fp16;
+``_step`` brackets every step with reducer preparation/synchronisation, post-step hooks
+and a pipeline barrier; state dicts (local / gathered), hooks, local views.
+"""
+import contextlib
+import os
+from collections import OrderedDict
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..backend.collectives import CommGroup
+from ..backend.exceptions import (
+    SMPInvalidArgumentError,
+    SMPRuntimeError,
+    StepFunctionCalledError,
+)
+from ..backend.logger import get_logger
+from ..parallel.ddp import BucketReducer
+from ..parallel.flat import FlatParamGroup
+from ..runtime.engine import PipelineEngine
+from .state_mod import state
+
+logger = get_logger()
+
+_FIRST_BUCKET_BYTES = 1 << 20
+
+
+def _is_scaled_batch(p):
+    return getattr(p, "_smp_scaled_batch", False)
+
+
+class DistributedModel(nn.Module):
+    def __init__(
+        self,
+        module,
+        trace_device="gpu",
+        trace_execution_times=False,
+        trace_memory_usage=False,
+        overlapping_allreduce=True,
+        backward_passes_per_step=1,
+        average_grads_across_microbatches=True,
+        bucket_cap_mb=None,
+        find_unused_parameters=False,
+        broadcast_buffers=True,
+        gradient_as_bucket_view=True,
+        **ddp_kwargs,
+    ):
+        super().__init__()
+        if not state.initialized:
+            raise SMPRuntimeError("smp.init() must be called before smp.DistributedModel")
+        if state.model is not None:
+            raise SMPRuntimeError("only one smp.DistributedModel per process is supported")
+        cfg = state.cfg
+        self.trace_device = trace_device
+        self.trace_execution_times = trace_execution_times
+        self.trace_memory_usage = trace_memory_usage
+        self.overlapping_allreduce = overlapping_allreduce
+        self.backward_passes_per_step = backward_passes_per_step
+        self.average_grads_across_microbatches = average_grads_across_microbatches
+        self.bucket_cap_mb = bucket_cap_mb if bucket_cap_mb is not None else cfg.amd_bucket_cap_mb
+        self.find_unused_parameters = find_unused_parameters
+        self.broadcast_buffers = broadcast_buffers
+        self.gradient_as_bucket_view = gradient_as_bucket_view
+        self.require_backward_grad_sync = True
+        self._backward_passes = 0
+        self._post_partition_hooks = OrderedDict()
+        self._post_step_hooks = OrderedDict()
+        self._post_step_hooks_run = set()
+        self._comm_hook = None
+        self.partitioned = False
+        self._partitions_assigned = False
+        self.flat_groups = {}
+        self.reducers = {}
+        self._optimizer = None
+        self._step_had_backward = False
+
+        mm = state.module_manager
+        state.model = self
+        # bit16 cast (Bit16_Module semantics: params + floating buffers)
+        if cfg.fp16 or cfg.fp16_params:
+            module = module.half()
+        elif cfg.bf16:
+            module = module.to(torch.bfloat16)
+        mm.simplify_tensor_parallelism_modules(module)
+        module = self._replace_tp_counterparts(module)
+        self.module = module
+        mm.set_main_module(module)
+        mm.name_modules_and_create_parent_map()
+        state.engine = PipelineEngine(state)
+
+        if state.loaded_model_state is not None:
+            self._deferred_load = state.loaded_model_state
+        else:
+            self._deferred_load = None
+
+        if state.core.pp_size() == 1:
+            for m in module.modules():
+                mm.assign_partition(m, 0)
+            self._partitions_assigned = True
+            self.post_partition()
+        elif not cfg.auto_partition or mm.partition_loaded:
+            self._partitions_assigned = True
+
+    # ============================================================ TP replace
+    def _replace_tp_counterparts(self, module):
+        mm = state.module_manager
+        reg = state.tp_registry
+        marked = mm.tp_modules()
+        if not marked or reg is None:
+            return module
+        before = sum(p.numel() for p in module.parameters())
+
+        def replace(parent):
+            for name, child in list(parent.named_children()):
+                if child in marked:
+                    new = reg.distribute(child, mm.get_tp_config(child))
+                    setattr(parent, name, new)
+                    mm.register_distributed(new)
+                else:
+                    replace(child)
+
+        if module in marked:
+            module = reg.distribute(module, mm.get_tp_config(module))
+            mm.register_distributed(module)
+        else:
+            replace(module)
+        if os.environ.get("SMP_SKIP_PARAMS_CHECKING", "0") != "1" and state.core.tp_size() > 1:
+            local = sum(p.numel() for p in module.parameters() if not _is_scaled_batch(p))
+            dist_local = sum(p.numel() for p in module.parameters() if _is_scaled_batch(p))
+            counts = state.comm.allgather(dist_local, CommGroup.TP_GROUP)
+            total = local + sum(counts)
+            if total < before * 0.98 or total > before * 1.05:
+                logger.warning(
+                    f"parameter count after TP replacement ({total}) differs from the original ({before}); "
+                    "set SMP_SKIP_PARAMS_CHECKING=1 to silence"
+                )
+        return module
+
+    # ============================================================ partition
+    def _ensure_partitioned(self, step_fn, mb_inputs):
+        if self.partitioned:
+            return
+        mm = state.module_manager
+        if not self._partitions_assigned:
+            from ..runtime.partition import auto_partition
+
+            auto_partition(self, step_fn, mb_inputs)
+            self._partitions_assigned = True
+        else:
+            mm.assign_unassigned_modules(self.module)
+            mm.set_main_module(self.module)
+        self.post_partition()
+
+    def post_partition(self):
+        mm = state.module_manager
+        device = state.device
+        me = state.core.pp_rank()
+        mm.assign_unassigned_modules(self.module)
+        mm._module_partitions[self.module] = 0
+        # modules sharing parameters must be co-located: owner = partition of first user
+        owner = {}
+        for m in self.module.modules():
+            for p in m.parameters(recurse=False):
+                owner.setdefault(p, mm.get_partition(m))
+        self._param_owner = owner
+        local_params = {p for p, part in owner.items() if part == me}
+        # move local modules, release non-local parameters
+        for m in self.module.modules():
+            for name, p in list(m.named_parameters(recurse=False)):
+                if p in local_params:
+                    if p.device != device:
+                        p.data = p.data.to(device)
+                else:
+                    p.requires_grad_(False)
+                    p.data = torch.empty(0, dtype=p.dtype, device=device)
+            if mm.get_partition(m) == me:
+                for name, b in list(m.named_buffers(recurse=False)):
+                    if b is not None and b.device != device:
+                        m._buffers[name] = b.to(device)
+        self._init_deferred_params()
+        self._local_params = [p for p in self._ordered_params() if p in local_params]
+        self._update_transformer_boundaries()
+        self._build_flat_and_reducers()
+        self._broadcast_params()
+        if state.core.pp_size() > 1:
+            from ..runtime.patch import patch_module_forwards
+
+            patch_module_forwards(self)
+            state.transport.warmup(state.core.get_pp_group())
+        self.partitioned = True
+        if self._deferred_load is not None:
+            self.load_state_dict(self._deferred_load["model"], **self._deferred_load.get("kwargs", {}))
+            self._deferred_load = None
+            state.loaded_model_state = None
+        for hook in list(self._post_partition_hooks.values()):
+            hook(self, state.optimizer)
+        if state.optimizer is not None:
+            state.optimizer._on_model_partitioned()
+        if state.cfg.delayed_parameter_initialization:
+            pass
+
+    def _init_deferred_params(self):
+        from ..parallel.delayed_init import materialize_local
+
+        materialize_local(self)
+
+    def _ordered_params(self):
+        seen, out = set(), []
+        for _, p in self.module.named_parameters(remove_duplicate=False):
+            if p not in seen:
+                seen.add(p)
+                out.append(p)
+        return out
+
+    def _update_transformer_boundaries(self):
+        from ..nn.transformer import DistributedTransformer
+
+        mm = state.module_manager
+        for m in self.module.modules():
+            if isinstance(m, DistributedTransformer):
+                m.update_layer_boundaries(mm.get_partition if state.core.pp_size() > 1 else None)
+
+    # ============================================================ reducers
+    def _param_groups_for_layout(self):
+        opt = state.optimizer
+        if opt is None:
+            return None
+        return [list(g["params"]) for g in opt._orig_param_groups]
+
+    def _build_flat_and_reducers(self, segments=None):
+        cfg = state.cfg
+        core = state.core
+        device = state.device
+        named = []
+        name_of = {}
+        for n, p in self.module.named_parameters():
+            name_of.setdefault(p, n)
+        for p in self._local_params:
+            if p.requires_grad:
+                named.append((name_of.get(p, str(id(p))), p))
+        tp = core.tp_size()
+        groups = {"default": [], "scaled": []}
+        for n, p in named:
+            key = "scaled" if (tp > 1 and _is_scaled_batch(p)) else "default"
+            groups[key].append((n, p))
+        for r in self.reducers.values():
+            r.remove_hooks()
+        self.flat_groups.clear()
+        self.reducers.clear()
+        shard = cfg.shard_optimizer_state
+        cap = int(self.bucket_cap_mb * (1 << 20))
+        for key, members in groups.items():
+            if not members:
+                continue
+            if key == "scaled":
+                group, gsize = state.pgs.rdp, core.rdp_size()
+                divisor = (cfg.microbatches * tp) if self.average_grads_across_microbatches else tp
+            else:
+                group, gsize = state.pgs.dp, core.dp_size()
+                divisor = cfg.microbatches if self.average_grads_across_microbatches else 1
+            dtypes = {p.dtype for _, p in members}
+            if len(dtypes) != 1:
+                raise SMPInvalidArgumentError(f"mixed parameter dtypes {dtypes} are not supported in one model")
+            dtype = dtypes.pop()
+            flat = FlatParamGroup(members, device, dtype, cap, _FIRST_BUCKET_BYTES, align=64 * max(1, gsize),
+                                  segments=segments)
+            self.flat_groups[key] = flat
+            self.reducers[key] = BucketReducer(flat, group if gsize > 1 else None, gsize, divisor,
+                                               overlap=self.overlapping_allreduce, shard=shard,
+                                               comm_hook=self._comm_hook, name=key)
+
+    def _relayout_for_optimizer(self, param_groups):
+        """Re-order the flat buffers by optimizer param group (one contiguous segment per
+        group, so the fused optimizer kernel sees one hyper-parameter set per range)."""
+        if self.partitioned:
+            self._build_flat_and_reducers(segments=param_groups)
+
+    def _broadcast_params(self):
+        core = state.core
+        if core.dp_size() <= 1:
+            return
+        src_dp = core.ranker.translate(core.pp_rank(), 0, 0)
+        with torch.no_grad():
+            for key, flat in self.flat_groups.items():
+                if key == "scaled":
+                    if core.rdp_size() > 1:
+                        src = core.ranker.translate(core.pp_rank(), core.tp_rank(), 0)
+                        dist.broadcast(flat.data, src, group=state.pgs.rdp)
+                else:
+                    dist.broadcast(flat.data, src_dp, group=state.pgs.dp)
+            if self.broadcast_buffers:
+                for b in self.local_buffers():
+                    if b is not None and b.numel() > 0 and b.is_floating_point():
+                        dist.broadcast(b, src_dp, group=state.pgs.dp)
+
+    # ============================================================ step hooks
+    def _begin_microbatch(self, mb, num_mb):
+        final = mb == num_mb - 1 and state.core.pp_size() == 1
+        for r in self.reducers.values():
+            r.set_final(final)
+
+    def _mark_fwd_pass_done(self, mb):
+        pass
+
+    def _on_microbatch_done(self, mb):
+        pass
+
+    @contextlib.contextmanager
+    def _step(self):
+        sync = (self._backward_passes + 1) % self.backward_passes_per_step == 0 and torch.is_grad_enabled()
+        self.require_backward_grad_sync = sync
+        if self.partitioned:
+            for r in self.reducers.values():
+                r.sync_enabled = sync
+                r.prepare_for_backward()
+        self._step_had_backward = False
+        yield
+        if not self.partitioned:
+            return
+        if self._step_had_backward:
+            self._backward_passes += 1
+            if sync:
+                for r in self.reducers.values():
+                    r.synchronize()
+        for name, hook in list(self._post_step_hooks.items()):
+            if name not in self._post_step_hooks_run:
+                self._post_step_hooks_run.add(name)
+                hook(self, state.optimizer)
+        if state.core.pp_size() > 1:
+            state.comm.barrier(CommGroup.PP_GROUP)
+
+    # ============================================================ forward/backward
+    def forward(self, *args, **kwargs):
+        if state.core.pp_size() > 1 and not state.in_step_func and not state.is_tracing:
+            raise StepFunctionCalledError("with pipeline parallelism the model can only be called inside smp.step")
+        return self.module(*args, **kwargs)
+
+    def backward(self, tensors, grad_tensors=None):
+        if state.is_tracing:
+            return
+        if not state.in_step_func:
+            raise StepFunctionCalledError("model.backward must be called inside an smp.step function")
+        cfg = state.cfg
+        if not isinstance(tensors, (list, tuple)):
+            tensors = [tensors]
+            grad_tensors = [grad_tensors] if grad_tensors is not None else None
+        tensors = list(tensors)
+        if cfg.fp16 or cfg.bf16 or cfg.fp16_params:
+            tensors = [t.float() if t.dtype != torch.float32 else t for t in tensors]
+        if grad_tensors is None:
+            grad_tensors = [torch.ones_like(t) if t.numel() == 1 else None for t in tensors]
+        if (cfg.fp16 or cfg.fp16_params) and state.optimizer is not None:
+            scale = state.optimizer.loss_scale
+            if scale != 1.0:
+                grad_tensors = [g * scale if g is not None else None for g in grad_tensors]
+        self._step_had_backward = True
+        if state.core.pp_size() == 1:
+            torch.autograd.backward(tensors, grad_tensors)
+        else:
+            state.engine.backward_root(tensors, grad_tensors)
+
+    # ============================================================ local execution
+    def _call_local(self, module, args, kwargs):
+        from ..runtime.patch import call_original
+
+        return call_original(module, args, kwargs)
+
+    def _run_local_chain(self, seq, children, i, j, h):
+        from ..runtime.patch import run_local_chain
+
+        return run_local_chain(seq, children, i, j, h)
+
+    # ============================================================ views / queries
+    def local_modules(self):
+        mm = state.module_manager
+        me = state.core.pp_rank()
+        return [m for m in self.module.modules() if mm.get_partition(m) == me]
+
+    def local_named_modules(self):
+        mm = state.module_manager
+        me = state.core.pp_rank()
+        return [(n, m) for n, m in self.module.named_modules() if mm.get_partition(m) == me]
+
+    def local_parameters(self, recurse=True):
+        for _, p in self.local_named_parameters():
+            yield p
+
+    def local_named_parameters(self, recurse=True):
+        owner = getattr(self, "_param_owner", None)
+        me = state.core.pp_rank()
+        for n, p in self.module.named_parameters():
+            if owner is None or owner.get(p) == me:
+                yield n, p
+
+    def local_buffers(self):
+        for _, b in self.local_named_buffers():
+            yield b
+
+    def local_named_buffers(self):
+        mm = state.module_manager
+        me = state.core.pp_rank()
+        for mn, m in self.module.named_modules():
+            if mm.get_partition(m) == me:
+                for bn, b in m.named_buffers(recurse=False):
+                    yield (f"{mn}.{bn}" if mn else bn), b
+
+    def virtual_named_parameters(self):
+        opt = state.optimizer
+        if opt is None:
+            return []
+        return list(opt.virtual_named_parameters())
+
+    def is_local_parameter(self, p):
+        owner = getattr(self, "_param_owner", None)
+        return owner is None or owner.get(p) == state.core.pp_rank()
+
+    def is_local_buffer(self, b):
+        return any(b is x for x in self.local_buffers())
+
+    def is_distributed_parameter(self, p):
+        return getattr(p, "_smp_distributed", False)
+
+    def is_distributed_buffer(self, b):
+        return getattr(b, "_smp_distributed", False)
+
+    def is_scaled_batch_parameter(self, p):
+        return _is_scaled_batch(p)
+
+    def is_scaled_batch_buffer(self, b):
+        return getattr(b, "_smp_scaled_batch", False)
+
+    def distributed_modules(self):
+        mm = state.module_manager
+        return [m for m in self.module.modules() if mm.is_distributed(m)]
+
+    def size(self):
+        return sum(p.numel() * p.element_size() for p in self.module.parameters())
+
+    def get_module(self):
+        return self.module
+
+    def get_param_name(self, param):
+        for n, p in self.module.named_parameters():
+            if p is param:
+                return n
+        return None
+
+    # ============================================================ hooks / ddp api
+    def register_post_partition_hook(self, hook):
+        handle = len(self._post_partition_hooks)
+        self._post_partition_hooks[handle] = hook
+        if self.partitioned:
+            hook(self, state.optimizer)
+        return handle
+
+    def register_post_step_hook(self, hook):
+        handle = f"hook{len(self._post_step_hooks)}"
+        self._post_step_hooks[handle] = hook
+        return handle
+
+    def register_comm_hook(self, state_obj, hook):
+        """DDP-style comm hook: hook(state, bucket) -> Future/Work; bucket.buffer() is the
+        flat gradient slice."""
+
+        def adapter(b, buf):
+            class _B:
+                def buffer(self_inner):
+                    return buf
+
+                def index(self_inner):
+                    return b.index
+
+            return hook(state_obj, _B())
+
+        self._comm_hook = adapter
+        for r in self.reducers.values():
+            r.comm_hook = adapter
+
+    def _register_builtin_comm_hook(self, comm_hook_type):
+        name = str(comm_hook_type)
+        if "FP16" in name.upper() or "BF16" in name.upper():
+            dt = torch.bfloat16 if "BF16" in name.upper() else torch.float16
+
+            def compress(b, buf):
+                tmp = buf.to(dt)
+                w = dist.all_reduce(tmp, group=None, async_op=True)
+
+                class _W:
+                    def wait(self_inner):
+                        w.wait()
+                        buf.copy_(tmp)
+
+                return _W()
+
+            self._comm_hook = compress
+            for r in self.reducers.values():
+                r.comm_hook = compress
+
+    @contextlib.contextmanager
+    def join(self, *args, **kwargs):
+        yield
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def get_ddp_logging_data(self):
+        return {
+            "bucket_cap_mb": self.bucket_cap_mb,
+            "num_buckets": {k: len(f.buckets) for k, f in self.flat_groups.items()},
+            "overlapping_allreduce": self.overlapping_allreduce,
+        }
+
+    # ============================================================ state dicts
+    def local_state_dict(self, *args, **kwargs):
+        from .checkpoint_utils import model_local_state_dict
+
+        return model_local_state_dict(self)
+
+    def state_dict(self, *args, gather_to_rank0=True, cast_to_cpu=True, **kwargs):
+        from .checkpoint_utils import model_full_state_dict
+
+        return model_full_state_dict(self, gather_to_rank0=gather_to_rank0, cast_to_cpu=cast_to_cpu)
+
+    def load_state_dict(self, state_dict, strict=True, translate_function=None, same_partition_load=False):
+        from .checkpoint_utils import model_load_state_dict
+
+        if not self.partitioned:
+            self._deferred_load = {"model": state_dict, "kwargs": dict(strict=strict, translate_function=translate_function,
+                                                                       same_partition_load=same_partition_load)}
+            return
+        return model_load_state_dict(self, state_dict, strict=strict, translate_function=translate_function,
+                                     same_partition_load=same_partition_load)
+
+    def display_partition(self):
+        mm = state.module_manager
+        for n, m in self.module.named_modules():
+            logger.info(f"{n or 'main'}: partition {mm.get_partition(m)}")
+
+    def load_saved_partition(self, partition_info):
+        state.module_manager.load_partition(partition_info)
+        self._partitions_assigned = True
+
+    def cpu(self):
+        return self
+
+    def cuda(self, *args, **kwargs):
+        if not self.partitioned:
+            logger.warning("model.cuda() before partitioning is ignored; local modules move after partitioning")
+        return self
+
+    def to(self, *args, **kwargs):
+        if not self.partitioned:
+            logger.warning("model.to() before partitioning is ignored; local modules move after partitioning")
+        return self
+
+
+@contextlib.contextmanager
+def model_creation(tensor_parallelism=False, dtype=None, distribute_embedding=False, **tp_config):
+    """Context for building a model: TP marking + default dtype (reference `model.py:79-107`)."""
+    mm = state.module_manager
+    prev_dtype = torch.get_default_dtype()
+    if dtype is not None:
+        torch.set_default_dtype(dtype)
+    cfg = dict(tp_config)
+    if distribute_embedding:
+        cfg["distribute_embedding"] = True
+    try:
+        if mm is not None:
+            with mm.tensor_parallelism(tensor_parallelism, **cfg):
+                yield
+        else:
+            yield
+    finally:
+        torch.set_default_dtype(prev_dtype)

@@ -1,0 +1,125 @@
+"""``@smp.step``: microbatch splitting + pipelined execution of a training/eval step.
+
+Reference parity: `smp/torch/step.py:53-357` -- ``step(non_split_inputs,
+input_split_axes, detach_outputs)``, the StepFunction call sequence (timeline, model
+``_step`` context, split on pp_rank 0 / serve on others, StepOutput of per-microbatch
+results), and the optional per-step memory metrics file (``SMP_WRITE_STEP_MEMORY_METRICS``).
+"""
+import functools
+import os
+
+import torch
+
+from ..backend.exceptions import DistributedModelNotWrappedError, SMPInvalidArgumentError
+from ..backend.logger import get_logger
+from ..backend.split import StepOutput, TensorSplitter
+from .state_mod import state
+
+logger = get_logger()
+
+
+class PTTensorSplitter(TensorSplitter):
+    def is_tensor(self, x):
+        return isinstance(x, torch.Tensor)
+
+    def tensor_size(self, x, axis):
+        return x.size(axis)
+
+    def slice_tensor(self, x, num_mb, mb, axis):
+        size = x.size(axis) // num_mb
+        return x.narrow(axis, mb * size, size)
+
+
+class StepMemoryMetricsCollector:
+    """Appends per-step peak memory to ``smp_step_memory_metrics_rank{r}.txt``."""
+
+    def __init__(self):
+        self.enabled = os.environ.get("SMP_WRITE_STEP_MEMORY_METRICS", "0") == "1"
+        self.path = None
+
+    def record(self, step):
+        if not self.enabled or not state.use_gpu:
+            return
+        if self.path is None:
+            self.path = f"smp_step_memory_metrics_rank{state.core.rank()}.txt"
+        dev = state.device
+        line = (
+            f"step={step} peak_allocated_MB={torch.cuda.max_memory_allocated(dev) / 2**20:.1f} "
+            f"peak_reserved_MB={torch.cuda.max_memory_reserved(dev) / 2**20:.1f}"
+        )
+        with open(self.path, "a") as f:
+            f.write(line + "\n")
+        torch.cuda.reset_peak_memory_stats(dev)
+
+
+class StepFunction:
+    _next_id = 0
+
+    def __init__(self, func, non_split_inputs=None, input_split_axes=None, detach_outputs=True):
+        functools.update_wrapper(self, func)
+        self.func = func
+        self.id = StepFunction._next_id
+        StepFunction._next_id += 1
+        self.splitter = PTTensorSplitter(func, non_split_inputs, input_split_axes)
+        self.detach_outputs = detach_outputs
+        self.memory_metrics = StepMemoryMetricsCollector()
+        state.step_func[self.id] = self
+
+    def __call__(self, *args, **kwargs):
+        if not state.initialized:
+            raise SMPInvalidArgumentError("smp.init() must be called before an smp.step function")
+        if state.model is None:
+            raise DistributedModelNotWrappedError("the model must be wrapped in smp.DistributedModel before calling an smp.step function")
+        state.current_step_fn_id = self.id
+        core = state.core
+        core.timeline_start_step(state.step_count)
+        num_mb = state.cfg.microbatches
+        state.in_step_func = True
+        try:
+            with state.model._step():
+                if core.pp_rank() == 0:
+                    mb_inputs = self.splitter.split(args, kwargs, num_mb)
+                else:
+                    mb_inputs = None
+                outputs = state.engine.run_step(self, mb_inputs)
+        finally:
+            state.in_step_func = False
+            core.timeline_end_step()
+        state.step_count += 1
+        self.memory_metrics.record(state.step_count)
+        if outputs is None:
+            return None
+        return StepOutput(outputs)
+
+    def run_microbatch(self, mb, mb_args, mb_kwargs):
+        """Executes the user function on one microbatch (called by the engine)."""
+        out = self.func(*mb_args, **mb_kwargs)
+        if self.detach_outputs:
+            out = _detach(out)
+        return out
+
+
+def _detach(obj):
+    if isinstance(obj, torch.Tensor):
+        return obj.detach()
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        return type(obj)(*[_detach(o) for o in obj])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_detach(o) for o in obj)
+    if isinstance(obj, dict):
+        try:
+            return type(obj)((k, _detach(v)) for k, v in obj.items())
+        except TypeError:
+            return {k: _detach(v) for k, v in obj.items()}
+    return obj
+
+
+def step(func=None, *, non_split_inputs=None, input_split_axes=None, detach_outputs=True):
+    """Decorator. Usable as ``@smp.step`` or ``@smp.step(non_split_inputs=[...])``."""
+    if func is not None and callable(func):
+        return StepFunction(func)
+
+    def deco(f):
+        return StepFunction(f, non_split_inputs, input_split_axes, detach_outputs)
+
+    return deco

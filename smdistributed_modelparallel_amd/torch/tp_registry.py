@@ -1,0 +1,113 @@
+"""Tensor-parallelism registry.
+
+Reference parity (`smp/torch/tp_registry.py:164-310`): a registered module class has its
+``__init__`` patched to record constructor arguments; when a module of that class is
+marked for TP, ``distribute`` builds the distributed counterpart from the (optionally
+``init_hook``-translated) arguments plus TP-config overrides, and wraps its forward with
+``forward_hook`` (user-module call signature -> distributed-module inputs) and
+``return_hook`` (distributed outputs -> user-module outputs).  ``translate_functions``
+(smp<->HF state-dict converters) are collected for checkpointing.
+"""
+import functools
+import inspect
+
+import torch.nn as nn
+
+from ..backend.logger import get_logger
+
+logger = get_logger()
+
+
+class _Entry:
+    def __init__(self, dist_cls, init_hook, forward_hook, return_hook):
+        self.dist_cls = dist_cls
+        self.init_hook = init_hook
+        self.forward_hook = forward_hook
+        self.return_hook = return_hook
+
+
+class TensorParallelismRegistry:
+    def __init__(self):
+        self._entries = {}
+        self._patched = {}
+        self.translate_functions = []
+
+    def register_builtins(self):
+        from ..nn.embedding import DistributedEmbedding
+        from ..nn.linear import DistributedLinear
+
+        self.register(nn.Linear, DistributedLinear,
+                      init_hook=lambda in_f, out_f, bias=True, device=None, dtype=None: ((in_f, out_f), {"bias": bias}))
+        self.register(nn.Embedding, DistributedEmbedding,
+                      init_hook=lambda num, dim, *a, **k: ((num, dim), {}))
+        try:
+            from ..nn.huggingface.predefined_hooks import register_predefined_hooks
+
+            register_predefined_hooks(self)
+        except Exception as e:  # transformers absent or incompatible
+            logger.debug(f"HF predefined TP hooks not registered: {e}")
+
+    def register(self, module_cls, dist_cls, init_hook=None, forward_hook=None, return_hook=None,
+                 translate_functions=None):
+        self._entries[module_cls] = _Entry(dist_cls, init_hook, forward_hook, return_hook)
+        if translate_functions is not None:
+            self.translate_functions.append(tuple(translate_functions))
+        self._patch_init(module_cls)
+
+    def is_supported(self, cls):
+        return cls in self._entries
+
+    def _patch_init(self, cls):
+        if cls in self._patched:
+            return
+        orig = cls.__init__
+
+        @functools.wraps(orig)
+        def init(module, *args, **kwargs):
+            orig(module, *args, **kwargs)
+            if type(module) is cls:
+                module.__dict__["_smp_ctor_args"] = (args, kwargs)
+
+        cls.__init__ = init
+        self._patched[cls] = orig
+
+    def unpatch(self):
+        for cls, orig in self._patched.items():
+            cls.__init__ = orig
+        self._patched.clear()
+
+    def distribute(self, module, tp_config=None):
+        e = self._entries[type(module)]
+        args, kwargs = module.__dict__.get("_smp_ctor_args", ((), {}))
+        if e.init_hook is not None:
+            args, kwargs = e.init_hook(*args, **kwargs)
+        kwargs = dict(kwargs)
+        if tp_config:
+            accepted = _accepted_kwargs(e.dist_cls)
+            for k, v in tp_config.items():
+                if accepted is None or k in accepted:
+                    kwargs[k] = v
+        dist_mod = e.dist_cls(*args, **kwargs)
+        if e.forward_hook is not None or e.return_hook is not None:
+            fwd = dist_mod.forward
+            fh, rh = e.forward_hook, e.return_hook
+
+            def wrapped(*a, **k):
+                if fh is not None:
+                    a, k = fh(*a, **k)
+                out = fwd(*a, **k)
+                return rh(out) if rh is not None else out
+
+            dist_mod.forward = wrapped
+        dist_mod.training = module.training
+        return dist_mod
+
+
+def _accepted_kwargs(cls):
+    keys = getattr(cls, "_KEYS", None)
+    if keys is not None:
+        return set(keys)
+    try:
+        return set(inspect.signature(cls.__init__).parameters)
+    except (TypeError, ValueError):
+        return None

@@ -1,0 +1,186 @@
+"""Numerics of the CDNA4 HIP kernels against plain PyTorch fp32 references
+(reference test strategy: `smp/test/torch/test_kernels.py:14-86`)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DT = [torch.bfloat16, torch.float16, torch.float32]
+
+
+def _tol(dt):
+    return {torch.float32: 2e-5, torch.float16: 2e-3, torch.bfloat16: 2e-2}[dt]
+
+
+@pytest.fixture(scope="module")
+def C():
+    from smdistributed_modelparallel_amd.ops._ext import ext
+
+    return ext()
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("cols", [64, 1600, 4096, 1000, 12288])
+def test_layernorm_fwd_bwd(C, dt, cols):
+    from smdistributed_modelparallel_amd.ops.layernorm import layer_norm
+
+    torch.manual_seed(0)
+    x = torch.randn(37, cols, device="cuda", dtype=dt, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(cols, device="cuda", dtype=dt)).requires_grad_()
+    b = (0.1 * torch.randn(cols, device="cuda", dtype=dt)).requires_grad_()
+    y = layer_norm(x, w, b, 1e-5)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (cols,), wr, br, 1e-5)
+    tol = _tol(dt) * 4
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 4, rtol=tol * 4)
+    assert torch.allclose(w.grad.float(), wr.grad, atol=tol * 40, rtol=tol * 4)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40, rtol=tol * 4)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_add_layernorm(C, dt):
+    from smdistributed_modelparallel_amd.ops.layernorm import add_layer_norm
+
+    torch.manual_seed(1)
+    x = torch.randn(64, 1600, device="cuda", dtype=dt, requires_grad=True)
+    r = torch.randn(64, 1600, device="cuda", dtype=dt, requires_grad=True)
+    w = torch.ones(1600, device="cuda", dtype=dt, requires_grad=True)
+    b = torch.zeros(1600, device="cuda", dtype=dt, requires_grad=True)
+    y, s = add_layer_norm(x, r, w, b)
+    xr, rr = x.detach().float().requires_grad_(), r.detach().float().requires_grad_()
+    sr = xr + rr
+    yr = torch.nn.functional.layer_norm(sr, (1600,), w.detach().float(), b.detach().float())
+    tol = _tol(dt) * 4
+    assert torch.allclose(s.float(), sr, atol=tol, rtol=tol)
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    gy, gs = torch.randn_like(yr), torch.randn_like(sr)
+    torch.autograd.backward([y, s], [gy.to(dt), gs.to(dt)])
+    torch.autograd.backward([yr, sr], [gy, gs])
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 4, rtol=tol * 4)
+    assert torch.allclose(r.grad.float(), rr.grad, atol=tol * 4, rtol=tol * 4)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_bias_gelu(C, dt):
+    from smdistributed_modelparallel_amd.ops.gelu import _gelu_tanh_ref, bias_gelu
+
+    torch.manual_seed(2)
+    x = torch.randn(33, 6400, device="cuda", dtype=dt, requires_grad=True)
+    b = torch.randn(6400, device="cuda", dtype=dt, requires_grad=True)
+    y = bias_gelu(x, b)
+    xr, br = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
+    yr = _gelu_tanh_ref(xr + br)
+    tol = _tol(dt) * 2
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50, rtol=tol * 4)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("sk", [128, 1024, 2048, 4096, 20000])
+def test_causal_softmax(C, dt, sk):
+    from smdistributed_modelparallel_amd.ops.softmax import _ref_softmax, scaled_causal_softmax
+
+    torch.manual_seed(3)
+    b, h = (2, 4) if sk <= 4096 else (1, 1)
+    sq = sk if sk <= 4096 else 64
+    x = torch.randn(b, h, sq, sk, device="cuda", dtype=dt, requires_grad=True)
+    y = scaled_causal_softmax(x, 0.125)
+    xr = x.detach().float().requires_grad_()
+    yr = _ref_softmax(xr, None, 0.125, True)
+    assert torch.allclose(y.float(), yr, atol=1e-3 if dt == torch.float16 else 4e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dt))
+    yr.backward(g)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=2e-3 if dt == torch.float16 else 1e-2)
+
+
+def test_masked_softmax(C):
+    from smdistributed_modelparallel_amd.ops.softmax import _ref_softmax, scaled_masked_softmax
+
+    torch.manual_seed(4)
+    x = torch.randn(4, 16, 1024, 1024, device="cuda", dtype=torch.float16)
+    mask = (torch.rand(4, 1, 1024, 1024, device="cuda") < 0.2).to(torch.uint8)
+    y = scaled_masked_softmax(x, mask, 1.0)
+    yr = _ref_softmax(x.float(), mask, 1.0, False)
+    assert torch.allclose(y.float(), yr, atol=1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("vocab", [50257, 1024, 12563])
+def test_cross_entropy(C, dt, vocab):
+    from smdistributed_modelparallel_amd.ops.cross_entropy import cross_entropy
+
+    torch.manual_seed(5)
+    logits = torch.randn(61, vocab, device="cuda", dtype=dt, requires_grad=True)
+    tgt = torch.randint(0, vocab, (61,), device="cuda")
+    tgt[3] = -100
+    loss = cross_entropy(logits, tgt)
+    lr = logits.detach().float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lr, tgt, ignore_index=-100)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    assert torch.allclose(logits.grad.float(), lr.grad, atol=1e-4 if dt == torch.float32 else 2e-4)
+
+
+@pytest.mark.parametrize("pdt", [torch.bfloat16, None])
+def test_fused_adam(C, pdt):
+    from smdistributed_modelparallel_amd.ops.multi_tensor import fused_adam_
+
+    torch.manual_seed(6)
+    n = 100003
+    master = torch.randn(n, device="cuda")
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    ref = master.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    low = master.to(pdt) if pdt is not None else None
+    for step in range(1, 4):
+        g = torch.randn(n, device="cuda")
+        gl = g.to(pdt) if pdt is not None else g
+        fused_adam_(low, gl, master, m, v, 1e-3, 0.9, 0.95, 1e-8, 0.1, step, grad_scale=1.0, adamw=True)
+        ref.grad = gl.float()
+        opt.step()
+    assert torch.allclose(master, ref.detach(), atol=1e-5, rtol=1e-5)
+    if low is not None:
+        assert torch.allclose(low.float(), master, atol=1e-2)
+
+
+def test_sumsq_nonfinite(C):
+    from smdistributed_modelparallel_amd.ops.multi_tensor import nonfinite_flag, sumsq
+
+    x = torch.randn(1 << 20, device="cuda", dtype=torch.bfloat16)
+    assert math.isclose(sumsq(x).item(), x.float().pow(2).sum().item(), rel_tol=1e-3)
+    assert nonfinite_flag(x).item() == 0.0
+    x[12345] = float("inf")
+    assert nonfinite_flag(x).item() == 1.0
+
+
+def test_gpt_step_gpu(C):
+    """End-to-end: tiny GPT forward/backward on GPU through the kernels matches fp32 CPU."""
+    from smdistributed_modelparallel_amd.models import build_gpt
+
+    torch.manual_seed(7)
+    m = build_gpt("gpt2-tiny", dropout=0.0, hidden_size=128, num_attention_heads=2, attention_head_size=64,
+                  intermediate_size=512)
+    ids = torch.randint(0, 512, (2, 64))
+    loss_cpu, _ = m((ids, None, None, None, ids))
+    loss_cpu.backward()
+    g_cpu = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    m = m.cuda()
+    loss_gpu, _ = m((ids.cuda(), None, None, None, ids.cuda()))
+    loss_gpu.backward()
+    assert abs(loss_gpu.item() - loss_cpu.item()) < 1e-3
+    for n, p in m.named_parameters():
+        assert torch.allclose(p.grad.cpu(), g_cpu[n], atol=2e-3, rtol=1e-2), n
