@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--microbatches", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--no-flash", action="store_true")
     ap.add_argument("--activation-checkpointing", action="store_true")
     ap.add_argument("--shard-optimizer-state", action="store_true")

@@ -300,6 +300,87 @@ at::Tensor xent_bwd(at::Tensor logits, at::Tensor target, at::Tensor lse, at::Te
   return d;
 }
 
+// ------------------------------------------------------------------- attention
+// q, k, v: [b, s, h, d] with the last dim contiguous (other strides arbitrary, e.g. views
+// of a fused [b, s, 3, h, d] QKV projection).
+void check_bshd(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4 && t.stride(3) == 1, n, " must be a GPU [b, s, h, d] tensor with contiguous d");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, n, " must be bf16/fp16");
+}
+
+smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool causal,
+                             int64_t window) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2) && q.size(3) == k.size(3),
+              "attention: q/k/v shape mismatch");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attention: dtype mismatch");
+  TORCH_CHECK(q.size(3) == 64 || q.size(3) == 128, "attention kernel supports head_dim 64 and 128");
+  for (const at::Tensor* t : {&q, &k, &v})
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0 && t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
+                    t->stride(0) % 8 == 0,
+                "attention: operands must be 16-byte aligned");
+  smpk::AttnParams p{};
+  p.q = q.data_ptr();
+  p.k = k.data_ptr();
+  p.v = v.data_ptr();
+  p.b = q.size(0);
+  p.sq = q.size(1);
+  p.h = q.size(2);
+  p.d = q.size(3);
+  p.sk = k.size(1);
+  p.q_sb = q.stride(0), p.q_ss = q.stride(1), p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0), p.k_ss = k.stride(1), p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0), p.v_ss = v.stride(1), p.v_sh = v.stride(2);
+  p.scale = static_cast<float>(scale);
+  p.causal = causal ? 1 : 0;
+  p.window = static_cast<int>(window);
+  return p;
+}
+
+std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale, bool causal,
+                                      int64_t window) {
+  auto p = attn_params(q, k, v, scale, causal, window);
+  auto o = at::empty({p.b, p.sq, p.h, p.d}, q.options());
+  auto lse = at::empty({p.b, p.h, p.sq}, q.options().dtype(at::kFloat));
+  p.o = o.data_ptr();
+  p.o_sb = o.stride(0), p.o_ss = o.stride(1), p.o_sh = o.stride(2);
+  p.lse = lse.data_ptr<float>();
+  check(smpk::attention_fwd(dt_code(q), p, stream()), "attention_fwd");
+  return {o, lse};
+}
+
+// Writes into the provided dq/dk/dv (may be views of one packed gradient buffer).
+void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                        at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window) {
+  smpk::AttnBwdParams P{};
+  P.f = attn_params(q, k, v, scale, causal, window);
+  check_bshd(dout, "dout");
+  check_bshd(o, "o");
+  check_bshd(dq, "dq");
+  check_bshd(dk, "dk");
+  check_bshd(dv, "dv");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes() &&
+                  dk.sizes() == k.sizes() && dv.sizes() == v.sizes(),
+              "attention_bwd: shape mismatch");
+  P.f.o = o.data_ptr();
+  P.f.o_sb = o.stride(0), P.f.o_ss = o.stride(1), P.f.o_sh = o.stride(2);
+  P.f.lse = lse.data_ptr<float>();
+  P.dout = dout.data_ptr();
+  P.do_sb = dout.stride(0), P.do_ss = dout.stride(1), P.do_sh = dout.stride(2);
+  P.dq = dq.data_ptr();
+  P.dk = dk.data_ptr();
+  P.dv = dv.data_ptr();
+  P.dq_sb = dq.stride(0), P.dq_ss = dq.stride(1), P.dq_sh = dq.stride(2);
+  P.dk_sb = dk.stride(0), P.dk_ss = dk.stride(1), P.dk_sh = dk.stride(2);
+  P.dv_sb = dv.stride(0), P.dv_ss = dv.stride(1), P.dv_sh = dv.stride(2);
+  auto delta = at::empty({P.f.b, P.f.h, P.f.sq}, q.options().dtype(at::kFloat));
+  P.delta = delta.data_ptr<float>();
+  P.dq_acc = nullptr;
+  check(smpk::attention_bwd(dt_code(q), P, stream()), "attention_bwd");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -324,4 +405,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scaled_softmax_bwd", &scaled_softmax_bwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("attention_fwd", &attention_fwd);
+  m.def("attention_bwd_into", &attention_bwd_into);
 }

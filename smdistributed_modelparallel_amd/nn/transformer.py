@@ -31,6 +31,7 @@ import torch.nn.functional as F
 
 from ..backend.exceptions import SMPInvalidArgumentError
 from ..ops.attention import attention as attention_op
+from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
 from ..ops.gelu import bias_gelu
 from ..ops.rope import apply_rotary
@@ -239,6 +240,14 @@ class DistributedAttentionLayer(DistributedModule):
             qkv = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
+            if not self.rotary_dim and mask is None and not self.attention_in_fp32:
+                ctx = attention_packed(
+                    qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
+                    window=self.window_size, training=self.training,
+                    use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
+                )
+                out = F.linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
+                return fwd_allreduce_for_tp(out)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)

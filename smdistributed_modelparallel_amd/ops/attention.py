@@ -45,8 +45,41 @@ class _FlashAttention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = ext().attention_bwd(do.contiguous(), q, k, v, o, lse, ctx.scale, ctx.causal, ctx.window)
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window)
         return dq, dk, dv, None, None, None
+
+
+class _FlashAttentionPacked(torch.autograd.Function):
+    """Self-attention straight from the fused QKV projection output [b, s, 3, h, d]:
+    the backward writes dQ/dK/dV into one packed gradient (no scatter/zero-fill copies)."""
+
+    @staticmethod
+    def forward(ctx, qkv, scale, causal, window):
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        o, lse = ext().attention_fwd(q, k, v, scale, causal, window)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.scale, ctx.causal, ctx.window = scale, causal, window
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        dqkv = torch.empty_like(qkv)
+        ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
+                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window)
+        return dqkv, None, None, None
+
+
+def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, training=True, use_flash=True):
+    """qkv: [b, s, 3, h, d] -> [b, s, h, d]."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    q = qkv[:, :, 0]
+    if use_flash and flash_supported(q, dropout_p if training else 0.0, None):
+        return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0))
+    return attention(q, qkv[:, :, 1], qkv[:, :, 2], causal=causal, scale=scale, dropout_p=dropout_p, window=window,
+                     training=training, use_flash=use_flash)
 
 
 def _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, fp32):
