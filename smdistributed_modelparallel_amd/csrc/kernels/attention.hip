@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(kThreads) attn_delta_kernel(AttnBwdParams p) {
 
 // ===================================================================== dK / dV
 template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kThreads, 1) attn_bwd_dkdv_kernel(AttnBwdParams P) {
+__global__ void __launch_bounds__(kThreads, 2) attn_bwd_dkdv_kernel(AttnBwdParams P) {
   constexpr int BKEYS = 128, BQ = 64, LD = D + 8;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[BQ * LD];
   __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * LD];
@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(kThreads, 1) attn_bwd_dkdv_kernel(AttnBwdParam
     }
     __syncthreads();
     if (CAUSAL && qt + BQ - 1 + diag < k0w) continue;  // whole tile sees none of this wave's keys
-#pragma unroll
+#pragma unroll 1
     for (int sub = 0; sub < 2; ++sub) {
       // S = Q K^T, dP = dO V^T for 32 queries x 32 keys (query rows in regs, key on lane)
       f32x16 s = f32x16{0}, dp = f32x16{0};
