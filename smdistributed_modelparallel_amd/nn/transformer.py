@@ -21,6 +21,7 @@ MI355X choices:
 * LayerNorm, residual-add+LayerNorm, bias+GeLU and the LM-head cross entropy are fused
   HIP kernels (see ``ops/``).
 """
+import functools
 import math
 import warnings
 from collections import OrderedDict
@@ -123,7 +124,31 @@ def _param_dtype():
 
 
 class DistributedModule(nn.Module):
-    """Base of every smp.nn distributed module (reference `nn/dist_module.py:5-32`)."""
+    """Base of every smp.nn distributed module (reference `nn/dist_module.py:5-32`).
+
+    Sub-modules created inside a distributed module's constructor are never themselves
+    marked for tensor parallelism (they are already the distributed implementation)."""
+
+    def __init_subclass__(cls, **kwargs):
+        super().__init_subclass__(**kwargs)
+        orig = cls.__dict__.get("__init__")
+        if orig is None:
+            return
+
+        @functools.wraps(orig)
+        def init(self, *a, **k):
+            from ..runtime.module_manager import DIST_CTOR_DEPTH
+
+            DIST_CTOR_DEPTH[0] += 1
+            # the TP degree is fixed at construction: modules built before smp.init (or
+            # outside the distributed path) stay unsharded and never communicate
+            self.__dict__["_tp"] = tp_size()
+            try:
+                orig(self, *a, **k)
+            finally:
+                DIST_CTOR_DEPTH[0] -= 1
+
+        cls.__init__ = init
 
     def can_distribute(self, *args, **kwargs):
         return True
@@ -193,14 +218,14 @@ class DistributedAttentionLayer(DistributedModule):
         self.reset_parameters()
         for p in self.parameters():
             mark_scaled_batch(p)
-        mark_tp(self.qkv_weight, 0, n_proj)
+        mark_tp(self.qkv_weight, 0, n_proj, unit=d)
         if self.qkv_bias is not None:
-            mark_tp(self.qkv_bias, 0, n_proj)
+            mark_tp(self.qkv_bias, 0, n_proj, unit=d)
         if self.cross_attention:
-            mark_tp(self.kv_weight, 0, 2)
+            mark_tp(self.kv_weight, 0, 2, unit=d)
             if self.kv_bias is not None:
-                mark_tp(self.kv_bias, 0, 2)
-        mark_tp(self.dense_weight, 1)
+                mark_tp(self.kv_bias, 0, 2, unit=d)
+        mark_tp(self.dense_weight, 1, unit=d)
         if self.dense_bias is not None:
             mark_tp(self.dense_bias, None, rank0_only=True)
 
@@ -227,12 +252,12 @@ class DistributedAttentionLayer(DistributedModule):
     def core(self, a, mask=None, cross_states=None, cross_mask=None):
         """a: [B, s, h] (already normalised). Returns the dense output after the TP
         all-reduce (bias included), [B, s, h]."""
-        a = bwd_allreduce_for_tp(a)
+        a = (bwd_allreduce_for_tp(a) if self._tp > 1 else a)
         B, s, _ = a.shape
         lh, d = self.local_heads, self.attention_head_size
         if self.cross_attention:
             q = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, lh, d)
-            c = bwd_allreduce_for_tp(cross_states)
+            c = (bwd_allreduce_for_tp(cross_states) if self._tp > 1 else cross_states)
             kv = F.linear(c, self.kv_weight, self.kv_bias).view(B, c.shape[1], 2, lh, d)
             k, v = kv[:, :, 0], kv[:, :, 1]
             causal, mask = False, cross_mask
@@ -247,7 +272,7 @@ class DistributedAttentionLayer(DistributedModule):
                     use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
                 )
                 out = F.linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
-                return fwd_allreduce_for_tp(out)
+                return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
@@ -260,7 +285,7 @@ class DistributedAttentionLayer(DistributedModule):
         )
         ctx = ctx.reshape(B, s, lh * d)
         out = F.linear(ctx, self.dense_weight, self.dense_bias)
-        return fwd_allreduce_for_tp(out)
+        return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 
     def forward(self, inputs):
         if self.cross_attention:
@@ -268,14 +293,14 @@ class DistributedAttentionLayer(DistributedModule):
         else:
             hidden, mask = inputs[0], inputs[1]
             cross_states = cross_mask = None
-        if tp_size() > 1 and self.input_layer and not _prescaled():
+        if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = allgather_for_tp(hidden, 0)
             mask = _gather_mask(mask)
         a = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
         out = self.dropout(self.core(a, mask, cross_states, cross_mask)) + hidden
         if self.post_layernorm:
             out = self.layernorm(out)
-        if tp_size() > 1 and self.output_layer and not _prescaled():
+        if self._tp > 1 and self.output_layer and not _prescaled():
             out = narrow_for_tp(out, 0)
         return (out,) + tuple(inputs[1:])
 
@@ -335,20 +360,20 @@ class DistributedTransformerOutputLayer(DistributedModule):
                 self.dense2_bias.zero_()
 
     def core(self, m):
-        m = bwd_allreduce_for_tp(m)
+        m = (bwd_allreduce_for_tp(m) if self._tp > 1 else m)
         x = F.linear(m, self.dense1_weight)
         x = _activation(x, self.activation, self.dense1_bias)
         out = F.linear(x, self.dense2_weight, self.dense2_bias)
-        return fwd_allreduce_for_tp(out)
+        return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 
     def forward(self, hidden):
-        if tp_size() > 1 and self.input_layer and not _prescaled():
+        if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = allgather_for_tp(hidden, 0)
         m = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
         out = self.dropout(self.core(m)) + hidden
         if self.post_layernorm:
             out = self.layernorm(out)
-        if tp_size() > 1 and self.output_layer and not _prescaled():
+        if self._tp > 1 and self.output_layer and not _prescaled():
             out = narrow_for_tp(out, 0)
         return out
 
@@ -382,7 +407,7 @@ class DistributedTransformerLayer(DistributedModule):
 
     def forward(self, inputs):
         hidden, mask = inputs[0], inputs[1]
-        if tp_size() > 1 and self.input_layer and not _prescaled():
+        if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = allgather_for_tp(hidden, 0)
             mask = _gather_mask(mask)
         at, out = self.attention, self.output
@@ -414,7 +439,7 @@ class DistributedTransformerLayer(DistributedModule):
             hidden = out.dropout(out.core(m)) + hidden
             if out.post_layernorm:
                 hidden = out.layernorm(hidden)
-        if tp_size() > 1 and self.output_layer and not _prescaled():
+        if self._tp > 1 and self.output_layer and not _prescaled():
             hidden = narrow_for_tp(hidden, 0)
         return (hidden,) + tuple(inputs[1:])
 
@@ -533,7 +558,7 @@ class DistributedTransformerLMHead(DistributedModule):
         if self.causal_mask_size is None and attention_mask is not None:
             mask = (attention_mask.view(B, -1) == 0).view(B, 1, 1, -1).expand(B, 1, s, s)
 
-        prescaled = _prescaled() and tp_size() > 1
+        prescaled = _prescaled() and self._tp > 1
         if prescaled and not self.distribute_embedding:
             input_ids, position_ids, token_type_ids = shard_sequence(input_ids, position_ids, token_type_ids,
                                                                      bwd_allgather=False)
@@ -555,7 +580,7 @@ class DistributedTransformerLMHead(DistributedModule):
             hidden = self.layernorm(hidden)
 
         if self.distribute_embedding:
-            hidden = bwd_allreduce_for_tp(hidden)
+            hidden = (bwd_allreduce_for_tp(hidden) if self._tp > 1 else hidden)
             logits = F.linear(hidden, self.word_embedding.weight)
             if labels is None:
                 return self.word_embedding.gather_vocab(logits)
@@ -564,7 +589,7 @@ class DistributedTransformerLMHead(DistributedModule):
             shift_logits = logits[..., :-1, :]
             shift_labels = labels[..., 1:]
             rows = cross_entropy(shift_logits, shift_labels, vocab_start=self.word_embedding.vocab_start_idx,
-                                 group=tp_group() if tp_size() > 1 else None, reduction="none")
+                                 group=tp_group() if self._tp > 1 else None, reduction="none")
             return rows.mean(), shift_logits
 
         if prescaled:

@@ -306,14 +306,16 @@ def is_scaled_batch(param):
     return getattr(param, "_smp_scaled_batch", False)
 
 
-def mark_tp(param, axis, groups=1, rank0_only=False):
+def mark_tp(param, axis, groups=1, rank0_only=False, unit=1):
     """Record how a parameter is split across the TP group, for checkpoint merge/slice:
     `axis` the sharded dim (None = replicated), `groups` > 1 when the full tensor is
     `groups` concatenated blocks each sharded separately (fused QKV), `rank0_only` for
-    row-parallel biases that exist only on tp_rank 0."""
+    row-parallel biases that exist only on tp_rank 0, `unit` the split granularity
+    (head_dim for attention projections: heads are split, not rows)."""
     param._smp_tp_axis = axis
     param._smp_tp_groups = groups
     param._smp_tp_rank0_only = rank0_only
+    param._smp_tp_unit = unit
     return param
 
 

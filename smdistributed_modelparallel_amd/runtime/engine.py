@@ -165,6 +165,10 @@ class PipelineEngine:
             self.pipeline = create_pipeline(cfg.pipeline, n, cfg.active_microbatches)
         try:
             self._serve(leader)
+        except SMPRuntimeError:
+            raise
+        except BaseException as e:  # noqa: B902 - tell the other stages before dying
+            self._abort(e)
         finally:
             self.state.transport.drain()
         outs = [self.results[i] for i in range(n)]
@@ -209,7 +213,7 @@ class PipelineEngine:
     def _spawn(self, fn, mb, kind, *args):
         w = _Worker(None, mb, kind)
 
-        def run():
+        def run(*_ignored):
             try:
                 w.result = fn(*args)
             except BaseException as e:  # noqa: B902 - re-raised in the server
@@ -472,6 +476,7 @@ class PipelineEngine:
             raise PipelineParallelBWDError(f"no saved tensors for {key} (mb {mb}) on rank {self.core.rank()}")
         tid = self._new_token(src, remote_token, mb)
         self.state.microbatch = mb
+        self.state.model._step_had_backward = True
         self._run_backward(tid, mb, saved, grads)
         self._maybe_finish(tid)
 

@@ -21,6 +21,9 @@ from ..backend.logger import get_logger
 
 logger = get_logger()
 
+# >0 while a DistributedModule constructor runs (its children are not TP-marked)
+DIST_CTOR_DEPTH = [0]
+
 
 class CheckpointConfig:
     def __init__(self, enabled=False, preserve_rng_state=True, module_name=None, strategy="each"):
@@ -190,6 +193,8 @@ class ModuleManager:
             self._tp_enabled, self._current_tp_config = prev_e, prev_c
 
     def maybe_mark_for_tensor_parallelism(self, module, registry):
+        if DIST_CTOR_DEPTH[0] > 0:
+            return
         if self._tp_enabled and registry is not None and registry.is_supported(type(module)):
             self._tp_modules.add(module)
             self._tp_config[module] = dict(self._current_tp_config)

@@ -239,11 +239,11 @@ class ModulePartitioner:
             alloc[bi] += 1
         return alloc
 
-    def _plan(self, parent_cost, children, devices):
+    def _plan(self, parent_cost, children, devices, min_k=1):
         """Best (segments, alloc) for children over `devices` (devices[0] holds the parent)."""
         costs = [c.cost for c in children]
         best = None
-        for k in range(1, min(len(children), len(devices)) + 1):
+        for k in range(min(min_k, len(children)), min(len(children), len(devices)) + 1):
             segs = self.minmax_segments(costs, k)
             seg_costs = [sum(costs[a:b]) for a, b in segs]
             caps = [sum(c.count for c in children[a:b]) for a, b in segs]
@@ -271,7 +271,9 @@ class ModulePartitioner:
             for c in children:
                 self._assign_subtree(c, devices[0])
             return
-        segs, alloc = self._plan(0.0, children, devices)
+        # a group that already shares several devices must be split (k >= 2), otherwise
+        # the recursion would see the same (group, devices) again
+        segs, alloc = self._plan(0.0, children, devices, min_k=2)
         nxt = 0
         for (a, b), n in zip(segs, alloc):
             group = children[a:b]
@@ -354,14 +356,20 @@ def auto_partition(model, step_fn, mb_inputs):
             except Exception as e:  # tracing is an optimisation: fall back to structure only
                 logger.warning(f"tracing failed ({e}); partitioning from structure only")
                 trace = None
-        mp = ModulePartitioner(model.module, core.pp_size(), trace, cfg.memory_weight,
-                               model.trace_execution_times or trace is not None,
-                               model.trace_memory_usage or True)
-        assignment = mp.partition()
-        info = {mm.get_module_name(m): p for m, p in assignment.items() if mm.get_module_name(m) is not None}
+        try:
+            mp = ModulePartitioner(model.module, core.pp_size(), trace, cfg.memory_weight,
+                                   model.trace_execution_times or trace is not None,
+                                   model.trace_memory_usage or True)
+            assignment = mp.partition()
+            info = {mm.get_module_name(m): p for m, p in assignment.items() if mm.get_module_name(m) is not None}
+        except BaseException as e:  # noqa: B902 - every rank must learn about the failure
+            state.comm.broadcast({"__error__": repr(e)}, CommGroup.WORLD)
+            raise
         state.comm.broadcast(info, CommGroup.WORLD)
     else:
         info = state.comm.recv_broadcast(0, CommGroup.WORLD)
+        if "__error__" in info:
+            raise PartitionError(f"auto-partitioning failed on rank 0: {info['__error__']}")
     for name, p in info.items():
         mm._module_partitions[mm.get_module(name)] = p
     if core.rank() == 0:

@@ -31,18 +31,25 @@ def merge_tp_tensors(shards, axis, groups=1):
     return torch.cat([torch.cat([b[g] for b in blocks], dim=axis) for g in range(groups)], dim=axis)
 
 
-def slice_tp_tensor(full, axis, groups, tp_rank, tp_size, sizes=None):
+def slice_tp_tensor(full, axis, groups, tp_rank, tp_size, sizes=None, unit=1):
+    """This tp_rank's shard of a full tensor: uneven splits give the first `n % tp` ranks
+    one extra `unit` (e.g. one extra attention head of `unit` = head_dim rows)."""
     if axis is None:
         return full
     if groups == 1:
-        n = full.size(axis)
+        n = full.size(axis) // unit
         if sizes is None:
             base, rem = divmod(n, tp_size)
             sizes = [base + (1 if r < rem else 0) for r in range(tp_size)]
-        start = sum(sizes[:tp_rank])
-        return full.narrow(axis, start, sizes[tp_rank])
+        start = sum(sizes[:tp_rank]) * unit
+        return full.narrow(axis, start, sizes[tp_rank] * unit)
     blocks = full.chunk(groups, dim=axis)
-    return torch.cat([slice_tp_tensor(b, axis, 1, tp_rank, tp_size) for b in blocks], dim=axis)
+    return torch.cat([slice_tp_tensor(b, axis, 1, tp_rank, tp_size, unit=unit) for b in blocks], dim=axis)
+
+
+def slice_for_param(full, p, tp_rank, tp_size):
+    axis, groups, _ = _tp_meta(p)
+    return slice_tp_tensor(full, axis, groups, tp_rank, tp_size, unit=getattr(p, "_smp_tp_unit", 1))
 
 
 def model_local_state_dict(model):
@@ -127,8 +134,7 @@ def model_load_state_dict(model, sd, strict=True, translate_function=None, same_
                 continue
             t = sd[n]
             if not is_partial and core.tp_size() > 1:
-                axis, groups, r0 = _tp_meta(p)
-                t = slice_tp_tensor(t, axis, groups, core.tp_rank(), core.tp_size())
+                t = slice_for_param(t, p, core.tp_rank(), core.tp_size())
             if tuple(t.shape) != tuple(p.shape):
                 raise CheckpointingError(f"shape mismatch for {n}: checkpoint {tuple(t.shape)} vs model {tuple(p.shape)}")
             p.copy_(t.to(p.device, p.dtype))

@@ -1,0 +1,48 @@
+"""Multi-process launcher for CPU (gloo) distributed tests."""
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_workers(module, world, args=(), timeout=240, env_extra=None):
+    """Run `python -m tests.workers.<module> args...` on `world` ranks; returns outputs.
+    Raises AssertionError with the logs if any rank fails."""
+    port = free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ)
+        env.update(RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SMP_FORCE_CPU="1", SMP_LOG_LEVEL="warning",
+                   PYTHONPATH=ROOT + os.pathsep + env.get("PYTHONPATH", ""), OMP_NUM_THREADS="1",
+                   SMP_CONNECT_TIMEOUT="60")
+        if env_extra:
+            env.update({k: str(v) for k, v in env_extra.items()})
+        procs.append(subprocess.Popen([sys.executable, "-m", f"tests.workers.{module}", *map(str, args)], cwd=ROOT,
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs, failed = [], False
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            o = "TIMEOUT\n" + (p.communicate()[0] or "")
+            failed = True
+        outs.append(o)
+        if p.returncode != 0:
+            failed = True
+    if failed:
+        msg = "\n".join(f"===== rank {i} (rc={p.returncode}) =====\n{o[-6000:]}" for i, (p, o) in enumerate(zip(procs, outs)))
+        raise AssertionError(msg)
+    return outs

@@ -1,0 +1,62 @@
+"""Multi-process CPU (gloo) equivalence tests of pipeline / tensor / data parallelism:
+the smp model must match an unpartitioned PyTorch model step by step (loss and
+parameters), like the reference's SMPTestBase harness (`smp/test/torch/smp_test_base.py`)."""
+import json
+
+import pytest
+
+from tests.dist_utils import run_workers
+
+
+def _run(world, pp, tp, mbs, pipe="interleaved", auto=0, steps=2, extra=None, timeout=200):
+    args = [pp, tp, mbs, pipe, auto, steps]
+    if extra:
+        args.append(json.dumps(extra))
+    outs = run_workers("pp_gpt", world, args, timeout=timeout)
+    assert all("OK" in o for o in outs)
+
+
+def test_pp2_manual_interleaved():
+    _run(2, 2, 1, 2)
+
+
+def test_pp2_simple_pipeline_4mb():
+    _run(2, 2, 1, 4, pipe="simple")
+
+
+def test_pp2_auto_partition():
+    _run(2, 2, 1, 2, auto=1)
+
+
+def test_pp4_auto_partition():
+    _run(4, 4, 1, 4, auto=1, extra={"model": {"num_layers": 6}})
+
+
+def test_pp2_dp2():
+    _run(4, 2, 1, 2)
+
+
+def test_dp2():
+    _run(2, 1, 1, 2)
+
+
+def test_tp2():
+    _run(2, 1, 2, 1)
+
+
+def test_tp2_uneven_heads():
+    _run(2, 1, 2, 2, extra={"model": {"num_attention_heads": 3, "attention_head_size": 16, "hidden_size": 48,
+                                      "intermediate_size": 96}})
+
+
+def test_pp2_tp2():
+    _run(4, 2, 2, 2)
+
+
+def test_pp2_activation_checkpointing():
+    _run(2, 2, 1, 2, extra={"ckpt_layers": True})
+
+
+@pytest.mark.parametrize("mbs", [1, 3])
+def test_pp2_microbatch_counts(mbs):
+    _run(2, 2, 1, mbs)

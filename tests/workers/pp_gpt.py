@@ -1,0 +1,111 @@
+"""Worker: GPT pipeline/data/tensor-parallel training vs an unpartitioned reference.
+
+argv: pp tp microbatches pipeline(simple|interleaved) auto(0|1) steps [extra_json]
+Each rank trains the smp model and an identical plain-PyTorch model on the same global
+batch and checks loss and parameters after every step.
+"""
+import json
+import sys
+
+import torch
+
+import smdistributed_modelparallel_amd.torch as smp
+from smdistributed_modelparallel_amd.models import build_gpt
+
+
+def main():
+    pp, tp, mbs, pipe, auto, steps = (int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4],
+                                      int(sys.argv[5]), int(sys.argv[6]))
+    extra = json.loads(sys.argv[7]) if len(sys.argv) > 7 else {}
+    world = int(__import__("os").environ["WORLD_SIZE"])
+    cfg = {"pipeline_parallel_degree": pp, "tensor_parallel_degree": tp, "microbatches": mbs, "pipeline": pipe,
+           "ddp": world > pp, "auto_partition": bool(auto)}
+    if not auto:
+        cfg["default_partition"] = 0
+    cfg.update(extra.get("cfg", {}))
+    torch.manual_seed(123)
+    kw = dict(num_layers=4, hidden_size=64, num_attention_heads=4, attention_head_size=16, intermediate_size=128,
+              vocab_size=96, num_positions=32)
+    kw.update(extra.get("model", {}))
+    ref = build_gpt("gpt2-tiny", dropout=0.0, **kw)  # built before init: unsharded reference
+    smp.init(cfg)
+    with smp.model_creation(tensor_parallelism=tp > 1):
+        net = build_gpt("gpt2-tiny", dropout=0.0, **kw)
+    if tp == 1:
+        net.load_state_dict(ref.state_dict())
+    else:
+        from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
+
+        # distributed modules created under TP: copy the sliced reference weights
+        rsd = ref.state_dict()
+        with torch.no_grad():
+            for n, p in net.named_parameters():
+                full = rsd[n]
+                axis = getattr(p, "_smp_tp_axis", None)
+                t = slice_for_param(full, p, smp.tp_rank(), smp.tp_size())
+                assert t.shape == p.shape, (n, tuple(full.shape), tuple(t.shape), tuple(p.shape), axis)
+                p.copy_(t)
+    if not auto and pp > 1:
+        # manual: first half of the layers on stage 0, rest on stage 1 (embeddings + head on 0)
+        layers = list(net.transformer.seq_layers)
+        for i, layer in enumerate(layers):
+            smp.set_partition(layer, (i * pp) // len(layers))
+    model = smp.DistributedModel(net)
+    if extra.get("ckpt_layers"):
+        for layer in model.get_module().transformer.seq_layers:
+            smp.set_activation_checkpointing(layer)
+    lr = 0.05
+    opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=lr))
+    ropt = torch.optim.SGD(ref.parameters(), lr=lr)
+
+    @smp.step
+    def train(model, ids, labels):
+        loss, _ = model((ids, None, None, None, labels))
+        model.backward(loss)
+        return loss
+
+    g = torch.Generator().manual_seed(7)
+    dp = smp.dp_size()
+    local_bs = 2 * mbs
+    for it in range(steps):
+        ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, 16), generator=g)
+        ids = ids_all[smp.dp_rank() * local_bs:(smp.dp_rank() + 1) * local_bs]
+        opt.zero_grad()
+        out = train(model, ids, ids)
+        opt.step()
+        # reference on the global batch, averaged the same way (per microbatch mean, then mean)
+        ropt.zero_grad()
+        losses = []
+        for d in range(dp):
+            chunk = ids_all[d * local_bs:(d + 1) * local_bs]
+            for m in range(mbs):
+                x = chunk[m * 2:(m + 1) * 2]
+                l, _ = ref((x, None, None, None, x))
+                losses.append(l)
+        ref_loss = torch.stack(losses).mean()
+        ref_loss.backward()
+        ropt.step()
+        my_losses = torch.stack([o.detach().float() for o in out.outputs]).mean()
+        mine = torch.tensor([my_losses.item()])
+        all_l = smp.allgather(mine.item(), smp.DP_GROUP)
+        if smp.pp_rank() == 0 or True:
+            avg = sum(all_l) / len(all_l)
+            assert abs(avg - ref_loss.item()) < 1e-4, (it, avg, ref_loss.item())
+    # parameter check (local, TP-sliced)
+    from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
+
+    rp = dict(ref.named_parameters())
+    worst = 0.0
+    for n, p in model.local_named_parameters():
+        if p.numel() == 0:
+            continue
+        full = rp[n].detach()
+        t = slice_for_param(full, p, smp.tp_rank(), smp.tp_size())
+        worst = max(worst, (p.detach().float() - t.float()).abs().max().item())
+    assert worst < 2e-4, worst
+    print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
+    smp.barrier()
+
+
+if __name__ == "__main__":
+    main()
