@@ -58,14 +58,34 @@ __device__ __forceinline__ typename MF<T>::e8 ld8(const uint16_t* p) {
   return __builtin_bit_cast(typename MF<T>::e8, *reinterpret_cast<const s16x8*>(p));
 }
 
+// ------------------------------------------------------------------ LDS tiles
+// Tiles are stored unpadded, [rows][D] bf16, with the 16-byte chunks of each row XOR-
+// swizzled so that BOTH access patterns are bank-conflict free:
+//  * row reads (ds_read_b128, lane = row, 16 rows per LDS cycle group), and
+//  * transposed reads (ds_read_b64_tr_b16: 4 rows x 32 columns per 32-lane group).
+// D = 64 (128-B rows, two rows per 64-bank line): chunk' = chunk ^ (bit1(row)<<2 | bits2-3(row)).
+// D = 128 (256-B rows, one row per line):        chunk' = chunk ^ (bits0-1(row)<<2 | bits2-3(row)).
+template <int D>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  const int g = D == 64 ? ((((row >> 1) & 1) << 2) | ((row >> 2) & 3)) : (((row & 3) << 2) | ((row >> 2) & 3));
+  return row * D + ((chunk ^ g) << 3);
+}
+
+// Row fetch (A/B operand with k along the row): 8 elements = chunk `chunk` of row `row`.
+template <typename T, int D>
+__device__ __forceinline__ typename MF<T>::e8 ld_row(const uint16_t* tile, int row, int chunk) {
+  return ld8<T>(tile + swz<D>(row, chunk));
+}
+
 // Transposed fetch of an A/B operand element set from a row-major LDS tile:
-// elements j=0..3 <- rows k0..k0+3, j=4..7 <- rows k0+8..k0+11, all at column `col`
-// (col = c0 + (lane & 15) implied by the 16-lane group addressing).
-template <typename T>
-__device__ __forceinline__ typename MF<T>::e8 ld_tr(const uint16_t* tile, int ldrow, int k0, int c0, int lane) {
-  const int q = (lane & 15) >> 2, p = lane & 3;
-  const uint16_t* a0 = tile + (k0 + q) * ldrow + c0 + 4 * p;
-  const uint16_t* a1 = a0 + 8 * ldrow;
+// elements j=0..3 <- rows k0..k0+3, j=4..7 <- rows k0+8..k0+11, at column
+// c0 + (lane & 15) (the 16-lane group addressing: lane 4q+p supplies row q, cols 4p..4p+3).
+template <typename T, int D>
+__device__ __forceinline__ typename MF<T>::e8 ld_tr(const uint16_t* tile, int k0, int c0, int lane) {
+  const int q = (lane & 15) >> 2, pp = lane & 3;
+  const int col = c0 + 4 * pp;
+  const uint16_t* a0 = tile + swz<D>(k0 + q, col >> 3) + (col & 7);
+  const uint16_t* a1 = tile + swz<D>(k0 + 8 + q, col >> 3) + (col & 7);
   s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
   s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
   s16x8 v = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
@@ -83,26 +103,56 @@ __device__ __forceinline__ typename MF<T>::e8 pack8(const f32x16& a, int s) {
 
 __device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
 
-// Cooperative copy of a [rows x D] tile (row stride `gs` elements) into padded LDS.
-template <int D>
-__device__ __forceinline__ void load_tile(uint16_t* lds, const uint16_t* g, int64_t gs, int row0, int nrows_valid,
-                                          int rows) {
-  constexpr int CH = D / 8;  // 16-byte chunks per row
-  constexpr int LD = D + 8;
-  for (int c = threadIdx.x; c < rows * CH; c += kThreads) {
-    const int r = c / CH, k = c % CH;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < nrows_valid) v = *reinterpret_cast<const uint4*>(g + static_cast<int64_t>(row0 + r) * gs + k * 8);
-    *reinterpret_cast<uint4*>(lds + r * LD + k * 8) = v;
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Register-staged tile copy (issue global loads early, write LDS late: the HBM/L2 latency
+// hides under the MFMA work of the current tile).
+template <int D, int ROWS>
+struct Stage {
+  static constexpr int CH = D / 8;
+  static constexpr int N = ROWS * CH / kThreads;
+  static_assert(N * kThreads == ROWS * CH, "tile must split evenly over the block");
+  uint4 v[N];
+  __device__ __forceinline__ void load(const uint16_t* g, int64_t gs, int row0, int valid) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int c = threadIdx.x + i * kThreads, r = c / CH, k = c % CH;
+      v[i] = r < valid ? *reinterpret_cast<const uint4*>(g + static_cast<int64_t>(row0 + r) * gs + k * 8)
+                       : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* lds) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int c = threadIdx.x + i * kThreads, r = c / CH, k = c % CH;
+      *reinterpret_cast<uint4*>(lds + swz<D>(r, k)) = v[i];
+    }
+  }
+};
+
+template <typename T, int D>
+__device__ __forceinline__ void store_rows(uint16_t* dst, const f32x16* acc, float mul, int hh) {
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 32 * i + 8 * g + 4 * hh;
+      s16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = __builtin_bit_cast(short, MF<T>::cvt(acc[i][4 * g + j] * mul));
+      *reinterpret_cast<s16x4*>(dst + d0) = w;
+    }
   }
 }
 
 // ================================================================== forward
+// Block = 4 waves x 32 queries; K/V tiles of 64 keys.  Interior tiles (every key visible
+// to every query of the wave) take a mask-free path.
 template <typename T, int D, bool CAUSAL>
 __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
-  constexpr int BM = 128, BN = 64, LD = D + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * LD];
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int64_t bh = blockIdx.y;
@@ -112,6 +162,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
   const int q0 = qb * BM + wave * 32;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
   const int diag = sk - sq;  // key index allowed up to query + diag
+  const int win = p.window;
 
   const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
   const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
@@ -134,114 +185,135 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) o[i] = f32x16{0};
 
-  int kv_end = sk;
+  int kv_end = sk, kv_begin = 0;
   if (CAUSAL) {
     const int lim = (qb + 1) * BM + diag;
     kv_end = lim < sk ? lim : sk;
   }
+  if (win > 0) {
+    const int lo = qb * BM + diag - win + 1;
+    kv_begin = lo > 0 ? (lo / BN) * BN : 0;
+  }
+  Stage<D, BN> stK, stV;
+  if (kv_begin < kv_end) {
+    stK.load(K, p.k_ss, kv_begin, sk - kv_begin);
+    stV.load(V, p.v_ss, kv_begin, sk - kv_begin);
+  }
   const int wave_last_q = q0 + 31;
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN) {
+  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
     __syncthreads();
-    load_tile<D>(sK, K, p.k_ss, kv0, sk - kv0, BN);
-    load_tile<D>(sV, V, p.v_ss, kv0, sk - kv0, BN);
+    stK.store(sK);
+    stV.store(sV);
     __syncthreads();
+    if (kv0 + BN < kv_end) {
+      stK.load(K, p.k_ss, kv0 + BN, sk - kv0 - BN);
+      stV.load(V, p.v_ss, kv0 + BN, sk - kv0 - BN);
+    }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
-    if (p.window > 0 && kv0 + BN - 1 < q0 + diag - p.window + 1) continue;
+    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
+    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
+                          (win <= 0 || kv0 > wave_last_q + diag - win);
     f32x16 s0 = f32x16{0}, s1 = f32x16{0};
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
-      s0 = MF<T>::mma(ld8<T>(sK + r * LD + 16 * t + 8 * hh), qf[t], s0);
-      s1 = MF<T>::mma(ld8<T>(sK + (32 + r) * LD + 16 * t + 8 * hh), qf[t], s1);
+      s0 = MF<T>::mma(ld_row<T, D>(sK, r, 2 * t + hh), qf[t], s0);
+      s1 = MF<T>::mma(ld_row<T, D>(sK, 32 + r, 2 * t + hh), qf[t], s1);
     }
-    float mx = -INFINITY;
+    if (!interior) {
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int k0 = kv0 + acc_row(reg, hh);
-      const int k1 = k0 + 32;
-      float v0 = s0[reg] * sl2, v1 = s1[reg] * sl2;
-      if (k0 >= sk || (CAUSAL && k0 > qrow + diag) || (p.window > 0 && k0 <= qrow + diag - p.window)) v0 = -INFINITY;
-      if (k1 >= sk || (CAUSAL && k1 > qrow + diag) || (p.window > 0 && k1 <= qrow + diag - p.window)) v1 = -INFINITY;
-      s0[reg] = v0;
-      s1[reg] = v1;
-      mx = fmaxf(mx, fmaxf(v0, v1));
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k0 = kv0 + acc_row(reg, hh);
+        const int k1 = k0 + 32;
+        if (k0 >= sk || (CAUSAL && k0 > qrow + diag) || (win > 0 && k0 <= qrow + diag - win)) s0[reg] = -INFINITY;
+        if (k1 >= sk || (CAUSAL && k1 > qrow + diag) || (win > 0 && k1 <= qrow + diag - win)) s1[reg] = -INFINITY;
+      }
     }
+    // raw-score row max (scale > 0 keeps the order), two independent chains
+    float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
+#pragma unroll
+    for (int reg = 2; reg < 16; reg += 2) {
+      mx0 = fmaxf(mx0, fmaxf(s0[reg], s1[reg]));
+      mx1 = fmaxf(mx1, fmaxf(s0[reg + 1], s1[reg + 1]));
+    }
+    float mx = fmaxf(mx0, mx1) * sl2;
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_i, mx);
-    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_i - m_new);
-    float rs = 0.f;
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
+    const float alpha = fast_exp2(m_i - m_use);
+    float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const float e0 = (m_new == -INFINITY) ? 0.f : exp2f(s0[reg] - m_new);
-      const float e1 = (m_new == -INFINITY) ? 0.f : exp2f(s1[reg] - m_new);
+      const float e0 = fast_exp2(fmaf(s0[reg], sl2, -m_use));
+      const float e1 = fast_exp2(fmaf(s1[reg], sl2, -m_use));
       s0[reg] = e0;
       s1[reg] = e1;
-      rs += e0 + e1;
+      rs0 += e0;
+      rs1 += e1;
     }
+    float rs = rs0 + rs1;
     rs += __shfl_xor(rs, 32, 64);
     l_i = l_i * alpha + rs;
-    m_i = m_new;
+    if (__any(m_new != m_i)) {  // rescale only when a row max moved
 #pragma unroll
-    for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
+      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
+    }
+    m_i = m_new;
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
       const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int kb = 16 * s + 4 * hh;
-        o[i] = MF<T>::mma(ld_tr<T>(sV, LD, kb, c0, lane), pf[s], o[i]);
-      }
+      for (int s = 0; s < 4; ++s) o[i] = MF<T>::mma(ld_tr<T, D>(sV, 16 * s + 4 * hh, c0, lane), pf[s], o[i]);
     }
   }
   if (qrow >= sq) return;
   const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
   uint16_t* O = static_cast<uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh + static_cast<int64_t>(qrow) * p.o_ss;
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d0 = 32 * i + 8 * g + 4 * hh;
-      s16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = __builtin_bit_cast(short, MF<T>::cvt(o[i][4 * g + j] * inv));
-      *reinterpret_cast<s16x4*>(O + d0) = w;
-    }
-  }
+  store_rows<T, D>(O, o, inv, hh);
   if (hh == 0) p.lse[bh * p.sq + qrow] = (l_i > 0.f) ? (m_i + log2f(l_i)) / kLog2e : -INFINITY;
 }
 
 // ============================================================= delta = rowsum(dO * O)
 template <typename T>
 __global__ void __launch_bounds__(kThreads) attn_delta_kernel(AttnBwdParams p) {
-  // one wave per (b, h, query) row
-  const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  // 16 lanes per (b, h, query) row, 8 elements per lane per step (16-byte loads)
+  const int sub = threadIdx.x & 15;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
   const int64_t total = p.f.b * p.f.h * p.f.sq;
-  if (row >= total) return;
-  const int64_t q = row % p.f.sq, bh = row / p.f.sq, b = bh / p.f.h, h = bh % p.f.h;
-  const T* O = static_cast<const T*>(p.f.o) + b * p.f.o_sb + h * p.f.o_sh + q * p.f.o_ss;
-  const T* dO = static_cast<const T*>(p.dout) + b * p.do_sb + h * p.do_sh + q * p.do_ss;
+  const bool valid = row < total;
   float acc = 0.f;
-  for (int d = lane; d < p.f.d; d += 64) acc += to_f32(O[d]) * to_f32(dO[d]);
-  acc = wave_sum(acc);
-  if (lane == 0) p.delta[row] = acc;
+  if (valid) {
+    const int64_t q = row % p.f.sq, bh = row / p.f.sq, b = bh / p.f.h, h = bh % p.f.h;
+    const T* O = static_cast<const T*>(p.f.o) + b * p.f.o_sb + h * p.f.o_sh + q * p.f.o_ss;
+    const T* dO = static_cast<const T*>(p.dout) + b * p.do_sb + h * p.do_sh + q * p.do_ss;
+    for (int d = sub * 8; d < p.f.d; d += 128) {
+      Vec16<T> a = load16<T>(O + d), g = load16<T>(dO + d);
+#pragma unroll
+      for (int j = 0; j < Vec16<T>::N; ++j) acc += to_f32(a.v[j]) * to_f32(g.v[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (valid && sub == 0) p.delta[row] = acc;
 }
 
 // ===================================================================== dK / dV
+// Block = 4 waves x 32 keys (key on the MFMA lane); Q/dO tiles of 64 queries, two 32-query
+// sub-steps.  S and dP accumulators start from the per-query row constants
+// (-lse*log2e/(scale*log2e), -delta), so p = exp2(S' * scale*log2e) and dS = p * dP'.
 template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kThreads, 2) attn_bwd_dkdv_kernel(AttnBwdParams P) {
-  constexpr int BKEYS = 128, BQ = 64, LD = D + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t sQ[BQ * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * LD];
-  __shared__ float sL[BQ], sDl[BQ];
+__global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kernel(AttnBwdParams P) {
+  constexpr int BKEYS = 128, BQ = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[BQ * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * D];
+  __shared__ __attribute__((aligned(16))) float sL[BQ], sDl[BQ];
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int64_t bh = blockIdx.y, b = bh / p.h, h = bh % p.h;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
-  const int nkb = (sk + BKEYS - 1) / BKEYS;
-  const int kb = CAUSAL ? static_cast<int>(blockIdx.x) : static_cast<int>(blockIdx.x);
-  (void)nkb;
+  const int win = p.window;
+  const int kb = static_cast<int>(blockIdx.x);
   const int k0w = kb * BKEYS + wave * 32;  // wave's first key
   const int krow = k0w + r;                // this lane's key (as B-operand column)
 
@@ -270,41 +342,85 @@ __global__ void __launch_bounds__(kThreads, 2) attn_bwd_dkdv_kernel(AttnBwdParam
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) dv[i] = dk[i] = f32x16{0};
   const float sl2 = p.scale * kLog2e;
-  int q_start = 0;
+  const float inv_sl2 = 1.f / sl2;
+  int q_start = 0, q_end = sq;
   if (CAUSAL) {
     q_start = kb * BKEYS - diag;
     q_start = q_start < 0 ? 0 : (q_start / BQ) * BQ;
   }
-  for (int qt = q_start; qt < sq; qt += BQ) {
-    __syncthreads();
-    load_tile<D>(sQ, Q, p.q_ss, qt, sq - qt, BQ);
-    load_tile<D>(sdO, dO, P.do_ss, qt, sq - qt, BQ);
+  if (win > 0) {
+    const int hi = (kb + 1) * BKEYS - 1 - diag + win;  // last query that sees the block's last key
+    q_end = hi + 1 < sq ? hi + 1 : sq;
+  }
+  Stage<D, BQ> stQ, stO;
+  float l_stage = 0.f, d_stage = 0.f;
+  if (q_start < q_end) {
+    stQ.load(Q, p.q_ss, q_start, sq - q_start);
+    stO.load(dO, P.do_ss, q_start, sq - q_start);
     if (threadIdx.x < BQ) {
-      const int qq = qt + threadIdx.x;
-      sL[threadIdx.x] = qq < sq ? LSE[qq] * kLog2e : 0.f;
-      sDl[threadIdx.x] = qq < sq ? DL[qq] : 0.f;
+      const int qq = q_start + threadIdx.x;
+      l_stage = qq < sq ? LSE[qq] : 0.f;
+      d_stage = qq < sq ? DL[qq] : 0.f;
+    }
+  }
+  const int klast = k0w + 31;
+  for (int qt = q_start; qt < q_end; qt += BQ) {
+    __syncthreads();
+    stQ.store(sQ);
+    stO.store(sdO);
+    if (threadIdx.x < BQ) {
+      // lse == -inf (fully masked row) contributes nothing: any finite constant works
+      sL[threadIdx.x] = l_stage == -INFINITY ? 0.f : -l_stage * kLog2e * inv_sl2;
+      sDl[threadIdx.x] = -d_stage;
     }
     __syncthreads();
-    if (CAUSAL && qt + BQ - 1 + diag < k0w) continue;  // whole tile sees none of this wave's keys
+    if (qt + BQ < q_end) {
+      stQ.load(Q, p.q_ss, qt + BQ, sq - qt - BQ);
+      stO.load(dO, P.do_ss, qt + BQ, sq - qt - BQ);
+      if (threadIdx.x < BQ) {
+        const int qq = qt + BQ + threadIdx.x;
+        l_stage = qq < sq ? LSE[qq] : 0.f;
+        d_stage = qq < sq ? DL[qq] : 0.f;
+      }
+    }
 #pragma unroll 1
     for (int sub = 0; sub < 2; ++sub) {
-      // S = Q K^T, dP = dO V^T for 32 queries x 32 keys (query rows in regs, key on lane)
-      f32x16 s = f32x16{0}, dp = f32x16{0};
+      const int qs = qt + 32 * sub;  // first query of this sub-step
+      if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
+      if (win > 0 && qs + diag - win + 1 > klast) continue;  // all keys left the window
+      const bool interior = qs + 31 < sq && klast < sk && (!CAUSAL || klast <= qs + diag) &&
+                            (win <= 0 || k0w > qs + 31 + diag - win);
+      // S' = Q K^T - lse/scale, dP' = dO V^T - delta (query rows in regs, key on lane)
+      f32x16 s, dp;
 #pragma unroll
-      for (int t = 0; t < D / 16; ++t) {
-        s = MF<T>::mma(ld8<T>(sQ + (32 * sub + r) * LD + 16 * t + 8 * hh), kf[t], s);
-        dp = MF<T>::mma(ld8<T>(sdO + (32 * sub + r) * LD + 16 * t + 8 * hh), vf[t], dp);
+      for (int g = 0; g < 4; ++g) {
+        const float4 lv = *reinterpret_cast<const float4*>(&sL[32 * sub + 8 * g + 4 * hh]);
+        const float4 dv4 = *reinterpret_cast<const float4*>(&sDl[32 * sub + 8 * g + 4 * hh]);
+        s[4 * g + 0] = lv.x; s[4 * g + 1] = lv.y; s[4 * g + 2] = lv.z; s[4 * g + 3] = lv.w;
+        dp[4 * g + 0] = dv4.x; dp[4 * g + 1] = dv4.y; dp[4 * g + 2] = dv4.z; dp[4 * g + 3] = dv4.w;
       }
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int ql = 32 * sub + acc_row(reg, hh);
-        const int qq = qt + ql;
-        float pv = exp2f(s[reg] * sl2 - sL[ql]);
-        if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) ||
-            (p.window > 0 && krow <= qq + diag - p.window))
-          pv = 0.f;
-        s[reg] = pv;
-        dp[reg] = pv * (dp[reg] - sDl[ql]);
+      for (int t = 0; t < D / 16; ++t) {
+        s = MF<T>::mma(ld_row<T, D>(sQ, 32 * sub + r, 2 * t + hh), kf[t], s);
+        dp = MF<T>::mma(ld_row<T, D>(sdO, 32 * sub + r, 2 * t + hh), vf[t], dp);
+      }
+      if (interior) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const float pv = fast_exp2(s[reg] * sl2);
+          s[reg] = pv;
+          dp[reg] *= pv;
+        }
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int qq = qs + acc_row(reg, hh);
+          float pv = fast_exp2(s[reg] * sl2);
+          if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win))
+            pv = 0.f;
+          s[reg] = pv;
+          dp[reg] *= pv;
+        }
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
       typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
@@ -313,39 +429,28 @@ __global__ void __launch_bounds__(kThreads, 2) attn_bwd_dkdv_kernel(AttnBwdParam
       for (int i = 0; i < D / 32; ++i) {
         const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
         const int kq = 32 * sub + 4 * hh;
-        dv[i] = MF<T>::mma(ld_tr<T>(sdO, LD, kq, c0, lane), pf0, dv[i]);
-        dv[i] = MF<T>::mma(ld_tr<T>(sdO, LD, kq + 16, c0, lane), pf1, dv[i]);
-        dk[i] = MF<T>::mma(ld_tr<T>(sQ, LD, kq, c0, lane), sf0, dk[i]);
-        dk[i] = MF<T>::mma(ld_tr<T>(sQ, LD, kq + 16, c0, lane), sf1, dk[i]);
+        dv[i] = MF<T>::mma(ld_tr<T, D>(sdO, kq, c0, lane), pf0, dv[i]);
+        dv[i] = MF<T>::mma(ld_tr<T, D>(sdO, kq + 16, c0, lane), pf1, dv[i]);
+        dk[i] = MF<T>::mma(ld_tr<T, D>(sQ, kq, c0, lane), sf0, dk[i]);
+        dk[i] = MF<T>::mma(ld_tr<T, D>(sQ, kq + 16, c0, lane), sf1, dk[i]);
       }
     }
   }
   if (krow >= sk) return;
   uint16_t* dK = static_cast<uint16_t*>(P.dk) + b * P.dk_sb + h * P.dk_sh + static_cast<int64_t>(krow) * P.dk_ss;
   uint16_t* dV = static_cast<uint16_t*>(P.dv) + b * P.dv_sb + h * P.dv_sh + static_cast<int64_t>(krow) * P.dv_ss;
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d0 = 32 * i + 8 * g + 4 * hh;
-      s16x4 wk, wv;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        wk[j] = __builtin_bit_cast(short, MF<T>::cvt(dk[i][4 * g + j] * p.scale));
-        wv[j] = __builtin_bit_cast(short, MF<T>::cvt(dv[i][4 * g + j]));
-      }
-      *reinterpret_cast<s16x4*>(dK + d0) = wk;
-      *reinterpret_cast<s16x4*>(dV + d0) = wv;
-    }
-  }
+  store_rows<T, D>(dK, dk, p.scale, hh);
+  store_rows<T, D>(dV, dv, 1.f, hh);
 }
 
 // ========================================================================= dQ
+// Block = 4 waves x 32 queries (query on the lane: S^T = K Q^T, dP^T = V dO^T); K/V tiles
+// of 64 keys; dQ^T += K^T dS^T with K^T from transposed LDS reads.
 template <typename T, int D, bool CAUSAL>
-__global__ void __launch_bounds__(kThreads, 2) attn_bwd_dq_kernel(AttnBwdParams P) {
-  constexpr int BM = 128, BN = 64, LD = D + 8;
-  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * LD];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * LD];
+__global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(AttnBwdParams P) {
+  constexpr int BM = 128, BN = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * D];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * D];
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -354,6 +459,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_bwd_dq_kernel(AttnBwdParams 
   const int qb = CAUSAL ? (nqb - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
   const int q0 = qb * BM + wave * 32;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
+  const int win = p.window;
   const int qrow = q0 + r;
   const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
   const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
@@ -374,65 +480,80 @@ __global__ void __launch_bounds__(kThreads, 2) attn_bwd_dq_kernel(AttnBwdParams 
       }
     }
   }
-  const float lse2 = qrow < sq ? p.lse[bh * p.sq + qrow] * kLog2e : 0.f;
-  const float dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
+  float lse = qrow < sq ? p.lse[bh * p.sq + qrow] : 0.f;
+  if (lse == -INFINITY) lse = 0.f;  // fully masked row: every p is masked to 0 below
   const float sl2 = p.scale * kLog2e;
+  const float s_init = -lse * kLog2e / sl2;
+  const float dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
   f32x16 dq[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) dq[i] = f32x16{0};
-  int kv_end = sk;
+  int kv_end = sk, kv_begin = 0;
   if (CAUSAL) {
     const int lim = (qb + 1) * BM + diag;
     kv_end = lim < sk ? lim : sk;
   }
-  for (int kv0 = 0; kv0 < kv_end; kv0 += BN) {
+  if (win > 0) {
+    const int lo = qb * BM + diag - win + 1;
+    kv_begin = lo > 0 ? (lo / BN) * BN : 0;
+  }
+  Stage<D, BN> stK, stV;
+  if (kv_begin < kv_end) {
+    stK.load(K, p.k_ss, kv_begin, sk - kv_begin);
+    stV.load(V, p.v_ss, kv_begin, sk - kv_begin);
+  }
+  const int wave_last_q = q0 + 31;
+  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
     __syncthreads();
-    load_tile<D>(sK, K, p.k_ss, kv0, sk - kv0, BN);
-    load_tile<D>(sV, V, p.v_ss, kv0, sk - kv0, BN);
+    stK.store(sK);
+    stV.store(sV);
     __syncthreads();
-    if (CAUSAL && kv0 > q0 + 31 + diag) continue;
-    // S^T = K Q^T, dP^T = V dO^T  (key rows in regs, query on lane)
+    if (kv0 + BN < kv_end) {
+      stK.load(K, p.k_ss, kv0 + BN, sk - kv0 - BN);
+      stV.load(V, p.v_ss, kv0 + BN, sk - kv0 - BN);
+    }
+    if (CAUSAL && kv0 > wave_last_q + diag) continue;
+    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
+    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
+                          (win <= 0 || kv0 > wave_last_q + diag - win);
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      s[u] = f32x16{0};
-      dp[u] = f32x16{0};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        s[u][j] = s_init;
+        dp[u][j] = -dl;
+      }
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) {
-        s[u] = MF<T>::mma(ld8<T>(sK + (32 * u + r) * LD + 16 * t + 8 * hh), qf[t], s[u]);
-        dp[u] = MF<T>::mma(ld8<T>(sV + (32 * u + r) * LD + 16 * t + 8 * hh), df[t], dp[u]);
+        s[u] = MF<T>::mma(ld_row<T, D>(sK, 32 * u + r, 2 * t + hh), qf[t], s[u]);
+        dp[u] = MF<T>::mma(ld_row<T, D>(sV, 32 * u + r, 2 * t + hh), df[t], dp[u]);
       }
+      if (interior) {
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int kk = kv0 + 32 * u + acc_row(reg, hh);
-        float pv = exp2f(s[u][reg] * sl2 - lse2);
-        if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (p.window > 0 && kk <= qrow + diag - p.window))
-          pv = 0.f;
-        dp[u][reg] = pv * (dp[u][reg] - dl);  // dS^T
+        for (int reg = 0; reg < 16; ++reg) dp[u][reg] *= fast_exp2(s[u][reg] * sl2);
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int kk = kv0 + 32 * u + acc_row(reg, hh);
+          float pv = fast_exp2(s[u][reg] * sl2);
+          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win))
+            pv = 0.f;
+          dp[u][reg] *= pv;  // dS^T
+        }
       }
     }
-    // dQ^T += K^T dS^T  (B = dS^T accumulator, A = K^T via transposed reads of sK)
     typename MF<T>::e8 sf[4] = {pack8<T>(dp[0], 0), pack8<T>(dp[0], 1), pack8<T>(dp[1], 0), pack8<T>(dp[1], 1)};
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
       const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
 #pragma unroll
-      for (int st = 0; st < 4; ++st) dq[i] = MF<T>::mma(ld_tr<T>(sK, LD, 16 * st + 4 * hh, c0, lane), sf[st], dq[i]);
+      for (int st = 0; st < 4; ++st) dq[i] = MF<T>::mma(ld_tr<T, D>(sK, 16 * st + 4 * hh, c0, lane), sf[st], dq[i]);
     }
   }
   if (qrow >= sq) return;
   uint16_t* dQ = static_cast<uint16_t*>(P.dq) + b * P.dq_sb + h * P.dq_sh + static_cast<int64_t>(qrow) * P.dq_ss;
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d0 = 32 * i + 8 * g + 4 * hh;
-      s16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = __builtin_bit_cast(short, MF<T>::cvt(dq[i][4 * g + j] * p.scale));
-      *reinterpret_cast<s16x4*>(dQ + d0) = w;
-    }
-  }
+  store_rows<T, D>(dQ, dq, p.scale, hh);
 }
 
 template <typename T, int D>
@@ -448,7 +569,7 @@ int launch_fwd(const AttnParams& p, hipStream_t s) {
 template <typename T, int D>
 int launch_bwd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = p.f.b * p.f.h * p.f.sq;
-  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 3) / 4), kThreads, 0, s>>>(p);
+  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
   dim3 gk(static_cast<unsigned>((p.f.sk + 127) / 128), static_cast<unsigned>(p.f.b * p.f.h));
   dim3 gq(static_cast<unsigned>((p.f.sq + 127) / 128), static_cast<unsigned>(p.f.b * p.f.h));
   if (p.f.causal) {

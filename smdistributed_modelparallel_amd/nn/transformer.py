@@ -380,6 +380,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
 
 # ========================================================== transformer layer
 class DistributedTransformerLayer(DistributedModule):
+    _smp_sdp_atomic = True  # forward calls attention.core() etc. directly: never split for ZeRO
     _KEYS = _LAYER_KEYS
 
     def __init__(self, *args, layer_idx=0, **kwargs):

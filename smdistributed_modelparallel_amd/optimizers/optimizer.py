@@ -77,6 +77,8 @@ class DistributedOptimizer:
         else:
             self.loss_scaler = LossScaler(1.0)
         self.kind = _kind_of(optimizer)
+        if self.kind == "lamb" and cfg.zero2d_enabled():
+            raise SMPInvalidArgumentError("FusedLAMB is not supported with sharded data parallelism")
         self.domains = []
         self._step_count = [0] * len(optimizer.param_groups)
         self._clip_coef = None
@@ -210,14 +212,15 @@ class DistributedOptimizer:
         inv = 1.0 / self.loss_scale
         for d in self.domains:
             # replicated (non-TP) params are identical on every tp_rank: count them once
-            if d.key == "default" and core.tp_size() > 1 and core.tp_rank() != 0:
+            if d.key == "default" and core.tp_size() > 1 and core.tp_rank() != 0 and not state.cfg.shard_optimizer_state:
                 continue
             mt.sumsq(self._grad_range(d), acc, scale=inv)
-        if state.cfg.shard_optimizer_state and core.dp_size() > 1:
-            if core.tp_size() > 1:
-                dist.all_reduce(acc, group=state.pgs.world)
-            else:
-                dist.all_reduce(acc, group=state.pgs.world)
+        if state.sdp is not None:
+            # every replica holds identical reduced shards: the norm spans one shard group
+            if state.pgs.shard is not None:
+                dist.all_reduce(acc, group=state.pgs.shard)
+        elif state.cfg.shard_optimizer_state and core.dp_size() > 1:
+            dist.all_reduce(acc, group=state.pgs.world)
         elif core.mp_size() > 1:
             dist.all_reduce(acc, group=state.pgs.mp)
         norm = acc.sqrt()
@@ -301,6 +304,8 @@ class DistributedOptimizer:
 
     def _allgather_shards(self):
         model = state.model
+        if state.sdp is not None:
+            state.sdp.after_optimizer_step()
         for r in model.reducers.values():
             if r.shard and r.group_size > 1:
                 r.allgather_params()

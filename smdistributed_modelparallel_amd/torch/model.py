@@ -191,8 +191,11 @@ class DistributedModel(nn.Module):
         self._init_deferred_params()
         self._local_params = [p for p in self._ordered_params() if p in local_params]
         self._update_transformer_boundaries()
-        self._build_flat_and_reducers()
-        self._broadcast_params()
+        if state.cfg.zero2d_enabled():
+            self._build_sharded_dp()
+        else:
+            self._build_flat_and_reducers()
+            self._broadcast_params()
         if state.core.pp_size() > 1:
             from ..runtime.patch import patch_module_forwards
 
@@ -280,10 +283,24 @@ class DistributedModel(nn.Module):
                                                overlap=self.overlapping_allreduce, shard=shard,
                                                comm_hook=self._comm_hook, name=key)
 
+    def _build_sharded_dp(self):
+        from ..parallel.sharded_dp import ShardedDataParallel, _NoReducer
+
+        cfg, core = state.cfg, state.core
+        S = cfg.sharded_data_parallel_degree
+        sdp = ShardedDataParallel(self, state.pgs.shard, S, state.pgs.shard_replica, core.size() // S, state.device)
+        state.sdp = sdp
+        self.flat_groups = {"zero": sdp.flat}
+        self.reducers = {"zero": _NoReducer()}
+
     def _relayout_for_optimizer(self, param_groups):
         """Re-order the flat buffers by optimizer param group (one contiguous segment per
         group, so the fused optimizer kernel sees one hyper-parameter set per range)."""
-        if self.partitioned:
+        if not self.partitioned:
+            return
+        if state.sdp is not None:
+            state.sdp.relayout(param_groups)
+        else:
             self._build_flat_and_reducers(segments=param_groups)
 
     def _broadcast_params(self):
@@ -333,6 +350,8 @@ class DistributedModel(nn.Module):
             if sync:
                 for r in self.reducers.values():
                     r.synchronize()
+                if state.sdp is not None:
+                    state.sdp.synchronize()
         for name, hook in list(self._post_step_hooks.items()):
             if name not in self._post_step_hooks_run:
                 self._post_step_hooks_run.add(name)
@@ -531,11 +550,16 @@ class DistributedModel(nn.Module):
     def local_state_dict(self, *args, **kwargs):
         from .checkpoint_utils import model_local_state_dict
 
+        if state.sdp is not None:
+            return state.sdp.shard_state_dict()
         return model_local_state_dict(self)
 
     def state_dict(self, *args, gather_to_rank0=True, cast_to_cpu=True, **kwargs):
         from .checkpoint_utils import model_full_state_dict
 
+        if state.sdp is not None:
+            sd = state.sdp.full_state_dict()
+            return sd if (not gather_to_rank0 or state.core.rank() == 0) else {}
         return model_full_state_dict(self, gather_to_rank0=gather_to_rank0, cast_to_cpu=cast_to_cpu)
 
     def load_state_dict(self, state_dict, strict=True, translate_function=None, same_partition_load=False):
@@ -545,6 +569,14 @@ class DistributedModel(nn.Module):
             self._deferred_load = {"model": state_dict, "kwargs": dict(strict=strict, translate_function=translate_function,
                                                                        same_partition_load=same_partition_load)}
             return
+        if state.sdp is not None:
+            from ..parallel.sharded_dp import is_zero_state_dict
+
+            if is_zero_state_dict(state_dict):
+                return state.sdp.load_shard_state_dict(state_dict)
+            if translate_function is not None:
+                state_dict = translate_function(state_dict)
+            return state.sdp.load_full_state_dict(state_dict, strict=strict)
         return model_load_state_dict(self, state_dict, strict=strict, translate_function=translate_function,
                                      same_partition_load=same_partition_load)
 

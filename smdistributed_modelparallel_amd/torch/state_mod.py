@@ -33,6 +33,8 @@ class ProcessGroups:
         self.mp = None
         self.p2p = {}  # (src_global, dst_global) -> group, GPU only
         self.cpu_tp = None  # gloo twin of the TP group (object/CPU traffic)
+        self.shard = None  # sharded data parallel: S consecutive ranks
+        self.shard_replica = None  # same shard index across the dp / S replicas
 
     def get(self, group):
         return {
@@ -78,6 +80,7 @@ class PTModelParallelState:
         self.offloaders = {}
         self.current_offloader = None
         self.transport = None
+        self.sdp = None
         self.first_step_done = False
         self.skip_graph_validation = os.environ.get("SMP_SKIP_GRAPH_VALIDATION", "0") == "1"
         self._lock = threading.RLock()
@@ -115,6 +118,19 @@ class PTModelParallelState:
         self.pgs.dp = make("dp") if core.dp_size() > 1 else None
         self.pgs.rdp = make("rdp") if core.rdp_size() > 1 else None
         self.pgs.mp = make("mp") if core.mp_size() > 1 else None
+        if self.cfg.zero2d_enabled():
+            S, n = self.cfg.sharded_data_parallel_degree, core.size()
+            for i in range(n // S):
+                ranks = list(range(i * S, (i + 1) * S))
+                g = dist.group.WORLD if S == n else dist.new_group(ranks, backend=backend)
+                if me in ranks:
+                    self.pgs.shard = g
+            if n // S > 1:
+                for j in range(S):
+                    ranks = list(range(j, n, S))
+                    g = dist.new_group(ranks, backend=backend)
+                    if me in ranks:
+                        self.pgs.shard_replica = g
         if self.use_gpu and core.tp_size() > 1:
             # CPU twin for host-side TP traffic (offload broadcast of host tensors)
             mine = None

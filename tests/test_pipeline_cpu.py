@@ -60,3 +60,14 @@ def test_pp2_activation_checkpointing():
 @pytest.mark.parametrize("mbs", [1, 3])
 def test_pp2_microbatch_counts(mbs):
     _run(2, 2, 1, mbs)
+
+
+_SDP = {"sdp_param_persistence_threshold": 100, "sdp_reduce_bucket_size": 20000}
+
+
+def test_sharded_dp2():
+    _run(2, 1, 1, 2, extra={"cfg": dict(_SDP, sharded_data_parallel_degree=2)})
+
+
+def test_sharded_dp2_replicas2_activation_checkpointing():
+    _run(4, 1, 1, 2, extra={"cfg": dict(_SDP, sharded_data_parallel_degree=2), "ckpt_layers": True})

@@ -96,6 +96,11 @@ def main():
 
     rp = dict(ref.named_parameters())
     worst = 0.0
+    if smp.state.cfg.zero2d_enabled():
+        # parameters are sharded: compare the gathered full state dict
+        sd = model.state_dict(gather_to_rank0=False)
+        for n, full in rp.items():
+            worst = max(worst, (sd[n].float() - full.detach().float()).abs().max().item())
     for n, p in model.local_named_parameters():
         if p.numel() == 0:
             continue
