@@ -38,7 +38,51 @@ def parse():
     ap.add_argument("--no-flash", action="store_true")
     ap.add_argument("--activation-checkpointing", action="store_true")
     ap.add_argument("--shard-optimizer-state", action="store_true")
+    ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
+                    help="hipBLASLt/rocBLAS GEMM solution selection via PyTorch TunableOp: 'use' loads the "
+                         "per-shape winners measured on MI355X (configs/tunableop), 'tune' re-measures them "
+                         "during warmup; auto = use when a results file exists")
     return ap.parse_args()
+
+
+def tunableop_file(args):
+    root = os.path.dirname(os.path.abspath(__file__))
+    return os.path.join(root, "configs", "tunableop",
+                        f"{args.model}_mbs{args.mbs}_s{args.seq}_pp{args.pp}_tp{args.tp}.csv")
+
+
+def setup_tunableop(args):
+    """GEMMs stay library GEMMs (hipBLASLt / rocBLAS): TunableOp picks, per shape, the
+    fastest solution measured on this GPU instead of the library heuristic."""
+    mode = args.tunableop
+    path = tunableop_file(args)
+    if mode == "auto":
+        mode = "use" if os.path.isfile(path) else "off"
+    if mode == "off" or not torch.cuda.is_available():
+        return "off"
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    if mode == "use":
+        tun.tuning_enable(False)
+        tun.set_filename(path, insert_device_ordinal=False)
+        if not tun.read_file(path):
+            tun.enable(False)
+            return "off"
+    else:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(40)
+        tun.set_filename(path, insert_device_ordinal=False)
+    return mode
+
+
+def write_tunableop_results(path):
+    """TunableOp results file: validator lines, then one line per tuned GEMM signature."""
+    tun = torch.cuda.tunable
+    lines = [f"Validator,{k},{v}" for k, v in tun.get_validators()]
+    lines += [",".join(str(x) for x in r) for r in tun.get_results()]
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
 
 
 def main():
@@ -60,6 +104,7 @@ def main():
     if args.pp > 1:
         cfg["auto_partition"] = True
     smp.init(cfg)
+    tmode = setup_tunableop(args)
     torch.manual_seed(1234 + smp.dp_rank())
     mc = GPT_CONFIGS[args.model]
     with smp.model_creation(tensor_parallelism=args.tp > 1, dtype=torch.float32):
@@ -96,6 +141,11 @@ def main():
 
     for i in range(args.warmup):
         out = one(i)
+    if tmode == "tune":
+        torch.cuda.synchronize()
+        torch.cuda.tunable.tuning_enable(False)
+        if smp.rank() == 0:
+            write_tunableop_results(tunableop_file(args))
     loss_val = float(out.reduce_mean()) if out is not None and smp.pp_rank() == 0 else float("nan")
 
     def sync():
@@ -144,6 +194,7 @@ def main():
                 "microbatches": args.microbatches,
                 "flash_attention": not args.no_flash,
                 "dropout": args.dropout,
+                "gemm_selection": "tunableop" if tmode != "off" else "heuristic",
             },
             "tokens_per_s": round(tokens_per_s, 1),
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),

@@ -152,7 +152,8 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
   auto dx = at::empty_like(x);
   const bool aligned = ((reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(dy.data_ptr()) |
                          reinterpret_cast<uintptr_t>(dx.data_ptr()) |
-                         (dres.has_value() ? reinterpret_cast<uintptr_t>(dres->data_ptr()) : 0)) &
+                         (dres.has_value() ? reinterpret_cast<uintptr_t>(dres->data_ptr()) : 0) |
+                         (w.has_value() ? reinterpret_cast<uintptr_t>(w->data_ptr()) : 0)) &
                         15) == 0;
   const int parts = smpk::layernorm_bwd_num_parts(dt_code(x), rows, cols, aligned);
   at::Tensor dwp, dbp, dw, db;
@@ -175,8 +176,9 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
     auto wo = w.has_value() ? w->options() : x.options();
     dw = at::empty({cols}, wo);
     db = at::empty({cols}, wo);
+    auto work = at::empty({smpk::kLnReduceSlices, 2, cols}, x.options().dtype(at::kFloat));
     check(smpk::layernorm_bwd_reduce(wdt, dwp.data_ptr<float>(), dbp.data_ptr<float>(), dw.data_ptr(), db.data_ptr(),
-                                     parts, cols, stream()),
+                                     parts, cols, work.data_ptr<float>(), stream()),
           "layernorm_bwd_reduce");
   }
   return {dx, dw, db};

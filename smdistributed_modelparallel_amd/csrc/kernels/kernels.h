@@ -43,8 +43,10 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
                   const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
                   int part_rows, const void* dres, hipStream_t s);
+// dgamma/dbeta from the per-block partials; work = [kLnReduceSlices][2][cols] fp32 scratch.
+constexpr int kLnReduceSlices = 32;
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
-                         int64_t cols, hipStream_t s);
+                         int64_t cols, float* work, hipStream_t s);
 // Distributed-LN pieces (hidden sharded across TP): apply with global stats, local sums.
 int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const void* b, const float* mean,
                           const float* var, void* y, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);

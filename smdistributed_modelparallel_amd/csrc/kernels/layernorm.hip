@@ -19,6 +19,27 @@ namespace {
 
 constexpr int kRowsPerBlock = 4;
 
+// N consecutive affine parameters (any W dtype) as fp32, with 16-byte loads when possible.
+template <typename W, int N>
+__device__ __forceinline__ void load_wn(const W* p, float (&o)[N]) {
+  if constexpr (sizeof(W) * N == 16) {
+    Vec16<W> a = load16(p);
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[j] = to_f32(a.v[j]);
+  } else if constexpr (sizeof(W) * N == 32) {
+    constexpr int H = N / 2;
+    Vec16<W> a = load16(p), b = load16(p + H);
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+      o[j] = to_f32(a.v[j]);
+      o[H + j] = to_f32(b.v[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[j] = to_f32(p[j]);
+  }
+}
+
 template <typename T, typename W, int VPT>
 __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const T* __restrict__ res,
                                                   T* __restrict__ x_out, const W* __restrict__ w,
@@ -80,13 +101,22 @@ __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const
   for (int k = 0; k < VPT; ++k) {
     const int c = (k * 64 + lane) * N;
     if (c < cols) {
+      float g[N], bb[N];
+      if (w) {
+        load_wn<W, N>(w + c, g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) g[j] = 1.f;
+      }
+      if (b) {
+        load_wn<W, N>(b + c, bb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) bb[j] = 0.f;
+      }
       Vec16<T> o;
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        float g = w ? to_f32(w[c + j]) : 1.f;
-        float bb = b ? to_f32(b[c + j]) : 0.f;
-        o.v[j] = from_f32<T>((v[k][j] - mean) * rstd * g + bb);
-      }
+      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>((v[k][j] - mean) * rstd * g[j] + bb[j]);
       store16(y + row * cols + c, o);
     }
   }
@@ -140,11 +170,19 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
   constexpr int N = Vec16<T>::N;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  float dwacc[VPT][N], dbacc[VPT][N];
+  float dwacc[VPT][N], dbacc[VPT][N], wv[VPT][N];
 #pragma unroll
-  for (int k = 0; k < VPT; ++k)
+  for (int k = 0; k < VPT; ++k) {
+    const int c = (k * 64 + lane) * N;
+    if (w != nullptr && c < cols) {
+      load_wn<W, N>(w + c, wv[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) wv[k][j] = 1.f;
+    }
 #pragma unroll
     for (int j = 0; j < N; ++j) dwacc[k][j] = dbacc[k][j] = 0.f;
+  }
 
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + wid; row < rows;
        row += static_cast<int64_t>(gridDim.x) * kRowsPerBlock) {
@@ -161,8 +199,7 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
         for (int j = 0; j < N; ++j) {
           const float dyv = to_f32(d.v[j]);
           xh[k][j] = (to_f32(a.v[j]) - mean) * rstd;
-          const float ww = w ? to_f32(w[c + j]) : 1.f;
-          g[k][j] = dyv * ww;
+          g[k][j] = dyv * wv[k][j];
           s1 += g[k][j];
           s2 += g[k][j] * xh[k][j];
           dwacc[k][j] += dyv * xh[k][j];
@@ -189,34 +226,32 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
       }
     }
   }
-  // combine the block's 4 waves through LDS (waves take turns: LDS = 2 x cols fp32),
-  // then write one partial row per block
-  extern __shared__ float lds[];  // [2][cols]
+  // every wave parks its dgamma/dbeta sums in its own LDS slice, then the block adds the
+  // 4 slices column-wise and writes one fp32 partial row
+  extern __shared__ float lds[];  // [kRowsPerBlock][2][cols]
   if (dw_part == nullptr) return;
-  for (int r = 0; r < kRowsPerBlock; ++r) {
-    if (wid == r) {
+  float* mine = lds + static_cast<int64_t>(wid) * 2 * cols;
 #pragma unroll
-      for (int k = 0; k < VPT; ++k) {
-        const int c = (k * 64 + lane) * N;
-        if (c < cols) {
+  for (int k = 0; k < VPT; ++k) {
+    const int c = (k * 64 + lane) * N;
+    if (c < cols) {
 #pragma unroll
-          for (int j = 0; j < N; ++j) {
-            if (r == 0) {
-              lds[c + j] = dwacc[k][j];
-              lds[cols + c + j] = dbacc[k][j];
-            } else {
-              lds[c + j] += dwacc[k][j];
-              lds[cols + c + j] += dbacc[k][j];
-            }
-          }
-        }
+      for (int j = 0; j < N; ++j) {
+        mine[c + j] = dwacc[k][j];
+        mine[cols + c + j] = dbacc[k][j];
       }
     }
-    __syncthreads();
   }
-  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
-    dw_part[static_cast<int64_t>(blockIdx.x) * cols + c] = lds[c];
-    if (db_part) db_part[static_cast<int64_t>(blockIdx.x) * cols + c] = lds[cols + c];
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * cols; c += blockDim.x) {
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < kRowsPerBlock; ++r) a += lds[r * 2 * cols + c];
+    if (c < cols) {
+      dw_part[static_cast<int64_t>(blockIdx.x) * cols + c] = a;
+    } else if (db_part) {
+      db_part[static_cast<int64_t>(blockIdx.x) * cols + c - cols] = a;
+    }
   }
 }
 
@@ -252,17 +287,18 @@ __global__ void __launch_bounds__(256) ln_bwd_stream(const T* __restrict__ dy, c
   }
 }
 
-template <typename W>
-__global__ void __launch_bounds__(256) ln_bwd_reduce_kernel(const float* __restrict__ dw_part,
-                                                            const float* __restrict__ db_part, W* __restrict__ dw,
-                                                            W* __restrict__ db, int parts, int64_t cols) {
-  // 256 threads = 64 columns x 4 part-lanes; coalesced over columns.
+// Stage 1: block (column chunk of 64, part slice) sums its slice of the partial rows.
+__global__ void __launch_bounds__(256) ln_bwd_reduce_stage1(const float* __restrict__ dw_part,
+                                                            const float* __restrict__ db_part, float* __restrict__ out,
+                                                            int parts, int64_t cols, int slices) {
   __shared__ float sw[4][64], sb[4][64];
   const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + cl;
+  const int per = (parts + slices - 1) / slices;
+  const int p0 = blockIdx.y * per, p1 = min(parts, p0 + per);
   float a = 0.f, b = 0.f;
   if (c < cols) {
-    for (int p = pl; p < parts; p += 4) {
+    for (int p = p0 + pl; p < p1; p += 4) {
       a += dw_part[p * cols + c];
       if (db_part) b += db_part[p * cols + c];
     }
@@ -271,11 +307,24 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce_kernel(const float* __restr
   sb[pl][cl] = b;
   __syncthreads();
   if (pl == 0 && c < cols) {
-    a = sw[0][cl] + sw[1][cl] + sw[2][cl] + sw[3][cl];
-    b = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
-    if (dw) dw[c] = from_f32<W>(a);
-    if (db) db[c] = from_f32<W>(b);
+    out[static_cast<int64_t>(blockIdx.y) * 2 * cols + c] = sw[0][cl] + sw[1][cl] + sw[2][cl] + sw[3][cl];
+    out[static_cast<int64_t>(blockIdx.y) * 2 * cols + cols + c] = sb[0][cl] + sb[1][cl] + sb[2][cl] + sb[3][cl];
   }
+}
+
+// Stage 2: one thread per column adds the slice sums (fixed order: deterministic).
+template <typename W>
+__global__ void __launch_bounds__(256) ln_bwd_reduce_stage2(const float* __restrict__ part2, W* __restrict__ dw,
+                                                            W* __restrict__ db, int64_t cols, int slices) {
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < slices; ++s) {
+    a += part2[static_cast<int64_t>(s) * 2 * cols + c];
+    b += part2[static_cast<int64_t>(s) * 2 * cols + cols + c];
+  }
+  if (dw) dw[c] = from_f32<W>(a);
+  if (db) db[c] = from_f32<W>(b);
 }
 
 template <typename T, typename W>
@@ -308,7 +357,7 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
       constexpr int N = Vec16<T>::N;
-      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(y) &&
+      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(y) && vec_ok<W>(w) && vec_ok<W>(b) &&
                            (residual == nullptr || (vec_ok<T>(residual) && vec_ok<T>(x_out)));
       const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
       const int grid = static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock);
@@ -351,7 +400,7 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
       constexpr int N = Vec16<T>::N;
-      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(dy) && vec_ok<T>(dx) &&
+      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(dy) && vec_ok<T>(dx) && vec_ok<W>(w) &&
                            (dres == nullptr || vec_ok<T>(dres));
       const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
       const bool reg = aligned && vpt <= 8;
@@ -363,7 +412,7 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
       T* dxx = static_cast<T*>(dx);
       const T* dr = static_cast<const T*>(dres);
       const int c = static_cast<int>(cols);
-      const size_t lds = static_cast<size_t>(2) * cols * sizeof(float);
+      const size_t lds = static_cast<size_t>(2 * kRowsPerBlock) * cols * sizeof(float);
       if (reg && vpt <= 1) {
         ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
       } else if (reg && vpt <= 2) {
@@ -382,10 +431,14 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
 }
 
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
-                         int64_t cols, hipStream_t s) {
+                         int64_t cols, float* work, hipStream_t s) {
+  // work: [kLnReduceSlices][2][cols] fp32
+  const int slices = parts < kLnReduceSlices ? parts : kLnReduceSlices;
+  dim3 g1(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(slices));
+  ln_bwd_reduce_stage1<<<g1, 256, 0, s>>>(dw_part, db_part, work, parts, cols, slices);
   SMPK_DISPATCH(wdt, W, {
-    ln_bwd_reduce_kernel<W><<<static_cast<int>((cols + 63) / 64), 256, 0, s>>>(
-        dw_part, db_part, static_cast<W*>(dw), static_cast<W*>(db), parts, cols);
+    ln_bwd_reduce_stage2<W><<<static_cast<int>((cols + 255) / 256), 256, 0, s>>>(
+        work, static_cast<W*>(dw), static_cast<W*>(db), cols, slices);
   });
   return static_cast<int>(hipGetLastError());
 }

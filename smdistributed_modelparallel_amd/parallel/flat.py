@@ -15,10 +15,14 @@ view into it.  This gives:
 Layout: parameters are grouped into *segments* (one per optimizer param group when the
 optimizer is known); inside a segment they are stored in reverse registration order so
 the first bucket covers the last layers, whose gradients are produced first in backward.
-Each bucket is padded to a multiple of ``align`` elements (the data-parallel degree x 64)
+Every parameter starts at a multiple of 64 elements; each bucket is padded to a multiple of ``align`` elements (the data-parallel degree x 64)
 so reduce-scatter chunks are equal and 128-byte aligned.
 """
 import torch
+
+# every parameter starts on a 128-byte boundary (bf16): kernels may use 16-byte vector
+# loads on any parameter view
+_PARAM_ALIGN = 64
 
 
 class Bucket:
@@ -84,6 +88,7 @@ class FlatParamGroup:
                 if cur and cur_n + n > limit:
                     off = self._close_bucket(cur, cur_start, off)
                     cur, cur_start, cur_n = [], off, 0
+                off = (off + _PARAM_ALIGN - 1) // _PARAM_ALIGN * _PARAM_ALIGN
                 self.offsets[p] = off
                 off += n
                 cur_n += n

@@ -66,7 +66,7 @@ class _Unit:
         off = 0
         for n in self.numels:
             self.offsets.append(off)
-            off += n
+            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
         self.numel = off
         q = shard_size * _ALIGN
         self.padded = ((off + q - 1) // q) * q
@@ -313,7 +313,7 @@ class ShardedDataParallel:
                 u.offsets, off = [], 0
                 for n in u.numels:
                     u.offsets.append(off)
-                    off += n
+                    off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
                 self._write_unit(u, tensors)
                 if was:
                     self._ensure(u)
