@@ -224,12 +224,33 @@ at::Tensor col_sum(at::Tensor x) {
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / cols;
-  int64_t parts = (rows + 63) / 64;
-  if (parts > 256) parts = 256;
-  auto ws = at::empty({std::max<int64_t>(parts, 1), cols}, x.options().dtype(at::kFloat));
+  const int64_t parts = smpk::col_sum_parts(rows);
+  auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
   auto out = at::empty({cols}, x.options());
   check(smpk::col_sum(dt_code(x), x.data_ptr(), out.data_ptr(), ws.data_ptr<float>(), rows, cols, stream()), "col_sum");
   return out;
+}
+
+// (dx, dbias) of gelu(x + bias) in one pass; falls back to bwd + col_sum for odd shapes.
+std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Tensor bias) {
+  check_gpu(dy, "dy");
+  check_gpu(x, "x");
+  check_gpu(bias, "bias");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  TORCH_CHECK(bias.numel() == cols && bias.scalar_type() == x.scalar_type(), "bias mismatch");
+  auto dx = at::empty_like(x);
+  auto db = at::empty({cols}, x.options());
+  const int64_t parts = smpk::col_sum_parts(rows);
+  auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
+  const int rc = smpk::bias_gelu_bwd_dbias(dt_code(x), dy.data_ptr(), x.data_ptr(), bias.data_ptr(), dx.data_ptr(),
+                                           db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream());
+  if (rc == -2) {
+    dx = bias_gelu_bwd(dy, x, bias);
+    return {dx, col_sum(dx.view({rows, cols}))};
+  }
+  check(rc, "bias_gelu_bwd_dbias");
+  return {dx, db};
 }
 
 // --------------------------------------------------------------------- softmax
@@ -402,6 +423,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("col_sum", &col_sum);
+  m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias);
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);
   m.def("scaled_upper_triang_softmax_fwd", &scaled_upper_triang_softmax_fwd);
   m.def("scaled_softmax_bwd", &scaled_softmax_bwd);

@@ -102,14 +102,76 @@ __global__ void __launch_bounds__(256) col_sum_partial(const T* __restrict__ x, 
   if (rl == 0 && c < cols) part[static_cast<int64_t>(blockIdx.y) * cols + c] = s[0][cl] + s[1][cl] + s[2][cl] + s[3][cl];
 }
 
+// Fused backward + bias gradient: each thread owns one 16-byte column vector and walks
+// `rows_per_part` rows, so dbias partial sums stay in registers (dx is never re-read).
 template <typename T>
-__global__ void __launch_bounds__(256) col_sum_final(const float* __restrict__ part, T* __restrict__ out, int parts,
-                                                     int64_t cols) {
+__global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                  const T* __restrict__ bias, T* __restrict__ dx,
+                                                                  float* __restrict__ part, int64_t rows, int64_t cols,
+                                                                  int64_t rows_per_part) {
+  constexpr int N = Vec16<T>::N;
+  const int64_t c = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * N;
+  if (c >= cols) return;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
+  const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
+  float bb[N], acc[N];
+  Vec16<T> bv = load16(bias + c);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    bb[j] = to_f32(bv.v[j]);
+    acc[j] = 0.f;
+  }
+#pragma unroll 4
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t i = r * cols + c;
+    Vec16<T> a = load16(x + i);
+    Vec16<T> d = load16(dy + i);
+    Vec16<T> o;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad(to_f32(a.v[j]) + bb[j]));
+      acc[j] += to_f32(o.v[j]);
+    }
+    store16(dx + i, o);
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) part[static_cast<int64_t>(blockIdx.y) * cols + c + j] = acc[j];
+}
+
+// [parts, cols] fp32 -> [cols] in two deterministic stages (slices of parts, then slices).
+__global__ void __launch_bounds__(256) parts_reduce_stage1(const float* __restrict__ part, float* __restrict__ out,
+                                                           int parts, int64_t cols, int slices) {
+  __shared__ float s[4][64];
+  const int cl = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int64_t c = static_cast<int64_t>(blockIdx.x) * 64 + cl;
+  const int per = (parts + slices - 1) / slices;
+  const int p0 = blockIdx.y * per, p1 = min(parts, p0 + per);
+  float a = 0.f;
+  if (c < cols)
+    for (int p = p0 + pl; p < p1; p += 4) a += part[static_cast<int64_t>(p) * cols + c];
+  s[pl][cl] = a;
+  __syncthreads();
+  if (pl == 0 && c < cols) out[static_cast<int64_t>(blockIdx.y) * cols + c] = s[0][cl] + s[1][cl] + s[2][cl] + s[3][cl];
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) parts_reduce_stage2(const float* __restrict__ part, T* __restrict__ out,
+                                                           int slices, int64_t cols) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (c >= cols) return;
   float a = 0.f;
-  for (int p = 0; p < parts; ++p) a += part[p * cols + c];
+  for (int p = 0; p < slices; ++p) a += part[static_cast<int64_t>(p) * cols + c];
   out[c] = from_f32<T>(a);
+}
+
+constexpr int kReduceSlices = 32;
+
+template <typename T>
+void reduce_parts(const float* part, int parts, int64_t cols, float* work, T* out, hipStream_t s) {
+  const int slices = parts < kReduceSlices ? parts : kReduceSlices;
+  dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(slices));
+  parts_reduce_stage1<<<g, 256, 0, s>>>(part, work, parts, cols, slices);
+  parts_reduce_stage2<T><<<static_cast<unsigned>((cols + 255) / 256), 256, 0, s>>>(work, out, slices, cols);
 }
 
 inline int elt_grid(int64_t total, int per_thread) {
@@ -159,17 +221,43 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
   return static_cast<int>(hipGetLastError());
 }
 
-// workspace: parts * cols floats with parts = min(256, ceil(rows / 64)).
-int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
-  if (rows <= 0 || cols <= 0) return 0;
+// workspace: (col_sum_parts(rows) + 32) * cols floats.
+int col_sum_parts(int64_t rows) {
   int64_t parts = (rows + 63) / 64;
   if (parts > 256) parts = 256;
+  return static_cast<int>(parts < 1 ? 1 : parts);
+}
+
+int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int parts = col_sum_parts(rows);
   const int64_t rpp = (rows + parts - 1) / parts;
   SMPK_DISPATCH(dt, T, {
     dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(parts));
     col_sum_partial<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), workspace, rows, cols, rpp);
-    col_sum_final<T><<<static_cast<int>((cols + 255) / 256), 256, 0, s>>>(workspace, static_cast<T*>(out),
-                                                                        static_cast<int>(parts), cols);
+    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(out), s);
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+// dx = dy * gelu'(x + bias) and dbias = colsum(dx) in one pass over dy/x.
+// Returns -2 when the shape/alignment needs the unfused path.  workspace as col_sum.
+int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return 0;
+  const int parts = col_sum_parts(rows);
+  const int64_t rpp = (rows + parts - 1) / parts;
+  SMPK_DISPATCH(dt, T, {
+    constexpr int N = Vec16<T>::N;
+    const bool vec = bias != nullptr && (cols % N == 0) &&
+                     ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+                       reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
+    if (!vec) return -2;
+    dim3 g(static_cast<unsigned>((cols / N + 255) / 256), static_cast<unsigned>(parts));
+    bias_gelu_bwd_dbias_kernel<T><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                    static_cast<const T*>(bias), static_cast<T*>(dx), workspace,
+                                                    rows, cols, rpp);
+    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(dbias), s);
   });
   return static_cast<int>(hipGetLastError());
 }

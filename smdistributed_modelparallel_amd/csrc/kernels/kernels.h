@@ -61,6 +61,9 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
                   hipStream_t s);
 // Column sums of a [rows, cols] matrix into fp32 partials then final (for bias grads).
 int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s);
+int col_sum_parts(int64_t rows);
+int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s);
 
 // --------------------------------------------------------------- softmax (softmax.hip)
 int scaled_masked_softmax_fwd(int dt, const void* x, const uint8_t* mask, void* y, int64_t batch, int64_t heads,

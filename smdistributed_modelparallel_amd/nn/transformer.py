@@ -35,6 +35,7 @@ from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
 from ..ops.gelu import bias_gelu
+from ..ops.linear import linear
 from ..ops.rope import apply_rotary
 from ..torch.state_mod import state
 from .layer_norm import FusedLayerNorm
@@ -256,13 +257,13 @@ class DistributedAttentionLayer(DistributedModule):
         B, s, _ = a.shape
         lh, d = self.local_heads, self.attention_head_size
         if self.cross_attention:
-            q = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, lh, d)
+            q = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, lh, d)
             c = (bwd_allreduce_for_tp(cross_states) if self._tp > 1 else cross_states)
-            kv = F.linear(c, self.kv_weight, self.kv_bias).view(B, c.shape[1], 2, lh, d)
+            kv = linear(c, self.kv_weight, self.kv_bias).view(B, c.shape[1], 2, lh, d)
             k, v = kv[:, :, 0], kv[:, :, 1]
             causal, mask = False, cross_mask
         else:
-            qkv = F.linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
+            qkv = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
             if not self.rotary_dim and mask is None and not self.attention_in_fp32:
@@ -271,7 +272,7 @@ class DistributedAttentionLayer(DistributedModule):
                     window=self.window_size, training=self.training,
                     use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
                 )
-                out = F.linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
+                out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
                 return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
@@ -284,7 +285,7 @@ class DistributedAttentionLayer(DistributedModule):
             use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
         )
         ctx = ctx.reshape(B, s, lh * d)
-        out = F.linear(ctx, self.dense_weight, self.dense_bias)
+        out = linear(ctx, self.dense_weight, self.dense_bias)
         return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 
     def forward(self, inputs):
@@ -361,9 +362,9 @@ class DistributedTransformerOutputLayer(DistributedModule):
 
     def core(self, m):
         m = (bwd_allreduce_for_tp(m) if self._tp > 1 else m)
-        x = F.linear(m, self.dense1_weight)
+        x = linear(m, self.dense1_weight)
         x = _activation(x, self.activation, self.dense1_bias)
-        out = F.linear(x, self.dense2_weight, self.dense2_bias)
+        out = linear(x, self.dense2_weight, self.dense2_bias)
         return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 
     def forward(self, hidden):

@@ -23,9 +23,11 @@ class _BiasGeLU(torch.autograd.Function):
     def backward(ctx, dy):
         x, bias = ctx.saved_tensors
         C = ext()
-        dx = C.bias_gelu_bwd(dy.contiguous(), x, bias)
-        db = C.col_sum(dx.view(-1, dx.shape[-1])) if (ctx.has_bias and ctx.needs_input_grad[1]) else None
-        return dx, db
+        if ctx.has_bias and ctx.needs_input_grad[1]:
+            # one pass: dx and its column sums (the bias gradient) together
+            dx, db = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias)
+            return dx, db
+        return C.bias_gelu_bwd(dy.contiguous(), x, bias), None
 
 
 def bias_gelu(x, bias=None):

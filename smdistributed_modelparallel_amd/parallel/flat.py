@@ -121,6 +121,7 @@ class FlatParamGroup:
         for p in self.offsets:
             p.data = self.view(p, self.data)
             p.grad = self.view(p, self.grad)
+            p._smp_fused_grad = True  # ops.linear may accumulate dW straight into the view
 
     def rebind_grads(self):
         base, es = self.grad.data_ptr(), self.grad.element_size()

@@ -67,11 +67,12 @@ def test_add_layernorm(C, dt):
 
 
 @pytest.mark.parametrize("dt", DT)
-def test_bias_gelu(C, dt):
+@pytest.mark.parametrize("rows", [33, 5000])
+def test_bias_gelu(C, dt, rows):
     from smdistributed_modelparallel_amd.ops.gelu import _gelu_tanh_ref, bias_gelu
 
     torch.manual_seed(2)
-    x = torch.randn(33, 6400, device="cuda", dtype=dt, requires_grad=True)
+    x = torch.randn(rows, 6400, device="cuda", dtype=dt, requires_grad=True)
     b = torch.randn(6400, device="cuda", dtype=dt, requires_grad=True)
     y = bias_gelu(x, b)
     xr, br = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
@@ -82,7 +83,7 @@ def test_bias_gelu(C, dt):
     y.backward(g.to(dt))
     yr.backward(g)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
-    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50, rtol=tol * 4)
+    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50 * max(1, rows // 200) ** 0.5, rtol=tol * 4)
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
