@@ -18,7 +18,7 @@ import os
 
 import yaml
 
-from .exceptions import SMPConfigError, SMPInvalidArgumentError
+from .exceptions import SMPConfigError, SMPConfigTypeError, SMPInvalidArgumentError
 from .logger import get_logger
 
 logger = get_logger()
@@ -158,7 +158,7 @@ class ModelParallelConfig:
         if types is not None:
             allowed = [_TYPES[t] for t in (types if isinstance(types, list) else [types])]
             if type(value) not in allowed:
-                raise SMPInvalidArgumentError(
+                raise SMPConfigTypeError(
                     f"Config parameter {key} type needs to be one of {[t.__name__ for t in allowed]}. "
                     f"Found: {type(value).__name__}."
                 )

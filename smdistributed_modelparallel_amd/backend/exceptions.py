@@ -20,6 +20,10 @@ class SMPInvalidArgumentError(SMPValidationError, ValueError):
     pass
 
 
+class SMPConfigTypeError(SMPInvalidArgumentError, TypeError):
+    """A config value has the wrong type (a TypeError, as in the reference)."""
+
+
 class SMPConfigError(SMPValidationError):
     pass
 

@@ -206,9 +206,11 @@ class DistributedAttentionLayer(DistributedModule):
             self.kv_weight = nn.Parameter(torch.empty(2 * lh * d, h, dtype=dtype))
             self.kv_bias = nn.Parameter(torch.zeros(2 * lh * d, dtype=dtype)) if self.use_qkv_bias else None
         self.dense_weight = nn.Parameter(torch.empty(h, lh * d, dtype=dtype))
-        self.dense_bias = (
-            nn.Parameter(torch.zeros(h, dtype=dtype)) if (self.use_attn_dense_bias and tp_rank() == 0) else None
-        )
+        # row-parallel bias lives on tp_rank 0 only; other ranks register the name as None
+        # (so full checkpoints, which contain it, load everywhere)
+        self.register_parameter(
+            "dense_bias",
+            nn.Parameter(torch.zeros(h, dtype=dtype)) if (self.use_attn_dense_bias and tp_rank() == 0) else None)
         if self.pre_layernorm:
             self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:
@@ -334,7 +336,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
         self.dense1_weight = nn.Parameter(torch.empty(li, h, dtype=dtype))
         self.dense1_bias = nn.Parameter(torch.zeros(li, dtype=dtype))
         self.dense2_weight = nn.Parameter(torch.empty(h, li, dtype=dtype))
-        self.dense2_bias = nn.Parameter(torch.zeros(h, dtype=dtype)) if tp_rank() == 0 else None
+        self.register_parameter("dense2_bias", nn.Parameter(torch.zeros(h, dtype=dtype)) if tp_rank() == 0 else None)
         if self.pre_layernorm:
             self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:

@@ -59,6 +59,17 @@ class PTPipeline:
     def next_action(self):  # pragma: no cover - abstract
         raise NotImplementedError
 
+    # reference-style driver interface (`smp/torch/pipeline.py:24-79`)
+    def get_next_microbatch(self):
+        a = self.next_action()
+        return None if a is None else a[1]
+
+    def mark_ready_for_backward(self, mb):
+        self.status[mb] = MbStatus.READY_FOR_BWD
+
+    def has_more_ticks(self):
+        return not self.is_done()
+
 
 class SimplePipeline(PTPipeline):
     """All forwards first, then backwards in microbatch order."""

@@ -1,0 +1,58 @@
+"""Checkpoint save/resume round trips on multi-process CPU (gloo) worlds: the partial
+format (`{tag}_partial/model_{pp}_{tp}.pt`, optimizer_states, smp_config.pt, newest) must
+continue training bit-for-bit; full checkpoints reload into a different pp/tp layout;
+sharded-data-parallel checkpoints round-trip shards (reference `smp/torch/checkpoint.py`)."""
+import json
+import os
+
+import pytest
+
+from tests.dist_utils import run_workers
+
+
+def _phase(phase, world, ckpt, pp, tp, partial, extra=None):
+    args = [phase, ckpt, pp, tp, int(partial)]
+    if extra:
+        args.append(json.dumps(extra))
+    outs = run_workers("ckpt_gpt", world, args, timeout=240)
+    assert all("OK" in o for o in outs)
+
+
+def test_partial_roundtrip_pp2(tmp_path):
+    ckpt = str(tmp_path)
+    _phase("save", 2, ckpt, 2, 1, True)
+    names = set(os.listdir(os.path.join(ckpt, "t_partial")))
+    assert {"model_0_0.pt", "model_1_0.pt", "optimizer_states_0_0.pt", "optimizer_states_1_0.pt",
+            "smp_config.pt", "user_content.pt"} <= names, names
+    assert open(os.path.join(ckpt, "newest")).read().split() == ["t_partial"]
+    _phase("load", 2, ckpt, 2, 1, True)
+
+
+def test_partial_roundtrip_tp2_deferred(tmp_path):
+    ckpt = str(tmp_path)
+    _phase("save", 2, ckpt, 1, 2, True)
+    _phase("load", 2, ckpt, 1, 2, True, {"early_resume": True})
+
+
+def test_partial_resume_rejects_layout_change(tmp_path):
+    ckpt = str(tmp_path)
+    _phase("save", 2, ckpt, 2, 1, True)
+    with pytest.raises(AssertionError):
+        _phase("load", 2, ckpt, 1, 2, True)
+
+
+def test_full_checkpoint_into_other_layout(tmp_path):
+    ckpt = str(tmp_path)
+    _phase("save", 2, ckpt, 2, 1, False)
+    assert os.path.isfile(os.path.join(ckpt, "t"))
+    _phase("load", 2, ckpt, 1, 2, False)
+
+
+def test_sharded_dp_checkpoint(tmp_path):
+    ckpt = str(tmp_path)
+    extra = {"cfg": {"sharded_data_parallel_degree": 2, "sdp_param_persistence_threshold": 100,
+                     "sdp_reduce_bucket_size": 20000}}
+    _phase("save", 2, ckpt, 1, 1, True, extra)
+    assert {"model_0.pt", "model_1.pt", "optimizer_0.pt", "optimizer_1.pt"} <= set(
+        os.listdir(os.path.join(ckpt, "t_partial")))
+    _phase("load", 2, ckpt, 1, 1, True, extra)
