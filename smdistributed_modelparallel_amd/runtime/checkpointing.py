@@ -7,8 +7,10 @@ recompute, nested checkpointing rejected, ``smp.checkpoint(module, *args)`` and
 ``offload_activations`` the checkpointed inputs are offloaded to pinned host memory on a
 side stream and prefetched back for the recompute (`offload.py`).
 
-Built on torch's non-reentrant checkpoint (saved-tensor hooks), so it composes with the
-segmented pipeline backward without re-entering autograd.
+Without offloading this is torch's non-reentrant checkpoint (saved-tensor hooks), which
+composes with the segmented pipeline backward without re-entering autograd.  With
+offloading, a reentrant-style Function keeps the inputs only as host copies
+(`runtime/offload.py`) and recomputes + back-propagates the region inside its backward.
 """
 import functools
 
@@ -46,16 +48,107 @@ def _context_fn():
     return contextlib.nullcontext(), saved
 
 
+def _flatten(obj, out):
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+        return _TensorSlot(len(out) - 1)
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        return type(obj)(*[_flatten(o, out) for o in obj])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_flatten(o, out) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _flatten(v, out) for k, v in obj.items()}
+    return obj
+
+
+class _TensorSlot:
+    __slots__ = ("i",)
+
+    def __init__(self, i):
+        self.i = i
+
+
+def _fill(obj, tensors):
+    if isinstance(obj, _TensorSlot):
+        return tensors[obj.i]
+    if isinstance(obj, tuple) and hasattr(obj, "_fields"):
+        return type(obj)(*[_fill(o, tensors) for o in obj])
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_fill(o, tensors) for o in obj)
+    if isinstance(obj, dict):
+        return {k: _fill(v, tensors) for k, v in obj.items()}
+    return obj
+
+
+class _OffloadedCheckpoint(torch.autograd.Function):
+    """Checkpoint whose saved inputs live in pinned host memory between forward and the
+    recompute (reference `CheckpointTupledFunction` + `TensorOffloader`)."""
+
+    @staticmethod
+    def forward(ctx, run, spec, preserve_rng, offloader, *tensors):
+        ctx.run, ctx.spec, ctx.preserve_rng, ctx.offloader = run, spec, preserve_rng, offloader
+        if preserve_rng:
+            ctx.cpu_rng = torch.get_rng_state()
+            ctx.dev_rng = torch.cuda.get_rng_state() if tensors and tensors[0].is_cuda else None
+            ctx.smp_rng = _SmpRngCtx()
+        with torch.no_grad():
+            out = run(*_fill(spec, list(tensors)))
+        ctx.handles = [offloader.offload(t) if t.is_floating_point() else t for t in tensors]
+        ctx.req = [t.requires_grad for t in tensors]
+        return out
+
+    @staticmethod
+    def backward(ctx, *grads):
+        off = ctx.offloader
+        handles = [h for h in ctx.handles if not isinstance(h, torch.Tensor)]
+        if handles:
+            off.prefetch_before(handles[0])
+        inputs = [h if isinstance(h, torch.Tensor) else off.load(h) for h in ctx.handles]
+        inputs = [x.detach().requires_grad_(r) for x, r in zip(inputs, ctx.req)]
+        devices = [inputs[0].device] if inputs and inputs[0].is_cuda else []
+        with torch.random.fork_rng(devices=devices, enabled=ctx.preserve_rng):
+            if ctx.preserve_rng:
+                torch.set_rng_state(ctx.cpu_rng)
+                if ctx.dev_rng is not None:
+                    torch.cuda.set_rng_state(ctx.dev_rng)
+            rng = ctx.smp_rng if ctx.preserve_rng else None
+            with torch.enable_grad(), (rng if rng is not None else _nullctx()):
+                out = ctx.run(*_fill(ctx.spec, inputs))
+        outs = out if isinstance(out, tuple) else (out,)
+        pairs = [(o, g) for o, g in zip(outs, grads) if isinstance(o, torch.Tensor) and o.requires_grad
+                 and g is not None]
+        if pairs:
+            torch.autograd.backward([o for o, _ in pairs], [g for _, g in pairs])
+        return (None, None, None, None) + tuple(x.grad if r else None for x, r in zip(inputs, ctx.req))
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def offloaded_checkpoint(fn, offloader, *args, preserve_rng_state=True, **kwargs):
+    """Run fn(*args, **kwargs) checkpointed, its tensor inputs parked on the host."""
+    tensors = []
+    spec = _flatten((args, kwargs), tensors)
+
+    def run(a, k):
+        return fn(*a, **k)
+
+    return _OffloadedCheckpoint.apply(run, spec, preserve_rng_state, offloader, *tensors)
+
+
 def checkpoint_call(fn, preserve_rng_state, *args, **kwargs):
     if _depth[0] > 0:
         raise CheckpointingError("nested activation checkpointing is not supported")
     _depth[0] += 1
     try:
         offloader = state.current_offloader if (state.cfg is not None and state.cfg.offload_activations) else None
-        if offloader is not None:
-            with offloader.save_on_host():
-                return _torch_checkpoint(fn, *args, use_reentrant=False, preserve_rng_state=preserve_rng_state,
-                                         context_fn=_context_fn, **kwargs)
+        if offloader is not None and torch.is_grad_enabled():
+            return offloaded_checkpoint(fn, offloader, *args, preserve_rng_state=preserve_rng_state, **kwargs)
         return _torch_checkpoint(fn, *args, use_reentrant=False, preserve_rng_state=preserve_rng_state,
                                  context_fn=_context_fn, **kwargs)
     finally:

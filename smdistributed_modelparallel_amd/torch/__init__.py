@@ -117,6 +117,10 @@ def init(config=None):
     seed = cfg.tensor_parallel_seed + 1000 * core.pp_rank() + 100000 * core.rdp_rank()
     state.rng_manager = RngManager(seed, state.device)
     state.create_process_groups()
+    if cfg.offload_activations:
+        from ..runtime.offload import create_offloader
+
+        state.current_offloader = create_offloader(cfg, state.device)
     state.transport = PipelineTransport(core, state.pgs, state.device)
     state.initialized = True
     _patch_module_init()

@@ -73,6 +73,8 @@ class StepFunction:
         state.current_step_fn_id = self.id
         core = state.core
         core.timeline_start_step(state.step_count)
+        if state.current_offloader is not None:
+            state.current_offloader.reset()
         num_mb = state.cfg.microbatches
         state.in_step_func = True
         try:

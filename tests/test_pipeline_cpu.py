@@ -71,3 +71,11 @@ def test_sharded_dp2():
 
 def test_sharded_dp2_replicas2_activation_checkpointing():
     _run(4, 1, 1, 2, extra={"cfg": dict(_SDP, sharded_data_parallel_degree=2), "ckpt_layers": True})
+
+
+def test_activation_offloading_with_checkpointing():
+    _run(2, 1, 1, 2, extra={"ckpt_layers": True, "cfg": {"offload_activations": True}})
+
+
+def test_pp2_activation_offloading():
+    _run(2, 2, 1, 2, extra={"ckpt_layers": True, "cfg": {"offload_activations": True}})

@@ -108,6 +108,10 @@ def main():
         t = slice_for_param(full, p, smp.tp_rank(), smp.tp_size())
         worst = max(worst, (p.detach().float() - t.float()).abs().max().item())
     assert worst < 2e-4, worst
+    if extra.get("cfg", {}).get("offload_activations") and smp.state.current_offloader is not None:
+        st = smp.state.current_offloader.stats
+        # every rank that runs checkpointed layers must have offloaded and reloaded them
+        assert st["offloaded_bytes"] > 0 and st["loaded_bytes"] == st["offloaded_bytes"], st
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
 
