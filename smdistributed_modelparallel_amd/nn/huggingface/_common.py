@@ -1,0 +1,149 @@
+"""Shared pieces of the HF integrations: key rewriting with arbitrary prefixes, fused-QKV
+packing, output wrappers and mask normalisation (transformers 5.x conventions)."""
+import re
+
+import torch
+
+
+def split_prefix(key, pattern):
+    """Match `pattern` (a regex anchored at a module boundary) anywhere in `key`; return
+    (prefix, groups) or None."""
+    m = re.match(r"^(.*?)" + pattern + r"$", key)
+    if m is None:
+        return None
+    return m.group(1), m.groups()[1:]
+
+
+class KeyMap:
+    """Bidirectional per-tensor key rules: (hf_regex, smp_template, kind) where kind is
+    'copy' or 't' (Conv1D weights are stored transposed in HF GPT-2)."""
+
+    def __init__(self, rules):
+        self.rules = rules
+
+    def hf_to_smp(self, sd, out):
+        rest = {}
+        for k, v in sd.items():
+            for hf, smp, kind in self.rules:
+                m = re.match(r"^(.*?)" + hf + r"$", k)
+                if m:
+                    pre = m.group(1)
+                    key = pre + smp.format(*m.groups()[1:])
+                    out[key] = v.t().contiguous() if kind == "t" else v
+                    break
+            else:
+                rest[k] = v
+        return rest
+
+    def smp_to_hf(self, sd, out):
+        rest = {}
+        for k, v in sd.items():
+            for hf, smp, kind in self.rules:
+                smp_re = re.escape(smp).replace(r"\{\}", r"(\d+)")
+                m = re.match(r"^(.*?)" + smp_re + r"$", k)
+                if m:
+                    pre = m.group(1)
+                    hf_key = _fill_regex(hf, m.groups()[1:])
+                    out[pre + hf_key] = v.t().contiguous() if kind == "t" else v
+                    break
+            else:
+                rest[k] = v
+        return rest
+
+
+def _fill_regex(pattern, groups):
+    it = iter(groups)
+    s = re.sub(r"\(\\d\+\)", lambda _: next(it), pattern)
+    return s.replace("\\.", ".")
+
+
+def pack_qkv(sd, out, q_re, k_re, v_re, smp_fmt, bias=False):
+    """Concatenate separate q/k/v projections into the fused [3*h, h] (or [3*h]) layout."""
+    qs = {}
+    rest = {}
+    for k, v in sd.items():
+        for role, pat in (("q", q_re), ("k", k_re), ("v", v_re)):
+            m = re.match(r"^(.*?)" + pat + r"$", k)
+            if m:
+                qs.setdefault((m.group(1), m.groups()[1:]), {})[role] = v
+                break
+        else:
+            rest[k] = v
+    for (pre, groups), parts in qs.items():
+        if len(parts) != 3:
+            raise KeyError(f"incomplete q/k/v set for {pre}{groups}")
+        out[pre + smp_fmt.format(*groups)] = torch.cat([parts["q"], parts["k"], parts["v"]], dim=0)
+    return rest
+
+
+def unpack_qkv(sd, out, smp_re, q_fmt, k_fmt, v_fmt):
+    rest = {}
+    for k, v in sd.items():
+        m = re.match(r"^(.*?)" + smp_re + r"$", k)
+        if m:
+            pre, groups = m.group(1), m.groups()[1:]
+            q, kk, vv = v.chunk(3, dim=0)
+            out[pre + q_fmt.format(*groups)] = q
+            out[pre + k_fmt.format(*groups)] = kk
+            out[pre + v_fmt.format(*groups)] = vv
+        else:
+            rest[k] = v
+    return rest
+
+
+def masked_from_hf(mask):
+    """HF attention mask (2-D keep-mask, 4-D additive float, or 4-D bool keep-mask) ->
+    bool [B, 1, sq|1, sk] with True = masked, or None."""
+    if mask is None:
+        return None
+    if mask.dim() == 2:
+        return (mask == 0).view(mask.shape[0], 1, 1, mask.shape[1])
+    if mask.dtype == torch.bool:
+        return ~mask
+    return mask < 0
+
+
+def causal_lm_output(out, labels_given):
+    from transformers.modeling_outputs import CausalLMOutputWithCrossAttentions
+
+    if labels_given:
+        loss, logits = out
+        return CausalLMOutputWithCrossAttentions(loss=loss, logits=logits)
+    return CausalLMOutputWithCrossAttentions(logits=out)
+
+
+def lm_forward_hook(input_ids=None, *args, attention_mask=None, token_type_ids=None, position_ids=None,
+                    labels=None, past_key_values=None, use_cache=None, **kwargs):
+    """HF *ForCausalLM call signature -> DistributedTransformerLMHead inputs."""
+    if args:
+        # positional past_key_values (the HF signature's 2nd argument)
+        past_key_values = args[0] if past_key_values is None else past_key_values
+    if past_key_values is not None:
+        raise NotImplementedError("past_key_values (incremental decoding) is not supported by the distributed LM head")
+    if kwargs.get("inputs_embeds") is not None:
+        raise NotImplementedError("inputs_embeds is not supported by the distributed LM head")
+    return ((input_ids, attention_mask, token_type_ids, position_ids, labels),), {}
+
+
+def lm_return_hook(out):
+    # the LM head returns (loss, logits) when labels were given, else logits
+    return causal_lm_output(out, isinstance(out, tuple))
+
+
+def encoder_forward_hook(hidden_states, attention_mask=None, *args, **kwargs):
+    return ((hidden_states, masked_from_hf(attention_mask)),), {}
+
+
+def encoder_return_hook(out):
+    from transformers.modeling_outputs import BaseModelOutputWithPastAndCrossAttentions
+
+    return BaseModelOutputWithPastAndCrossAttentions(last_hidden_state=out[0])
+
+
+def add_tied(sd, src_suffix, dst_suffix):
+    """Re-materialise a tied weight (deduplicated in smp state dicts) under its HF name."""
+    for k in list(sd.keys()):
+        if k.endswith(src_suffix):
+            dst = k[: -len(src_suffix)] + dst_suffix
+            sd.setdefault(dst, sd[k])
+    return sd

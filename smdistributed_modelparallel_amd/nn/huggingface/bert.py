@@ -1,0 +1,77 @@
+"""BERT / RoBERTa encoders (HF ``BertEncoder`` / ``RobertaEncoder``) <-> ``DistributedTransformer``.
+
+Reference: `smp/torch/nn/huggingface/bert.py`, `roberta.py`.  Post-LayerNorm layers,
+bidirectional attention with the HF padding mask, exact-erf GeLU (``hidden_act="gelu"``).
+Only the encoder stack is distributed; embeddings and pooler stay HF modules, so keys
+keep their ``...encoder.`` prefix: ``encoder.layer.{i}.*`` <-> ``encoder.seq_layers.{i}.*``.
+"""
+from ._common import KeyMap, encoder_forward_hook, encoder_return_hook, pack_qkv, unpack_qkv
+
+_L = r"encoder\.layer\.(\d+)\."
+_S = "encoder.seq_layers.{}."
+RULES = KeyMap([
+    (_L + r"attention\.output\.dense\.weight", _S + "attention.dense_weight", "copy"),
+    (_L + r"attention\.output\.dense\.bias", _S + "attention.dense_bias", "copy"),
+    (_L + r"attention\.output\.LayerNorm\.weight", _S + "attention.layernorm.weight", "copy"),
+    (_L + r"attention\.output\.LayerNorm\.bias", _S + "attention.layernorm.bias", "copy"),
+    (_L + r"intermediate\.dense\.weight", _S + "output.dense1_weight", "copy"),
+    (_L + r"intermediate\.dense\.bias", _S + "output.dense1_bias", "copy"),
+    (_L + r"output\.dense\.weight", _S + "output.dense2_weight", "copy"),
+    (_L + r"output\.dense\.bias", _S + "output.dense2_bias", "copy"),
+    (_L + r"output\.LayerNorm\.weight", _S + "output.layernorm.weight", "copy"),
+    (_L + r"output\.LayerNorm\.bias", _S + "output.layernorm.bias", "copy"),
+])
+
+_ACT = {"gelu": "gelu_exact", "gelu_new": "gelu", "gelu_pytorch_tanh": "gelu", "relu": "relu"}
+
+
+def config_to_kwargs(config):
+    h = config.hidden_size
+    return {
+        "num_layers": config.num_hidden_layers,
+        "num_attention_heads": config.num_attention_heads,
+        "attention_head_size": h // config.num_attention_heads,
+        "hidden_size": h,
+        "intermediate_size": config.intermediate_size,
+        "attention_dropout_prob": config.attention_probs_dropout_prob,
+        "hidden_dropout_prob": config.hidden_dropout_prob,
+        "activation": _ACT.get(config.hidden_act, "gelu_exact"),
+        "layernorm_epsilon": config.layer_norm_eps,
+        "initializer_range": config.initializer_range,
+        "use_normal_initialization": True,
+        "causal_mask_size": None,
+        "pre_layernorm": False,
+        "post_layernorm": True,
+    }
+
+
+def init_hook(config, *args, **kwargs):
+    return (), config_to_kwargs(config)
+
+
+forward_hook = encoder_forward_hook
+return_hook = encoder_return_hook
+
+
+def hf_to_smp(sd):
+    out = {}
+    rest = pack_qkv(sd, out, _L + r"attention\.self\.query\.weight", _L + r"attention\.self\.key\.weight",
+                    _L + r"attention\.self\.value\.weight", _S + "attention.qkv_weight")
+    rest = pack_qkv(rest, out, _L + r"attention\.self\.query\.bias", _L + r"attention\.self\.key\.bias",
+                    _L + r"attention\.self\.value\.bias", _S + "attention.qkv_bias")
+    rest = RULES.hf_to_smp(rest, out)
+    out.update(rest)
+    return out
+
+
+def smp_to_hf(sd):
+    out = {}
+    rest = unpack_qkv(sd, out, r"encoder\.seq_layers\.(\d+)\.attention\.qkv_weight",
+                      "encoder.layer.{}.attention.self.query.weight", "encoder.layer.{}.attention.self.key.weight",
+                      "encoder.layer.{}.attention.self.value.weight")
+    rest = unpack_qkv(rest, out, r"encoder\.seq_layers\.(\d+)\.attention\.qkv_bias",
+                      "encoder.layer.{}.attention.self.query.bias", "encoder.layer.{}.attention.self.key.bias",
+                      "encoder.layer.{}.attention.self.value.bias")
+    rest = RULES.smp_to_hf(rest, out)
+    out.update(rest)
+    return out

@@ -141,7 +141,8 @@ def model_load_state_dict(model, sd, strict=True, translate_function=None, same_
         for n, b in buffers.items():
             if n in sd and b is not None:
                 b.copy_(sd[n].to(b.device, b.dtype))
-    all_names = {n for n, _ in model.module.named_parameters()} | {n for n, _ in model.module.named_buffers()}
+    all_names = {n for n, _ in model.module.named_parameters(remove_duplicate=False)} | \
+        {n for n, _ in model.module.named_buffers()}
     # parameters registered as None here but present on another TP rank (rank-0-only biases)
     for mn, m in model.module.named_modules():
         for pn, pv in m._parameters.items():

@@ -19,17 +19,19 @@ logger = get_logger()
 
 
 class _Entry:
-    def __init__(self, dist_cls, init_hook, forward_hook, return_hook):
+    def __init__(self, dist_cls, init_hook, forward_hook, return_hook, translate_functions=None):
         self.dist_cls = dist_cls
         self.init_hook = init_hook
         self.forward_hook = forward_hook
         self.return_hook = return_hook
+        self.translate_functions = tuple(translate_functions) if translate_functions is not None else None
 
 
 class TensorParallelismRegistry:
     def __init__(self):
         self._entries = {}
         self._patched = {}
+        # (smp_to_hf, hf_to_smp) of the module types actually replaced in this model
         self.translate_functions = []
 
     def register_builtins(self):
@@ -49,9 +51,7 @@ class TensorParallelismRegistry:
 
     def register(self, module_cls, dist_cls, init_hook=None, forward_hook=None, return_hook=None,
                  translate_functions=None):
-        self._entries[module_cls] = _Entry(dist_cls, init_hook, forward_hook, return_hook)
-        if translate_functions is not None:
-            self.translate_functions.append(tuple(translate_functions))
+        self._entries[module_cls] = _Entry(dist_cls, init_hook, forward_hook, return_hook, translate_functions)
         self._patch_init(module_cls)
 
     def is_supported(self, cls):
@@ -88,6 +88,8 @@ class TensorParallelismRegistry:
                 if accepted is None or k in accepted:
                     kwargs[k] = v
         dist_mod = e.dist_cls(*args, **kwargs)
+        if e.translate_functions is not None and e.translate_functions not in self.translate_functions:
+            self.translate_functions.append(e.translate_functions)
         if e.forward_hook is not None or e.return_hook is not None:
             fwd = dist_mod.forward
             fh, rh = e.forward_hook, e.return_hook

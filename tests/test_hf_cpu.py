@@ -1,0 +1,115 @@
+"""HF transformers integration: config translation + state-dict translators reproduce the
+HF models' outputs with the smp distributed modules (single process, fp32, CPU), and a
+TP=2 gloo run of an HF GPT-2 auto-replaced through ``smp.model_creation`` matches HF.
+(The reference pins the same through `test/torch/mpi/test_translate_state_dict.py` and
+its model zoo; parity here is against the installed transformers 5.x models.)"""
+import pytest
+import torch
+
+transformers = pytest.importorskip("transformers")
+
+from smdistributed_modelparallel_amd.nn import DistributedTransformer, DistributedTransformerLMHead  # noqa: E402
+from tests.dist_utils import run_workers  # noqa: E402
+
+
+def _lm_parity(hf_model, mod, vocab, seq=16, atol=2e-4):
+    torch.manual_seed(0)
+    hf_model.eval()
+    smp_model = DistributedTransformerLMHead(**mod.config_to_kwargs(hf_model.config))
+    smp_model.eval()
+    sd = mod.hf_to_smp(hf_model.state_dict())
+    missing, unexpected = smp_model.load_state_dict(sd, strict=False)
+    assert not missing, missing
+    assert not [k for k in unexpected if "bias" not in k or "attn" not in k], unexpected
+    ids = torch.randint(0, vocab, (2, seq))
+    with torch.no_grad():
+        ref = hf_model(input_ids=ids, labels=ids)
+        loss, logits = smp_model((ids, None, None, None, ids))
+    assert torch.allclose(logits, ref.logits, atol=atol, rtol=1e-3), (logits - ref.logits).abs().max()
+    assert abs(loss.item() - ref.loss.item()) < 1e-4
+    # and back: smp -> HF keys reproduce the HF state dict exactly
+    back = mod.smp_to_hf(smp_model.state_dict())
+    hf_sd = hf_model.state_dict()
+    for k, v in hf_sd.items():
+        if k in back:
+            assert torch.equal(back[k], v), k
+    assert len([k for k in hf_sd if k not in back]) == 0, [k for k in hf_sd if k not in back][:5]
+
+
+def test_gpt2_parity():
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gpt2
+
+    cfg = GPT2Config(n_layer=2, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0)
+    _lm_parity(GPT2LMHeadModel(cfg), gpt2, 97)
+
+
+def test_gptj_parity():
+    from transformers import GPTJConfig, GPTJForCausalLM
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gptj
+
+    cfg = GPTJConfig(n_layer=2, n_embd=64, n_head=4, rotary_dim=8, vocab_size=97, n_positions=32, bos_token_id=0,
+                     eos_token_id=0)
+    _lm_parity(GPTJForCausalLM(cfg), gptj, 97)
+
+
+def test_gptneo_parity():
+    from transformers import GPTNeoConfig, GPTNeoForCausalLM
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gptneo
+
+    cfg = GPTNeoConfig(num_layers=2, hidden_size=64, num_heads=4, vocab_size=97, max_position_embeddings=32,
+                       attention_types=[[["global", "local"], 1]], window_size=5, bos_token_id=0, eos_token_id=0)
+    _lm_parity(GPTNeoForCausalLM(cfg), gptneo, 97)
+
+
+def test_gptneox_parity():
+    from transformers import GPTNeoXConfig, GPTNeoXForCausalLM
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gptneox
+
+    cfg = GPTNeoXConfig(num_hidden_layers=2, hidden_size=64, num_attention_heads=4, intermediate_size=256,
+                        vocab_size=97, max_position_embeddings=32, bos_token_id=0, eos_token_id=0)
+    _lm_parity(GPTNeoXForCausalLM(cfg), gptneox, 97)
+
+
+@pytest.mark.parametrize("family", ["bert", "roberta"])
+def test_encoder_parity(family):
+    if family == "bert":
+        from transformers import BertConfig as C
+        from transformers import BertModel as M
+
+        from smdistributed_modelparallel_amd.nn.huggingface import bert as mod
+    else:
+        from transformers import RobertaConfig as C
+        from transformers import RobertaModel as M
+
+        from smdistributed_modelparallel_amd.nn.huggingface import roberta as mod
+    torch.manual_seed(0)
+    hf = M(C(num_hidden_layers=2, hidden_size=64, num_attention_heads=4, intermediate_size=128, vocab_size=97,
+             max_position_embeddings=40, pad_token_id=1))
+    hf.eval()
+    enc = DistributedTransformer(**mod.config_to_kwargs(hf.config))
+    enc.eval()
+    sd = {k[len("encoder."):] if k.startswith("encoder.") else k: v
+          for k, v in mod.hf_to_smp({k: v for k, v in hf.state_dict().items() if k.startswith("encoder.")}).items()}
+    missing, _ = enc.load_state_dict(sd, strict=False)
+    assert not missing, missing
+    ids = torch.randint(2, 97, (2, 12))
+    am = torch.ones(2, 12, dtype=torch.long)
+    am[1, 8:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=ids, attention_mask=am).last_hidden_state
+        emb = hf.embeddings(input_ids=ids)
+        from smdistributed_modelparallel_amd.nn.huggingface._common import masked_from_hf
+
+        out = enc((emb, masked_from_hf(am)))[0]
+    valid = am.bool()
+    assert torch.allclose(out[valid], ref[valid], atol=2e-4, rtol=1e-3), (out[valid] - ref[valid]).abs().max()
+
+
+def test_hf_gpt2_auto_tp2_matches_hf():
+    outs = run_workers("hf_gpt2_tp", 2, [], timeout=240)
+    assert all("OK" in o for o in outs)
