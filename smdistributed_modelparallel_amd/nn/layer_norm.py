@@ -105,6 +105,10 @@ class DistributedLayerNorm(nn.Module):
             self.bias = nn.Parameter(torch.zeros(self.local_dim, device=device, dtype=dtype))
             self.weight._smp_scaled_batch = True
             self.bias._smp_scaled_batch = True
+            from .utils import mark_tp
+
+            mark_tp(self.weight, 0)
+            mark_tp(self.bias, 0)
         else:
             self.register_parameter("weight", None)
             self.register_parameter("bias", None)

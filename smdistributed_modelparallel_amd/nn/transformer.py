@@ -38,7 +38,7 @@ from ..ops.gelu import bias_gelu
 from ..ops.linear import linear
 from ..ops.rope import apply_rotary
 from ..torch.state_mod import state
-from .layer_norm import FusedLayerNorm
+from .layer_norm import DistributedLayerNorm, FusedLayerNorm
 from .utils import (
     allgather_for_tp,
     bwd_allreduce_for_tp,
@@ -49,6 +49,8 @@ from .utils import (
     mark_scaled_batch,
     mark_tp,
     narrow_for_tp,
+    reduce_scatter_for_tp,
+    scatter_and_merge_for_tp,
     shard_sequence,
     tp_group,
     tp_rank,
@@ -144,6 +146,8 @@ class DistributedModule(nn.Module):
             # the TP degree is fixed at construction: modules built before smp.init (or
             # outside the distributed path) stay unsharded and never communicate
             self.__dict__["_tp"] = tp_size()
+            # optimize="memory": activations between layers are sharded on the hidden dim
+            self.__dict__["_mem"] = self.__dict__["_tp"] > 1 and state.initialized and state.cfg.optimize == "memory"
             try:
                 orig(self, *a, **k)
             finally:
@@ -200,8 +204,19 @@ class DistributedAttentionLayer(DistributedModule):
         self.full_attn = self.num_attention_heads * d
         dtype = _param_dtype()
         n_proj = 1 if self.cross_attention else 3
-        self.qkv_weight = nn.Parameter(torch.empty(n_proj * lh * d, h, dtype=dtype))
-        self.qkv_bias = nn.Parameter(torch.zeros(n_proj * lh * d, dtype=dtype)) if self.use_qkv_bias else None
+        if self._mem:
+            if self.cross_attention:
+                raise SMPInvalidArgumentError("cross attention is not supported with optimize='memory'")
+            # input-partitioned projection: [3 * all heads, local hidden]; the partial
+            # products are reduce-scattered onto each rank's heads
+            self.local_hidden = get_local_channels(h)
+            self.qkv_weight = nn.Parameter(torch.empty(n_proj * self.full_attn, self.local_hidden, dtype=dtype))
+            self.register_parameter(
+                "qkv_bias", nn.Parameter(torch.zeros(n_proj * self.full_attn, dtype=dtype))
+                if (self.use_qkv_bias and tp_rank() == 0) else None)
+        else:
+            self.qkv_weight = nn.Parameter(torch.empty(n_proj * lh * d, h, dtype=dtype))
+            self.qkv_bias = nn.Parameter(torch.zeros(n_proj * lh * d, dtype=dtype)) if self.use_qkv_bias else None
         if self.cross_attention:
             self.kv_weight = nn.Parameter(torch.empty(2 * lh * d, h, dtype=dtype))
             self.kv_bias = nn.Parameter(torch.zeros(2 * lh * d, dtype=dtype)) if self.use_qkv_bias else None
@@ -211,19 +226,25 @@ class DistributedAttentionLayer(DistributedModule):
         self.register_parameter(
             "dense_bias",
             nn.Parameter(torch.zeros(h, dtype=dtype)) if (self.use_attn_dense_bias and tp_rank() == 0) else None)
+        LN = DistributedLayerNorm if self._mem else FusedLayerNorm
         if self.pre_layernorm:
-            self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            self.pre_layernorm_module = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:
-            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            self.layernorm = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         self.dropout = _Dropout(self.hidden_dropout_prob)
         self.input_layer = True
         self.output_layer = True
         self.reset_parameters()
         for p in self.parameters():
             mark_scaled_batch(p)
-        mark_tp(self.qkv_weight, 0, n_proj, unit=d)
-        if self.qkv_bias is not None:
-            mark_tp(self.qkv_bias, 0, n_proj, unit=d)
+        if self._mem:
+            mark_tp(self.qkv_weight, 1)
+            if self.qkv_bias is not None:
+                mark_tp(self.qkv_bias, None, rank0_only=True)
+        else:
+            mark_tp(self.qkv_weight, 0, n_proj, unit=d)
+            if self.qkv_bias is not None:
+                mark_tp(self.qkv_bias, 0, n_proj, unit=d)
         if self.cross_attention:
             mark_tp(self.kv_weight, 0, 2, unit=d)
             if self.kv_bias is not None:
@@ -255,6 +276,8 @@ class DistributedAttentionLayer(DistributedModule):
     def core(self, a, mask=None, cross_states=None, cross_mask=None):
         """a: [B, s, h] (already normalised). Returns the dense output after the TP
         all-reduce (bias included), [B, s, h]."""
+        if self._mem:
+            return self._core_memory(a, mask)
         a = (bwd_allreduce_for_tp(a) if self._tp > 1 else a)
         B, s, _ = a.shape
         lh, d = self.local_heads, self.attention_head_size
@@ -290,6 +313,32 @@ class DistributedAttentionLayer(DistributedModule):
         out = linear(ctx, self.dense_weight, self.dense_bias)
         return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 
+    def _core_memory(self, a, mask):
+        """optimize='memory': a is [B, s, h/tp] (hidden-sharded).  Partial QKV products
+        are reduce-scattered onto this rank's heads; the dense output is reduce-scattered
+        back onto this rank's hidden slice (reference `transformer.py:1430-1541`)."""
+        B, s, _ = a.shape
+        lh, d, nh = self.local_heads, self.attention_head_size, self.num_attention_heads
+        part = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, self.full_attn)
+        head_sizes = [get_local_channels(nh, r) * d for r in range(self._tp)]
+        qkv = reduce_scatter_for_tp(part, 3, head_sizes).view(B, s, 3, lh, d)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        causal = self.causal_mask_size is not None
+        if self.rotary_dim:
+            base = self.rotary_emb_base or 10000
+            q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
+            k = apply_rotary(k, self.rotary_dim, base, self.gpt_neox_type_rotary)
+        if not self.rotary_dim and mask is None and not self.attention_in_fp32:
+            ctx = attention_packed(qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
+                                   window=self.window_size, training=self.training,
+                                   use_flash=state.cfg.amd_fused_attention)
+        else:
+            ctx = attention_op(q, k, v, causal=causal, mask=mask, scale=self._scale(),
+                               dropout_p=self.attention_dropout_prob, window=self.window_size, training=self.training,
+                               attention_in_fp32=self.attention_in_fp32, use_flash=state.cfg.amd_fused_attention)
+        out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
+        return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
+
     def forward(self, inputs):
         if self.cross_attention:
             hidden, mask, cross_states, cross_mask = inputs
@@ -297,19 +346,35 @@ class DistributedAttentionLayer(DistributedModule):
             hidden, mask = inputs[0], inputs[1]
             cross_states = cross_mask = None
         if self._tp > 1 and self.input_layer and not _prescaled():
-            hidden = allgather_for_tp(hidden, 0)
+            hidden = _enter_tp(hidden, self._mem, self.hidden_size)
             mask = _gather_mask(mask)
         a = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
         out = self.dropout(self.core(a, mask, cross_states, cross_mask)) + hidden
         if self.post_layernorm:
             out = self.layernorm(out)
         if self._tp > 1 and self.output_layer and not _prescaled():
-            out = narrow_for_tp(out, 0)
+            out = _leave_tp(out, self._mem, self.hidden_size)
         return (out,) + tuple(inputs[1:])
 
 
 def _prescaled():
     return state.initialized and state.cfg.prescaled_batch
+
+
+def _enter_tp(hidden, mem, h):
+    """Local batch [b, s, h] -> the layout inside the TP stack: full TP-group batch
+    [B, s, h] (speed) or [B, s, h/tp] hidden-sharded (memory, one all-to-all)."""
+    if mem:
+        return scatter_and_merge_for_tp(hidden, 2, 0, get_merge_shapes(h), None)
+    return allgather_for_tp(hidden, 0)
+
+
+def _leave_tp(out, mem, h, full_batch=False):
+    if mem:
+        if full_batch:
+            return allgather_for_tp(out, 2, get_merge_shapes(h))
+        return scatter_and_merge_for_tp(out, 0, 2, None, get_merge_shapes(h))
+    return out if full_batch else narrow_for_tp(out, 0)
 
 
 def _gather_mask(mask):
@@ -333,22 +398,34 @@ class DistributedTransformerOutputLayer(DistributedModule):
         self.local_inter = get_local_channels(self.intermediate_size)
         h, li = self.hidden_size, self.local_inter
         dtype = _param_dtype()
-        self.dense1_weight = nn.Parameter(torch.empty(li, h, dtype=dtype))
-        self.dense1_bias = nn.Parameter(torch.zeros(li, dtype=dtype))
+        if self._mem:
+            # input-partitioned first projection: [intermediate, local hidden], bias on rank 0
+            self.dense1_weight = nn.Parameter(torch.empty(self.intermediate_size, get_local_channels(h), dtype=dtype))
+            self.register_parameter("dense1_bias", nn.Parameter(torch.zeros(self.intermediate_size, dtype=dtype))
+                                    if tp_rank() == 0 else None)
+        else:
+            self.dense1_weight = nn.Parameter(torch.empty(li, h, dtype=dtype))
+            self.dense1_bias = nn.Parameter(torch.zeros(li, dtype=dtype))
         self.dense2_weight = nn.Parameter(torch.empty(h, li, dtype=dtype))
         self.register_parameter("dense2_bias", nn.Parameter(torch.zeros(h, dtype=dtype)) if tp_rank() == 0 else None)
+        LN = DistributedLayerNorm if self._mem else FusedLayerNorm
         if self.pre_layernorm:
-            self.pre_layernorm_module = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            self.pre_layernorm_module = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:
-            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            self.layernorm = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         self.dropout = _Dropout(self.hidden_dropout_prob)
         self.input_layer = True
         self.output_layer = True
         self.reset_parameters()
         for p in self.parameters():
             mark_scaled_batch(p)
-        mark_tp(self.dense1_weight, 0)
-        mark_tp(self.dense1_bias, 0)
+        if self._mem:
+            mark_tp(self.dense1_weight, 1)
+            if self.dense1_bias is not None:
+                mark_tp(self.dense1_bias, None, rank0_only=True)
+        else:
+            mark_tp(self.dense1_weight, 0)
+            mark_tp(self.dense1_bias, 0)
         mark_tp(self.dense2_weight, 1)
         if self.dense2_bias is not None:
             mark_tp(self.dense2_bias, None, rank0_only=True)
@@ -358,11 +435,19 @@ class DistributedTransformerOutputLayer(DistributedModule):
         init_weight_(self.dense1_weight, self.hidden_size, self.intermediate_size, r, normal)
         init_weight_(self.dense2_weight, self.intermediate_size, self.hidden_size, r, normal)
         with torch.no_grad():
-            self.dense1_bias.zero_()
+            if self.dense1_bias is not None:
+                self.dense1_bias.zero_()
             if self.dense2_bias is not None:
                 self.dense2_bias.zero_()
 
     def core(self, m):
+        if self._mem:
+            # m: [B, s, h/tp]; partial products reduce-scattered on the output channels
+            x = linear(m, self.dense1_weight, self.dense1_bias)
+            x = reduce_scatter_for_tp(x, 2, get_merge_shapes(self.intermediate_size))
+            x = _activation(x, self.activation, None)
+            out = linear(x, self.dense2_weight, self.dense2_bias)
+            return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
         m = (bwd_allreduce_for_tp(m) if self._tp > 1 else m)
         x = linear(m, self.dense1_weight)
         x = _activation(x, self.activation, self.dense1_bias)
@@ -371,13 +456,13 @@ class DistributedTransformerOutputLayer(DistributedModule):
 
     def forward(self, hidden):
         if self._tp > 1 and self.input_layer and not _prescaled():
-            hidden = allgather_for_tp(hidden, 0)
+            hidden = _enter_tp(hidden, self._mem, self.hidden_size)
         m = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
         out = self.dropout(self.core(m)) + hidden
         if self.post_layernorm:
             out = self.layernorm(out)
         if self._tp > 1 and self.output_layer and not _prescaled():
-            out = narrow_for_tp(out, 0)
+            out = _leave_tp(out, self._mem, self.hidden_size)
         return out
 
 
@@ -412,7 +497,7 @@ class DistributedTransformerLayer(DistributedModule):
     def forward(self, inputs):
         hidden, mask = inputs[0], inputs[1]
         if self._tp > 1 and self.input_layer and not _prescaled():
-            hidden = allgather_for_tp(hidden, 0)
+            hidden = _enter_tp(hidden, self._mem, self.hidden_size)
             mask = _gather_mask(mask)
         at, out = self.attention, self.output
         if self.parallel_attn_output:
@@ -444,7 +529,9 @@ class DistributedTransformerLayer(DistributedModule):
             if out.post_layernorm:
                 hidden = out.layernorm(hidden)
         if self._tp > 1 and self.output_layer and not _prescaled():
-            hidden = narrow_for_tp(hidden, 0)
+            hidden = _leave_tp(hidden, self._mem, self.hidden_size)
+        elif self._tp > 1 and self._mem and getattr(self, "_full_batch_out", False):
+            hidden = _leave_tp(hidden, True, self.hidden_size, full_batch=True)
         return (hidden,) + tuple(inputs[1:])
 
 
@@ -479,6 +566,8 @@ class DistributedTransformer(DistributedModule):
             nxt = partition_of(layers[i + 1]) if (partition_of and i + 1 < len(layers)) else p
             layer.input_layer = i == 0 or prev != p
             layer.output_layer = (i == len(layers) - 1 and not self._output_full_batch) or nxt != p
+            # memory mode + full-batch output (vocab-parallel head): un-shard the hidden dim
+            layer._full_batch_out = i == len(layers) - 1 and self._output_full_batch
             for sub in (layer.attention, layer.output):
                 sub.input_layer = False
                 sub.output_layer = False

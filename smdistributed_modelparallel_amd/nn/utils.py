@@ -136,7 +136,21 @@ def _all_to_all(x, split_dim, merge_dim, split_sizes=None, merge_sizes=None):
         out_shapes.append(s)
     outs = [x.new_empty(s) for s in out_shapes]
     # each received piece r has this rank's split slice and rank r's merge extent
-    dist.all_to_all(outs, pieces, group=tp_group())
+    group = tp_group()
+    if x.is_cuda:
+        dist.all_to_all(outs, pieces, group=group)  # RCCL all-to-all over xGMI
+    else:
+        # gloo has no all-to-all: pairwise exchange
+        ops = []
+        for r in range(ws):
+            if r == me:
+                outs[r].copy_(pieces[r])
+                continue
+            peer = dist.get_global_rank(group, r)
+            ops.append(dist.P2POp(dist.isend, pieces[r], peer, group))
+            ops.append(dist.P2POp(dist.irecv, outs[r], peer, group))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
     return torch.cat(outs, dim=merge_dim)
 
 

@@ -79,3 +79,17 @@ def test_activation_offloading_with_checkpointing():
 
 def test_pp2_activation_offloading():
     _run(2, 2, 1, 2, extra={"ckpt_layers": True, "cfg": {"offload_activations": True}})
+
+
+def test_tp2_optimize_memory():
+    _run(2, 1, 2, 2, extra={"cfg": {"optimize": "memory"}})
+
+
+def test_tp2_optimize_memory_uneven():
+    _run(2, 1, 2, 1, extra={"cfg": {"optimize": "memory"},
+                            "model": {"num_attention_heads": 3, "attention_head_size": 16, "hidden_size": 48,
+                                      "intermediate_size": 96}})
+
+
+def test_pp2_tp2_optimize_memory():
+    _run(4, 2, 2, 2, extra={"cfg": {"optimize": "memory"}})
