@@ -272,6 +272,9 @@ def gather(obj, group, rank=0):
     return state.comm.gather(obj, group, rank, is_user_api=True)
 
 
+from .collectives import allgatherv_tensor, scatter_and_merge_tensor  # noqa: E402,F401
+
+
 def barrier(group=CommGroup.WORLD):
     state.comm.barrier(group, is_user_api=True)
 

@@ -93,3 +93,8 @@ def test_tp2_optimize_memory_uneven():
 
 def test_pp2_tp2_optimize_memory():
     _run(4, 2, 2, 2, extra={"cfg": {"optimize": "memory"}})
+
+
+def test_dist_modules_and_tensor_collectives_tp2():
+    outs = run_workers("dist_modules", 2, [], timeout=200)
+    assert all("OK" in o for o in outs)
