@@ -71,23 +71,40 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   return row * D + ((chunk ^ g) << 3);
 }
 
-// Row fetch (A/B operand with k along the row): 8 elements = chunk `chunk` of row `row`.
-template <typename T, int D>
-__device__ __forceinline__ typename MF<T>::e8 ld_row(const uint16_t* tile, int row, int chunk) {
-  return ld8<T>(tile + swz<D>(row, chunk));
-}
+// Per-lane LDS element offsets, swizzle resolved ONCE per kernel (the swizzle depends on
+// row bits 0-3 only, so rows +16/+32/+64 are immediate offsets of these bases).
+//  * RowOff: A/B operand row reads -- row (lane & 31) [+32 j], chunk 2t + (lane >> 5);
+//  * TrOff: transposed reads -- lane 4q+p of each 16-lane group supplies row q (and q + 8)
+//    at columns c0 + 4p..4p+3, c0 = 32 i + 16 * bit4(lane), rows based at 4 * (lane >> 5).
+template <int D>
+struct RowOff {
+  int o[D / 16];
+  __device__ __forceinline__ RowOff(int r, int hh) {
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) o[t] = swz<D>(r, 2 * t + hh);
+  }
+};
 
-// Transposed fetch of an A/B operand element set from a row-major LDS tile:
-// elements j=0..3 <- rows k0..k0+3, j=4..7 <- rows k0+8..k0+11, at column
-// c0 + (lane & 15) (the 16-lane group addressing: lane 4q+p supplies row q, cols 4p..4p+3).
-template <typename T, int D>
-__device__ __forceinline__ typename MF<T>::e8 ld_tr(const uint16_t* tile, int k0, int c0, int lane) {
-  const int q = (lane & 15) >> 2, pp = lane & 3;
-  const int col = c0 + 4 * pp;
-  const uint16_t* a0 = tile + swz<D>(k0 + q, col >> 3) + (col & 7);
-  const uint16_t* a1 = tile + swz<D>(k0 + 8 + q, col >> 3) + (col & 7);
-  s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
-  s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+template <int D>
+struct TrOff {
+  int lo[D / 32], hi[D / 32];
+  __device__ __forceinline__ explicit TrOff(int lane) {
+    const int q = (lane & 15) >> 2, pp = lane & 3, hh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+      const int col = 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
+      lo[i] = swz<D>(4 * hh + q, col >> 3) + (col & 7);
+      hi[i] = swz<D>(4 * hh + 8 + q, col >> 3) + (col & 7);
+    }
+  }
+};
+
+// Transposed fetch: elements j=0..3 <- rows k0..k0+3, j=4..7 <- rows k0+8..k0+11 (k0 folded
+// into the offsets), one ds_read_b64_tr_b16 per half.
+template <typename T>
+__device__ __forceinline__ typename MF<T>::e8 ld_tr(const uint16_t* tile, int off_lo, int off_hi) {
+  s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_lo));
+  s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_hi));
   s16x8 v = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
   return __builtin_bit_cast(typename MF<T>::e8, v);
 }
@@ -105,6 +122,22 @@ __device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 *
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// fmaxf on MFMA results makes clang insert a canonicalising v_max per operand; scores are
+// never signalling NaNs, so issue v_max3 directly (2 elements per instruction).
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float d;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// value of lane ^ 32 (the other half-wave) without an LDS round trip
+__device__ __forceinline__ float xor32(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const int lane = threadIdx.x & 63;
+  return __builtin_bit_cast(float, lane < 32 ? r[1] : r[0]);
+}
+
 // Register-staged tile copy (issue global loads early, write LDS late: the HBM/L2 latency
 // hides under the MFMA work of the current tile).
 template <int D, int ROWS>
@@ -113,20 +146,30 @@ struct Stage {
   static constexpr int N = ROWS * CH / kThreads;
   static_assert(N * kThreads == ROWS * CH, "tile must split evenly over the block");
   uint4 v[N];
-  __device__ __forceinline__ void load(const uint16_t* g, int64_t gs, int row0, int valid) {
+  int goff[N], loff[N], row[N];
+  __device__ __forceinline__ explicit Stage(int64_t gs) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       const int c = threadIdx.x + i * kThreads, r = c / CH, k = c % CH;
-      v[i] = r < valid ? *reinterpret_cast<const uint4*>(g + static_cast<int64_t>(row0 + r) * gs + k * 8)
-                       : make_uint4(0, 0, 0, 0);
+      row[i] = r;
+      goff[i] = static_cast<int>(r * gs) + k * 8;
+      loff[i] = swz<D>(r, k);
     }
+  }
+  // tile: pointer to the tile's first row; rows >= valid read as zeros
+  __device__ __forceinline__ void load(const uint16_t* tile, int valid) {
+    if (valid >= ROWS) {  // wave-uniform: interior tiles load without per-lane predication
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = *reinterpret_cast<const uint4*>(tile + goff[i]);
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      v[i] = row[i] < valid ? *reinterpret_cast<const uint4*>(tile + goff[i]) : make_uint4(0, 0, 0, 0);
   }
   __device__ __forceinline__ void store(uint16_t* lds) const {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int c = threadIdx.x + i * kThreads, r = c / CH, k = c % CH;
-      *reinterpret_cast<uint4*>(lds + swz<D>(r, k)) = v[i];
-    }
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + loff[i]) = v[i];
   }
 };
 
@@ -194,10 +237,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
     const int lo = qb * BM + diag - win + 1;
     kv_begin = lo > 0 ? (lo / BN) * BN : 0;
   }
-  Stage<D, BN> stK, stV;
+  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D> tro(lane);
   if (kv_begin < kv_end) {
-    stK.load(K, p.k_ss, kv_begin, sk - kv_begin);
-    stV.load(V, p.v_ss, kv_begin, sk - kv_begin);
+    stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
+    stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
   }
   const int wave_last_q = q0 + 31;
   for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
@@ -206,8 +251,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
     stV.store(sV);
     __syncthreads();
     if (kv0 + BN < kv_end) {
-      stK.load(K, p.k_ss, kv0 + BN, sk - kv0 - BN);
-      stV.load(V, p.v_ss, kv0 + BN, sk - kv0 - BN);
+      stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
+      stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
     }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
     if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
@@ -216,8 +261,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
     f32x16 s0 = f32x16{0}, s1 = f32x16{0};
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
-      s0 = MF<T>::mma(ld_row<T, D>(sK, r, 2 * t + hh), qf[t], s0);
-      s1 = MF<T>::mma(ld_row<T, D>(sK, 32 + r, 2 * t + hh), qf[t], s1);
+      s0 = MF<T>::mma(ld8<T>(sK + ro.o[t]), qf[t], s0);
+      s1 = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * D), qf[t], s1);
     }
     if (!interior) {
 #pragma unroll
@@ -228,15 +273,15 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
         if (k1 >= sk || (CAUSAL && k1 > qrow + diag) || (win > 0 && k1 <= qrow + diag - win)) s1[reg] = -INFINITY;
       }
     }
-    // raw-score row max (scale > 0 keeps the order), two independent chains
-    float mx0 = fmaxf(s0[0], s1[0]), mx1 = fmaxf(s0[1], s1[1]);
+    // raw-score row max (scale > 0 keeps the order), two independent v_max3 chains
+    float mx0 = max3(s0[0], s1[0], s0[1]), mx1 = max3(s1[1], s0[2], s1[2]);
 #pragma unroll
-    for (int reg = 2; reg < 16; reg += 2) {
-      mx0 = fmaxf(mx0, fmaxf(s0[reg], s1[reg]));
-      mx1 = fmaxf(mx1, fmaxf(s0[reg + 1], s1[reg + 1]));
+    for (int reg = 3; reg < 15; reg += 2) {
+      mx0 = max3(mx0, s0[reg], s1[reg]);
+      mx1 = max3(mx1, s0[reg + 1], s1[reg + 1]);
     }
-    float mx = fmaxf(mx0, mx1) * sl2;
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float mx = max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2;
+    mx = fmaxf(mx, xor32(mx));
     const float m_new = fmaxf(m_i, mx);
     const float m_use = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
     const float alpha = fast_exp2(m_i - m_use);
@@ -251,7 +296,7 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
       rs1 += e1;
     }
     float rs = rs0 + rs1;
-    rs += __shfl_xor(rs, 32, 64);
+    rs += xor32(rs);
     l_i = l_i * alpha + rs;
     if (__any(m_new != m_i)) {  // rescale only when a row max moved
 #pragma unroll
@@ -261,9 +306,8 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
-      const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) o[i] = MF<T>::mma(ld_tr<T, D>(sV, 16 * s + 4 * hh, c0, lane), pf[s], o[i]);
+      for (int s = 0; s < 4; ++s) o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * D, tro.hi[i] + 16 * s * D), pf[s], o[i]);
     }
   }
   if (qrow >= sq) return;
@@ -352,11 +396,13 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     const int hi = (kb + 1) * BKEYS - 1 - diag + win;  // last query that sees the block's last key
     q_end = hi + 1 < sq ? hi + 1 : sq;
   }
-  Stage<D, BQ> stQ, stO;
+  Stage<D, BQ> stQ(p.q_ss), stO(P.do_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D> tro(lane);
   float l_stage = 0.f, d_stage = 0.f;
   if (q_start < q_end) {
-    stQ.load(Q, p.q_ss, q_start, sq - q_start);
-    stO.load(dO, P.do_ss, q_start, sq - q_start);
+    stQ.load(Q + static_cast<int64_t>(q_start) * p.q_ss, sq - q_start);
+    stO.load(dO + static_cast<int64_t>(q_start) * P.do_ss, sq - q_start);
     if (threadIdx.x < BQ) {
       const int qq = q_start + threadIdx.x;
       l_stage = qq < sq ? LSE[qq] : 0.f;
@@ -375,8 +421,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     }
     __syncthreads();
     if (qt + BQ < q_end) {
-      stQ.load(Q, p.q_ss, qt + BQ, sq - qt - BQ);
-      stO.load(dO, P.do_ss, qt + BQ, sq - qt - BQ);
+      stQ.load(Q + static_cast<int64_t>(qt + BQ) * p.q_ss, sq - qt - BQ);
+      stO.load(dO + static_cast<int64_t>(qt + BQ) * P.do_ss, sq - qt - BQ);
       if (threadIdx.x < BQ) {
         const int qq = qt + BQ + threadIdx.x;
         l_stage = qq < sq ? LSE[qq] : 0.f;
@@ -401,8 +447,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       }
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) {
-        s = MF<T>::mma(ld_row<T, D>(sQ, 32 * sub + r, 2 * t + hh), kf[t], s);
-        dp = MF<T>::mma(ld_row<T, D>(sdO, 32 * sub + r, 2 * t + hh), vf[t], dp);
+        s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * D), kf[t], s);
+        dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * D), vf[t], dp);
       }
       if (interior) {
 #pragma unroll
@@ -427,12 +473,11 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
 #pragma unroll
       for (int i = 0; i < D / 32; ++i) {
-        const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
-        const int kq = 32 * sub + 4 * hh;
-        dv[i] = MF<T>::mma(ld_tr<T, D>(sdO, kq, c0, lane), pf0, dv[i]);
-        dv[i] = MF<T>::mma(ld_tr<T, D>(sdO, kq + 16, c0, lane), pf1, dv[i]);
-        dk[i] = MF<T>::mma(ld_tr<T, D>(sQ, kq, c0, lane), sf0, dk[i]);
-        dk[i] = MF<T>::mma(ld_tr<T, D>(sQ, kq + 16, c0, lane), sf1, dk[i]);
+        const int a0 = 32 * sub * D, a1 = (32 * sub + 16) * D;
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
       }
     }
   }
@@ -497,10 +542,12 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     const int lo = qb * BM + diag - win + 1;
     kv_begin = lo > 0 ? (lo / BN) * BN : 0;
   }
-  Stage<D, BN> stK, stV;
+  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D> tro(lane);
   if (kv_begin < kv_end) {
-    stK.load(K, p.k_ss, kv_begin, sk - kv_begin);
-    stV.load(V, p.v_ss, kv_begin, sk - kv_begin);
+    stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
+    stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
   }
   const int wave_last_q = q0 + 31;
   for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
@@ -509,8 +556,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     stV.store(sV);
     __syncthreads();
     if (kv0 + BN < kv_end) {
-      stK.load(K, p.k_ss, kv0 + BN, sk - kv0 - BN);
-      stV.load(V, p.v_ss, kv0 + BN, sk - kv0 - BN);
+      stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
+      stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
     }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
     if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
@@ -526,8 +573,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) {
-        s[u] = MF<T>::mma(ld_row<T, D>(sK, 32 * u + r, 2 * t + hh), qf[t], s[u]);
-        dp[u] = MF<T>::mma(ld_row<T, D>(sV, 32 * u + r, 2 * t + hh), df[t], dp[u]);
+        s[u] = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * u * D), qf[t], s[u]);
+        dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[t] + 32 * u * D), df[t], dp[u]);
       }
       if (interior) {
 #pragma unroll
@@ -546,9 +593,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     typename MF<T>::e8 sf[4] = {pack8<T>(dp[0], 0), pack8<T>(dp[0], 1), pack8<T>(dp[1], 0), pack8<T>(dp[1], 1)};
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
-      const int c0 = 32 * i + 16 * ((lane >> 4) & 1);
 #pragma unroll
-      for (int st = 0; st < 4; ++st) dq[i] = MF<T>::mma(ld_tr<T, D>(sK, 16 * st + 4 * hh, c0, lane), sf[st], dq[i]);
+      for (int st = 0; st < 4; ++st)
+        dq[i] = MF<T>::mma(ld_tr<T>(sK, tro.lo[i] + 16 * st * D, tro.hi[i] + 16 * st * D), sf[st], dq[i]);
     }
   }
   if (qrow >= sq) return;
