@@ -25,7 +25,16 @@ How it is built here (our design, not the reference's):
   receive counting (`module_manager.py:360-720`, `server.py:162-252`).
 * Microbatch state is freed when pp_rank 0 broadcasts the microbatch-end message, which
   also carries the step outputs to every stage (`MicrobatchEndResult` semantics).
+* **Deterministic task order under tensor parallelism.**  The TP peers of a stage run
+  separate engines fed by separate pipelines, but their modules issue TP collectives that
+  must match one-to-one.  tp_rank 0 decides: before executing any event (a message, a
+  locally queued result, a scheduling action) it sends the event's TP-invariant key to
+  its TP peers, which execute exactly that sequence (reference `DeterministicServerQueue`,
+  `server_queue.py:224-626`, forced when TP > 1).  Message ids are (pp_rank, counter),
+  so the same logical message has the same key on every TP peer.
 """
+import os
+from collections import deque
 import itertools
 
 import torch
@@ -112,7 +121,8 @@ class PipelineEngine:
         self._local_q = []
 
     def _new_id(self):
-        return (self.core.rank(), next(self._ids))
+        # (pp_rank, n): identical on every TP / DP peer executing the same task sequence
+        return (self.core.pp_rank(), next(self._ids))
 
     def _mb(self, mb):
         s = self.mbstate.get(mb)
@@ -176,18 +186,26 @@ class PipelineEngine:
         return outs
 
     def _serve(self, leader):
+        core = self.core
+        self._det = core.tp_size() > 1 and os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") != "1"
+        if self._det:
+            me = core.rank()
+            self._tp_peers = [r for r in core.get_tp_group() if r != me]
+            if core.tp_rank() != 0:
+                return self._serve_follower(leader)
         timeout = 0.05
         while not self._stop:
             progressed = False
             while self._local_q:
                 result_id, payload = self._local_q.pop(0)
+                self._announce(("lres", result_id))
                 self._resume(self.waiting.pop(("res", result_id)), payload)
                 progressed = True
             while True:
                 m = self.state.transport.poll(0.0)
                 if m is None:
                     break
-                self._dispatch(*m)
+                self._dispatch_decided(m)
                 progressed = True
                 if self._stop:
                     return
@@ -197,17 +215,89 @@ class PipelineEngine:
                     return
                 act = self.pipeline.next_action()
                 if act is not None:
-                    kind, mb = act
-                    if kind == "fwd":
-                        self._start_microbatch(mb)
-                    else:
-                        self.pipeline.set_status(mb, MbStatus.BWD)
-                        self._resume(self.waiting.pop(("bwd_start", mb)), None)
+                    self._announce(("act",) + tuple(act))
+                    self._do_action(act)
                     progressed = True
             if not progressed:
                 m = self.state.transport.poll(timeout)
                 if m is not None:
-                    self._dispatch(*m)
+                    self._dispatch_decided(m)
+
+    def _do_action(self, act):
+        kind, mb = act
+        if kind == "fwd":
+            self._start_microbatch(mb)
+        else:
+            self.pipeline.set_status(mb, MbStatus.BWD)
+            self._resume(self.waiting.pop(("bwd_start", mb)), None)
+
+    def _event_key(self, src, stubbed):
+        kind = stubbed[0]
+        if kind in ("fwd", "res"):
+            return (kind, stubbed[1])
+        if kind == "bwd":
+            return (kind, self.core.ranker.get_pp_rank(src), stubbed[4])
+        if kind == "ack":
+            return (kind, self.core.ranker.get_pp_rank(src), stubbed[1])
+        if kind == "mbdone":
+            return (kind, stubbed[1])
+        return (kind,)
+
+    def _announce(self, key):
+        if self._det:
+            # tagged with the step: a decider may start step t+1 while a TP peer (in
+            # another pipeline) is still finishing step t
+            msg = ("dec", self.state.step_count, key)
+            for r in self._tp_peers:
+                self.state.transport.send(r, msg, [])
+
+    def _dispatch_decided(self, m):
+        src, stubbed, tensors = m
+        if stubbed[0] not in ("abort", "dec"):
+            self._announce(self._event_key(src, stubbed))
+        self._dispatch(src, stubbed, tensors)
+
+    def _serve_follower(self, leader):
+        """TP peer of a deciding rank: execute events strictly in the decided order."""
+        pending = {}
+        step = self.state.step_count
+        stash = getattr(self, "_dec_stash", deque())
+        decisions = deque(k for st, k in stash if st == step)
+        self._dec_stash = deque((st, k) for st, k in stash if st != step)
+        timeout = 0.05
+        while not self._stop:
+            m = self.state.transport.poll(0.0 if decisions else timeout)
+            while m is not None:
+                src, stubbed, tensors = m
+                if stubbed[0] == "dec":
+                    if stubbed[1] == step:
+                        decisions.append(stubbed[2])
+                    else:
+                        self._dec_stash.append((stubbed[1], stubbed[2]))
+                elif stubbed[0] == "abort":
+                    self._dispatch(src, stubbed, tensors)
+                else:
+                    pending[self._event_key(src, stubbed)] = m
+                m = self.state.transport.poll(0.0)
+            while decisions and not self._stop:
+                key = decisions[0]
+                if key[0] == "act":
+                    decisions.popleft()
+                    self._do_action(key[1:])
+                elif key[0] == "lres":
+                    idx = next((i for i, (rid, _) in enumerate(self._local_q) if rid == key[1]), None)
+                    if idx is None:
+                        raise SMPRuntimeError(f"decided local result {key[1]} not produced on rank {self.core.rank()}")
+                    decisions.popleft()
+                    result_id, payload = self._local_q.pop(idx)
+                    self._resume(self.waiting.pop(("res", result_id)), payload)
+                elif key in pending:
+                    decisions.popleft()
+                    self._dispatch(*pending.pop(key))
+                else:
+                    break  # the decided message has not arrived yet
+            if leader and self.pipeline.is_done() and not decisions:
+                self._stop = True
 
     # ----------------------------------------------------------- coroutines
     def _spawn(self, fn, mb, kind, *args):

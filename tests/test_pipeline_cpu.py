@@ -98,3 +98,8 @@ def test_pp2_tp2_optimize_memory():
 def test_dist_modules_and_tensor_collectives_tp2():
     outs = run_workers("dist_modules", 2, [], timeout=200)
     assert all("OK" in o for o in outs)
+
+
+@pytest.mark.parametrize("pipe", ["interleaved", "simple"])
+def test_pp2_tp2_deterministic_order_under_jitter(pipe):
+    _run(4, 2, 2, 4, pipe=pipe, steps=3, extra={"jitter": True})

@@ -51,6 +51,20 @@ def main():
         for i, layer in enumerate(layers):
             smp.set_partition(layer, (i * pp) // len(layers))
     model = smp.DistributedModel(net)
+    if extra.get("jitter"):
+        # perturb message timing differently on every rank: TP peers must still agree on order
+        import random
+        import time
+
+        rnd = random.Random(smp.rank() * 7919 + 1)
+        tr = smp.state.transport
+        orig_send = tr.send
+
+        def jittery_send(*a, **k):
+            time.sleep(rnd.random() * 0.003)
+            return orig_send(*a, **k)
+
+        tr.send = jittery_send
     if extra.get("ckpt_layers"):
         for layer in model.get_module().transformer.seq_layers:
             smp.set_activation_checkpointing(layer)
