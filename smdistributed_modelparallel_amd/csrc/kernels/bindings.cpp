@@ -253,6 +253,22 @@ std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Ten
   return {dx, db};
 }
 
+// ------------------------------------------------------------------------ rope
+at::Tensor rope_apply(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, int64_t rotary_dim, bool neox, bool inverse,
+                      int64_t pos_offset) {
+  TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");  // strided (b, s, h) views are fine
+  TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "x must be [b, s, h, d] with contiguous d");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat, "cos/sin tables must be fp32");
+  TORCH_CHECK(cos_t.is_contiguous() && sin_t.is_contiguous(), "cos/sin tables must be contiguous");
+  TORCH_CHECK(cos_t.size(0) >= x.size(1) + pos_offset && cos_t.size(1) == rotary_dim / 2, "cos/sin table shape");
+  auto y = at::empty({x.size(0), x.size(1), x.size(2), x.size(3)}, x.options());
+  check(smpk::rope_apply(dt_code(x), x.data_ptr(), y.data_ptr(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(),
+                         x.size(0), x.size(1), x.size(2), x.size(3), rotary_dim, x.stride(0), x.stride(1), x.stride(2),
+                         neox ? 1 : 0, inverse ? 1 : 0, pos_offset, stream()),
+        "rope_apply");
+  return y;
+}
+
 // --------------------------------------------------------------------- softmax
 at::Tensor scaled_masked_softmax_fwd(at::Tensor x, c10::optional<at::Tensor> mask, double scale) {
   check_gpu(x, "x");
@@ -423,6 +439,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("col_sum", &col_sum);
+  m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias);
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);
   m.def("scaled_upper_triang_softmax_fwd", &scaled_upper_triang_softmax_fwd);

@@ -34,8 +34,42 @@ def _rotate_half(x):
     return torch.cat((-x[..., h:], x[..., :h]), dim=-1)
 
 
+class _RopeHIP(torch.autograd.Function):
+    """HIP kernel (csrc/kernels/rope.hip): reads q/k straight from their strided views into
+    the packed QKV projection; backward is the inverse rotation of the gradient."""
+
+    @staticmethod
+    def forward(ctx, x, cos, sin, rotary_dim, neox, offset):
+        from ._ext import ext
+
+        ctx.save_for_backward(cos, sin)
+        ctx.args = (rotary_dim, neox, offset)
+        return ext().rope_apply(x, cos, sin, rotary_dim, neox, False, offset)
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._ext import ext
+
+        cos, sin = ctx.saved_tensors
+        rd, neox, offset = ctx.args
+        g = g if g.stride(-1) == 1 else g.contiguous()
+        return ext().rope_apply(g, cos, sin, rd, neox, True, offset), None, None, None, None, None
+
+
 def apply_rotary(x, rotary_dim, base=10000, neox_style=False, offset=0):
     """Returns a new tensor with rotary applied (autograd-friendly)."""
+    if rotary_dim is None or rotary_dim == 0:
+        return x
+    if x.is_cuda and x.dtype in (torch.float16, torch.bfloat16, torch.float32) and x.stride(-1) == 1 \
+            and rotary_dim % 2 == 0:
+        s = x.shape[1]
+        cos, sin = rope_tables(s + offset, rotary_dim, base, x.device, 0)
+        return _RopeHIP.apply(x, cos.contiguous(), sin.contiguous(), rotary_dim, neox_style, offset)
+    return apply_rotary_torch(x, rotary_dim, base, neox_style, offset)
+
+
+def apply_rotary_torch(x, rotary_dim, base=10000, neox_style=False, offset=0):
+    """Plain torch implementation (CPU path and the numerics reference)."""
     if rotary_dim is None or rotary_dim == 0:
         return x
     b, s, h, d = x.shape

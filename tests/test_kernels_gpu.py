@@ -218,3 +218,26 @@ def test_offloaded_checkpoint_gpu():
     g_ref = [p.grad for m in layers for p in m.parameters()] + [x.grad]
     for a, b in zip(g_off, g_ref):
         assert torch.allclose(a, b, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("neox", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_rope_kernel(neox, dt):
+    from smdistributed_modelparallel_amd.ops.rope import apply_rotary, apply_rotary_torch
+
+    torch.manual_seed(4)
+    qkv = torch.randn(2, 37, 3, 5, 64, device="cuda", dtype=dt)
+    q = qkv[:, :, 0]  # strided view into the packed QKV projection
+    x = q.detach().clone().requires_grad_()
+    y = apply_rotary(q, 32, 10000, neox)
+    yr = apply_rotary_torch(q.float(), 32, 10000, neox)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
+    y2 = apply_rotary(x, 32, 10000, neox, offset=3)
+    xr = x.detach().float().requires_grad_()
+    yr2 = apply_rotary_torch(xr, 32, 10000, neox, offset=3)
+    assert torch.allclose(y2.float(), yr2, atol=tol, rtol=tol)
+    g = torch.randn_like(yr2)
+    y2.backward(g.to(dt))
+    yr2.backward(g)
+    assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
