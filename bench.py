@@ -126,7 +126,7 @@ def main():
         model.backward(loss)
         return loss
 
-    dev = torch.device("cuda", smp.local_rank()) if torch.cuda.is_available() else torch.device("cpu")
+    dev = smp.state.device  # the device smp.init bound this rank to
     batch = args.mbs * args.microbatches
     g = torch.Generator(device=dev)
     g.manual_seed(42 + smp.rank())
@@ -173,7 +173,8 @@ def main():
     if smp.rank() == 0:
         par = f"pp{args.pp}xtp{args.tp}xdp{max(1, world // (args.pp * args.tp))}"
         rec = {
-            "metric": "samples/sec (whole node) GPT-2 XL seq2048",
+            "metric": ("samples/sec (whole node) GPT-2 XL seq2048" if (args.model, args.seq) == ("gpt2-xl", 2048)
+                       else f"samples/sec (whole node) {args.model} seq{args.seq}"),
             "value": round(samples_per_s, 3),
             "unit": "samples/s",
             "n_gpus": world,

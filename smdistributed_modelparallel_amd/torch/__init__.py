@@ -87,8 +87,10 @@ def init(config=None):
     os.environ.setdefault("LOCAL_WORLD_SIZE", os.environ.get("OMPI_COMM_WORLD_LOCAL_SIZE", str(world)))
     use_gpu = torch.cuda.is_available() and os.environ.get("SMP_FORCE_CPU", "0") != "1"
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        state.device = torch.device("cuda", local_rank)
+        # SMP_DEVICE_INDEX: pin every rank to one device (multi-rank rehearsals on a 1-GPU box)
+        dev_idx = int(os.environ.get("SMP_DEVICE_INDEX", local_rank))
+        torch.cuda.set_device(dev_idx)
+        state.device = torch.device("cuda", dev_idx)
     else:
         state.device = torch.device("cpu")
     if not dist.is_initialized():
@@ -100,11 +102,15 @@ def init(config=None):
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29760")
         backend = "cpu:gloo,cuda:nccl" if use_gpu else "gloo"
-        kw = {"device_id": state.device} if use_gpu else {}
+        if os.environ.get("SMP_DIST_BACKEND"):  # e.g. "gloo" for single-GPU multi-rank rehearsals
+            backend = os.environ["SMP_DIST_BACKEND"]
+        kw = {"device_id": state.device} if (use_gpu and "nccl" in backend) else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     store = dist.distributed_c10d._get_default_store()
     core = ModelParallelCore()
-    core.initialize(cfg, store, torch.cuda.device_count() if use_gpu else None)
+    # the local-size <= device-count check is skipped when every rank is pinned to one device
+    ndev = torch.cuda.device_count() if (use_gpu and "SMP_DEVICE_INDEX" not in os.environ) else None
+    core.initialize(cfg, store, ndev)
     state.cfg = cfg
     state.core = core
     state.comm = core.comm

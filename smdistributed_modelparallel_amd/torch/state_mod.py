@@ -98,6 +98,8 @@ class PTModelParallelState:
         core = self.core
         ranker = core.ranker
         backend = "nccl" if self.use_gpu else "gloo"
+        if os.environ.get("SMP_DIST_BACKEND") == "gloo":
+            backend = "gloo"
         self.pgs.world = dist.group.WORLD
         me = core.rank()
 
@@ -148,7 +150,7 @@ class PTModelParallelState:
                     for b in ranks:
                         if a == b:
                             continue
-                        g = dist.new_group([a, b], backend="nccl")
+                        g = dist.new_group([a, b], backend=backend)
                         if me in (a, b):
                             self.pgs.p2p[(a, b)] = g
 
