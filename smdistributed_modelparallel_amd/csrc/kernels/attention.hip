@@ -58,6 +58,26 @@ __device__ __forceinline__ typename MF<T>::e8 ld8(const uint16_t* p) {
   return __builtin_bit_cast(typename MF<T>::e8, *reinterpret_cast<const s16x8*>(p));
 }
 
+// ------------------------------------------------------- XCD-aware block mapping
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own 4 MB L2).  A 1-D grid
+// of tiles x (b*h) blocks is mapped so that all tiles of one (b, h) run on the SAME XCD,
+// consecutively: their shared K/V (fwd, dQ) or Q/dO (dK/dV) tiles stay L2-resident
+// instead of being fetched by all 8 XCDs.  Heads beyond the last multiple of 8 fall back
+// to the linear order.
+__device__ __forceinline__ void xcd_map(int ntiles, int64_t nbh, int& tile, int64_t& bh) {
+  const int64_t L = blockIdx.x;
+  const int64_t full = (nbh / 8) * 8 * ntiles;
+  if (L < full) {
+    const int64_t xcd = L % 8, j = L / 8;
+    bh = xcd + 8 * (j / ntiles);
+    tile = static_cast<int>(j % ntiles);
+  } else {
+    const int64_t r = L - full;
+    bh = (nbh / 8) * 8 + r / ntiles;
+    tile = static_cast<int>(r % ntiles);
+  }
+}
+
 // ------------------------------------------------------------------ LDS tiles
 // Tiles are stored unpadded, [rows][D] bf16, with the 16-byte chunks of each row XOR-
 // swizzled so that BOTH access patterns are bank-conflict free:
@@ -198,10 +218,12 @@ __global__ void __launch_bounds__(kThreads, 2) attn_fwd_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t sV[BN * D];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int64_t bh = blockIdx.y;
-  const int64_t b = bh / p.h, h = bh % p.h;
   const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
-  const int qb = CAUSAL ? (nqb - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
+  int tile;
+  int64_t bh;
+  xcd_map(nqb, p.b * p.h, tile, bh);
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;  // heaviest causal blocks first
   const int q0 = qb * BM + wave * 32;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
   const int diag = sk - sq;  // key index allowed up to query + diag
@@ -354,10 +376,12 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / p.h, h = bh % p.h;
+  int kb;
+  int64_t bh;
+  xcd_map(static_cast<int>((p.sk + BKEYS - 1) / BKEYS), p.b * p.h, kb, bh);
+  const int64_t b = bh / p.h, h = bh % p.h;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
   const int win = p.window;
-  const int kb = static_cast<int>(blockIdx.x);
   const int k0w = kb * BKEYS + wave * 32;  // wave's first key
   const int krow = k0w + r;                // this lane's key (as B-operand column)
 
@@ -499,9 +523,12 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
-  const int64_t bh = blockIdx.y, b = bh / p.h, h = bh % p.h;
   const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
-  const int qb = CAUSAL ? (nqb - 1 - static_cast<int>(blockIdx.x)) : static_cast<int>(blockIdx.x);
+  int tile;
+  int64_t bh;
+  xcd_map(nqb, p.b * p.h, tile, bh);
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;
   const int q0 = qb * BM + wave * 32;
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
   const int win = p.window;
@@ -605,7 +632,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
 
 template <typename T, int D>
 int launch_fwd(const AttnParams& p, hipStream_t s) {
-  dim3 grid(static_cast<unsigned>((p.sq + 127) / 128), static_cast<unsigned>(p.b * p.h));
+  const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
   if (p.causal)
     attn_fwd_kernel<T, D, true><<<grid, kThreads, 0, s>>>(p);
   else
@@ -617,8 +644,8 @@ template <typename T, int D>
 int launch_bwd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = p.f.b * p.f.h * p.f.sq;
   attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
-  dim3 gk(static_cast<unsigned>((p.f.sk + 127) / 128), static_cast<unsigned>(p.f.b * p.f.h));
-  dim3 gq(static_cast<unsigned>((p.f.sq + 127) / 128), static_cast<unsigned>(p.f.b * p.f.h));
+  const unsigned gk = static_cast<unsigned>(((p.f.sk + 127) / 128) * p.f.b * p.f.h);
+  const unsigned gq = static_cast<unsigned>(((p.f.sq + 127) / 128) * p.f.b * p.f.h);
   if (p.f.causal) {
     attn_bwd_dkdv_kernel<T, D, true><<<gk, kThreads, 0, s>>>(p);
     attn_bwd_dq_kernel<T, D, true><<<gq, kThreads, 0, s>>>(p);

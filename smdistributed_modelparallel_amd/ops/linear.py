@@ -15,6 +15,15 @@ import torch
 import torch.nn.functional as F
 
 
+def _col_sum(x2):
+    """Bias gradient: HIP two-stage column sum on GPU (HBM-rate), torch elsewhere."""
+    if x2.is_cuda and x2.dtype in (torch.float16, torch.bfloat16, torch.float32) and x2.is_contiguous():
+        from ._ext import ext
+
+        return ext().col_sum(x2)
+    return x2.sum(0)
+
+
 def _fusable(w):
     g = w.grad
     return (getattr(w, "_smp_fused_grad", False) and g is not None and g.dtype == w.dtype and g.shape == w.shape
@@ -36,7 +45,7 @@ class _LinearWGradAccum(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(dy, w)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
+            db = _col_sum(dy2)
         if ctx.needs_input_grad[1]:
             if _fusable(w):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the
