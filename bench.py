@@ -30,7 +30,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-xl")
     ap.add_argument("--seq", type=int, default=2048)
-    ap.add_argument("--mbs", type=int, default=8, help="per-GPU micro-batch size")
+    ap.add_argument("--mbs", type=int, default=16,
+                    help="per-GPU micro-batch size (16 x 2048 tokens: GEMM M = 32768 keeps the MFMA pipes fed; "
+                         "well inside 288 GB HBM3E)")
     ap.add_argument("--microbatches", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
@@ -71,7 +73,8 @@ def setup_tunableop(args):
     else:
         os.makedirs(os.path.dirname(path), exist_ok=True)
         tun.tuning_enable(True)
-        tun.set_max_tuning_duration(40)
+        tun.set_max_tuning_duration(20)
+        tun.set_max_tuning_iterations(30)
         tun.set_filename(path, insert_device_ordinal=False)
     return mode
 
@@ -141,6 +144,8 @@ def main():
 
     for i in range(args.warmup):
         out = one(i)
+        if tmode == "tune" and smp.rank() == 0:
+            print(f"tuning warmup step {i} done", flush=True)
     if tmode == "tune":
         torch.cuda.synchronize()
         torch.cuda.tunable.tuning_enable(False)
@@ -200,6 +205,7 @@ def main():
             "tokens_per_s": round(tokens_per_s, 1),
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),
             "final_loss": round(loss_val, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None,
         }
         print(json.dumps(rec), flush=True)
     smp.barrier()
