@@ -669,6 +669,10 @@ class DistributedTransformerLMHead(DistributedModule):
 
         tx_in = (hidden, mask, cross_states, cross_mask) if self.add_cross_attention else (hidden, mask)
         hidden = self.transformer(tx_in)[0]
+        if prescaled and not self.distribute_embedding:
+            # shard the sequence BEFORE the (per-token) final LayerNorm: its gradient is then a
+            # per-shard partial like the embeddings', summed by the data-parallel reduction
+            (hidden,) = shard_sequence(hidden, shift=-1)
         if self.final_layernorm:
             hidden = self.layernorm(hidden)
 
@@ -685,14 +689,15 @@ class DistributedTransformerLMHead(DistributedModule):
                                  group=tp_group() if self._tp > 1 else None, reduction="none")
             return rows.mean(), shift_logits
 
-        if prescaled:
-            (hidden,) = shard_sequence(hidden, shift=-1)
         logits = self.lm_head(hidden) if self.add_lm_head else hidden
         if labels is None:
             return logits
         # shift labels (not logits): position t predicts token t+1; the last position is
         # ignored.  Same loss as slicing logits[..., :-1, :] without copying [B, s, V].
         shift_labels = F.pad(labels[..., 1:], (0, 1), value=-100)
+        if prescaled:
+            # this rank's sequence shard of the (shifted) labels, matching its logits
+            (shift_labels,) = shard_sequence(shift_labels, bwd_allgather=False)
         loss = cross_entropy(logits, shift_labels, ignore_index=-100)
         return loss, logits
 

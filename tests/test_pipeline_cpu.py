@@ -103,3 +103,11 @@ def test_dist_modules_and_tensor_collectives_tp2():
 @pytest.mark.parametrize("pipe", ["interleaved", "simple"])
 def test_pp2_tp2_deterministic_order_under_jitter(pipe):
     _run(4, 2, 2, 4, pipe=pipe, steps=3, extra={"jitter": True})
+
+
+def test_tp2_prescaled_batch():
+    _run(2, 1, 2, 1, extra={"cfg": {"prescaled_batch": True}})
+
+
+def test_pp2_tp2_prescaled_batch():
+    _run(4, 2, 2, 2, extra={"cfg": {"prescaled_batch": True}})

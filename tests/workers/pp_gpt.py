@@ -79,11 +79,14 @@ def main():
         return loss
 
     g = torch.Generator().manual_seed(7)
-    dp = smp.dp_size()
+    prescaled = bool(extra.get("cfg", {}).get("prescaled_batch"))
+    # prescaled_batch: every TP rank of a group sees the SAME batch (distinct per RDP rank)
+    dp = smp.rdp_size() if prescaled else smp.dp_size()
+    my_dp = smp.rdp_rank() if prescaled else smp.dp_rank()
     local_bs = 2 * mbs
     for it in range(steps):
         ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, 16), generator=g)
-        ids = ids_all[smp.dp_rank() * local_bs:(smp.dp_rank() + 1) * local_bs]
+        ids = ids_all[my_dp * local_bs:(my_dp + 1) * local_bs]
         opt.zero_grad()
         out = train(model, ids, ids)
         opt.step()
@@ -94,6 +97,16 @@ def main():
             chunk = ids_all[d * local_bs:(d + 1) * local_bs]
             for m in range(mbs):
                 x = chunk[m * 2:(m + 1) * 2]
+                if prescaled:
+                    # objective = mean over TP ranks of each rank's sequence-shard loss
+                    _, logits = ref((x, None, None, None, x))
+                    lab = torch.nn.functional.pad(x[:, 1:], (0, 1), value=-100)
+                    half = x.shape[1] // 2
+                    sl = [torch.nn.functional.cross_entropy(logits[:, a:b].reshape(-1, logits.shape[-1]),
+                                                            lab[:, a:b].reshape(-1), ignore_index=-100)
+                          for a, b in ((0, half), (half, x.shape[1]))]
+                    losses.append(torch.stack(sl).mean())
+                    continue
                 l, _ = ref((x, None, None, None, x))
                 losses.append(l)
         ref_loss = torch.stack(losses).mean()
@@ -102,6 +115,8 @@ def main():
         my_losses = torch.stack([o.detach().float() for o in out.outputs]).mean()
         mine = torch.tensor([my_losses.item()])
         all_l = smp.allgather(mine.item(), smp.DP_GROUP)
+        # prescaled: each TP rank reports its sequence shard's loss; averaging all DP-group
+        # entries equally gives the mean over shards and RDP replicas (the objective above)
         if smp.pp_rank() == 0 or True:
             avg = sum(all_l) / len(all_l)
             assert abs(avg - ref_loss.item()) < 1e-4, (it, avg, ref_loss.item())
@@ -109,7 +124,7 @@ def main():
     from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
 
     rp = dict(ref.named_parameters())
-    worst = 0.0
+    worst, worst_name = 0.0, None
     if smp.state.cfg.zero2d_enabled():
         # parameters are sharded: compare the gathered full state dict
         sd = model.state_dict(gather_to_rank0=False)
@@ -120,8 +135,10 @@ def main():
             continue
         full = rp[n].detach()
         t = slice_for_param(full, p, smp.tp_rank(), smp.tp_size())
-        worst = max(worst, (p.detach().float() - t.float()).abs().max().item())
-    assert worst < 2e-4, worst
+        d = (p.detach().float() - t.float()).abs().max().item()
+        if d > worst:
+            worst, worst_name = d, n
+    assert worst < 2e-4, (worst, worst_name if worst > 0 else None)
     if extra.get("cfg", {}).get("offload_activations") and smp.state.current_offloader is not None:
         st = smp.state.current_offloader.stats
         # every rank that runs checkpointed layers must have offloaded and reloaded them
