@@ -142,6 +142,18 @@ def main():
         opt.step()
         return out
 
+    if tmode == "tune" and smp.rank() == 0:
+        # GEMM tuning runs silently for minutes: keep a heartbeat on stdout
+        import threading
+
+        t_start = time.time()
+
+        def heartbeat():
+            while True:
+                time.sleep(60)
+                print(f"tunableop: tuning in progress, {time.time() - t_start:.0f} s", flush=True)
+
+        threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(args.warmup):
         out = one(i)
         if tmode == "tune" and smp.rank() == 0:
