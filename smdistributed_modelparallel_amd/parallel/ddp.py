@@ -89,7 +89,7 @@ class BucketReducer:
             b.work = None
             return
         if self.comm_hook is not None:
-            b.work = self.comm_hook(b, buf)
+            b.work = self.comm_hook(b, buf, self.group)
             return
         if self.shard:
             n = b.numel // self.group_size

@@ -73,6 +73,7 @@ class DistributedModel(nn.Module):
         self.broadcast_buffers = broadcast_buffers
         self.gradient_as_bucket_view = gradient_as_bucket_view
         self.require_backward_grad_sync = True
+        self._no_sync = False
         self._backward_passes = 0
         self._post_partition_hooks = OrderedDict()
         self._post_step_hooks = OrderedDict()
@@ -335,7 +336,8 @@ class DistributedModel(nn.Module):
 
     @contextlib.contextmanager
     def _step(self):
-        sync = (self._backward_passes + 1) % self.backward_passes_per_step == 0 and torch.is_grad_enabled()
+        sync = (self._backward_passes + 1) % self.backward_passes_per_step == 0 and torch.is_grad_enabled() and \
+            not self._no_sync
         self.require_backward_grad_sync = sync
         if self.partitioned:
             for r in self.reducers.values():
@@ -492,7 +494,7 @@ class DistributedModel(nn.Module):
         """DDP-style comm hook: hook(state, bucket) -> Future/Work; bucket.buffer() is the
         flat gradient slice."""
 
-        def adapter(b, buf):
+        def adapter(b, buf, group):
             class _B:
                 def buffer(self_inner):
                     return buf
@@ -500,7 +502,20 @@ class DistributedModel(nn.Module):
                 def index(self_inner):
                     return b.index
 
-            return hook(state_obj, _B())
+                def process_group(self_inner):
+                    return group
+
+            fut = hook(state_obj, _B())
+
+            class _W:
+                def wait(self_inner):
+                    out = fut.wait() if hasattr(fut, "wait") else fut
+                    if isinstance(out, (list, tuple)):
+                        out = out[0]
+                    if isinstance(out, torch.Tensor) and out.data_ptr() != buf.data_ptr():
+                        buf.copy_(out)
+
+            return _W()
 
         self._comm_hook = adapter
         for r in self.reducers.values():
@@ -511,9 +526,9 @@ class DistributedModel(nn.Module):
         if "FP16" in name.upper() or "BF16" in name.upper():
             dt = torch.bfloat16 if "BF16" in name.upper() else torch.float16
 
-            def compress(b, buf):
+            def compress(b, buf, group):
                 tmp = buf.to(dt)
-                w = dist.all_reduce(tmp, group=None, async_op=True)
+                w = dist.all_reduce(tmp, group=group, async_op=True)
 
                 class _W:
                     def wait(self_inner):
@@ -532,12 +547,13 @@ class DistributedModel(nn.Module):
 
     @contextlib.contextmanager
     def no_sync(self):
-        old = self.require_backward_grad_sync
-        self.require_backward_grad_sync = False
+        """Steps inside accumulate gradients locally; the next synced step reduces the sum."""
+        old = self._no_sync
+        self._no_sync = True
         try:
             yield
         finally:
-            self.require_backward_grad_sync = old
+            self._no_sync = old
 
     def get_ddp_logging_data(self):
         return {

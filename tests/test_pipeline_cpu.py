@@ -111,3 +111,9 @@ def test_tp2_prescaled_batch():
 
 def test_pp2_tp2_prescaled_batch():
     _run(4, 2, 2, 2, extra={"cfg": {"prescaled_batch": True}})
+
+
+@pytest.mark.parametrize("mode", ["nosync", "hook", "bf16"])
+def test_ddp_features(mode):
+    outs = run_workers("ddp_features", 2, [mode], timeout=200)
+    assert all("OK" in o for o in outs)
