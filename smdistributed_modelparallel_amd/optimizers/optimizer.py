@@ -230,6 +230,10 @@ class DistributedOptimizer:
 
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if state.sdp is not None and self._clip_coef is None and state.cfg.sdp_gradient_clipping > 0:
+            # sharded data parallelism clips to sdp_gradient_clipping on every step (the
+            # DeepSpeed `gradient_clipping` the reference configures, zero_config.py)
+            self.clip_master_grads(state.cfg.sdp_gradient_clipping)
         inv_scale = 1.0 / self.loss_scale
         if self.fp16:
             self.overflow = self._check_overflow()

@@ -62,7 +62,7 @@ def test_pp2_microbatch_counts(mbs):
     _run(2, 2, 1, mbs)
 
 
-_SDP = {"sdp_param_persistence_threshold": 100, "sdp_reduce_bucket_size": 20000}
+_SDP = {"sdp_param_persistence_threshold": 100, "sdp_reduce_bucket_size": 20000, "sdp_gradient_clipping": 0.0}
 
 
 def test_sharded_dp2():
@@ -117,3 +117,13 @@ def test_pp2_tp2_prescaled_batch():
 def test_ddp_features(mode):
     outs = run_workers("ddp_features", 2, [mode], timeout=200)
     assert all("OK" in o for o in outs)
+
+
+def test_sharded_dp2_gradient_clipping():
+    cfg = dict(_SDP, sharded_data_parallel_degree=2, sdp_gradient_clipping=0.05)
+    _run(2, 1, 1, 2, extra={"cfg": cfg, "ref_clip": 0.05})
+
+
+@pytest.mark.parametrize("world,pp,tp", [(2, 1, 1), (2, 1, 2), (2, 2, 1), (4, 2, 2)])
+def test_clip_master_grads_global_norm(world, pp, tp):
+    _run(world, pp, tp, 2, extra={"opt_clip": 0.05})

@@ -89,6 +89,8 @@ def main():
         ids = ids_all[my_dp * local_bs:(my_dp + 1) * local_bs]
         opt.zero_grad()
         out = train(model, ids, ids)
+        if extra.get("opt_clip"):
+            opt.clip_master_grads(extra["opt_clip"])
         opt.step()
         # reference on the global batch, averaged the same way (per microbatch mean, then mean)
         ropt.zero_grad()
@@ -111,6 +113,8 @@ def main():
                 losses.append(l)
         ref_loss = torch.stack(losses).mean()
         ref_loss.backward()
+        if extra.get("ref_clip") or extra.get("opt_clip"):
+            torch.nn.utils.clip_grad_norm_(ref.parameters(), extra.get("ref_clip") or extra["opt_clip"])
         ropt.step()
         my_losses = torch.stack([o.detach().float() for o in out.outputs]).mean()
         mine = torch.tensor([my_losses.item()])
