@@ -6,9 +6,12 @@ validation, ExitHook, shutdown on exit).  MPI is replaced by the launcher enviro
 is wired up through a key-value store rendezvous (the torch.distributed TCPStore).
 """
 import atexit
+import faulthandler
 import os
 import socket
 import sys
+import threading
+import time
 
 from .collectives import CollectiveCommunicator, CommGroup
 from .exceptions import InvalidEnvironmentError, NotInitializedError, WorkerSizeError
@@ -49,6 +52,80 @@ class ExitHook:
         self._orig_excepthook(exc_type, exc, *args)
 
 
+class Watchdog:
+    """Failure detector (new relative to the reference, which waits forever -- SURVEY §5.3).
+
+    A daemon thread blocks in the native ``Mailbox.wait_error`` (GIL released).  When a
+    peer aborts or its process vanishes, receives on the mailbox already raise in the
+    main thread; a rank stuck inside an RCCL/gloo collective cannot be interrupted, so
+    after ``SMP_ABORT_GRACE_S`` seconds (default 60) the watchdog dumps every thread's
+    stack and ends the process with exit code 1 instead of hanging the job.
+
+    Step timeout: with ``SMP_STEP_TIMEOUT_S`` set, a ``@smp.step`` call running longer
+    than that is treated as a hang: stacks are dumped, peers get ABORT, the process exits.
+    """
+
+    def __init__(self, core):
+        self.core = core
+        self.grace = float(os.environ.get("SMP_ABORT_GRACE_S", "60"))
+        t = os.environ.get("SMP_STEP_TIMEOUT_S")
+        self.step_timeout = float(t) if t else None
+        self._step_started = None
+        self._stop = False
+        self._thread = threading.Thread(target=self._run, name="smp-watchdog", daemon=True)
+
+    def start(self):
+        self._thread.start()
+
+    def stop(self):
+        self._stop = True
+
+    def join(self):
+        # Joined before interpreter finalisation: a daemon thread returning from native
+        # code (GIL released) into a finalising interpreter is torn down with a forced
+        # unwind, which aborts the process.
+        if self._thread.is_alive() and self._thread is not threading.current_thread():
+            self._thread.join(timeout=5.0)
+
+    def step_started(self):
+        self._step_started = time.monotonic()
+
+    def step_finished(self):
+        self._step_started = None
+
+    def _fatal(self, why):
+        logger.error(f"[smp watchdog] rank {self.core._rank}: {why}; dumping stacks and exiting")
+        try:
+            faulthandler.dump_traceback(all_threads=True)
+        except Exception:  # pragma: no cover
+            pass
+        try:
+            self.core.mailbox.shutdown(False)
+        except Exception:  # pragma: no cover
+            pass
+        os._exit(1)
+
+    def _run(self):
+        mb = self.core.mailbox
+        while not self._stop:
+            err = mb.wait_error(1.0)
+            if self._stop:
+                return
+            if err:
+                logger.error(f"[smp watchdog] rank {self.core._rank}: peer failure: {err}")
+                deadline = time.monotonic() + self.grace
+                while time.monotonic() < deadline:
+                    if self._stop:
+                        return
+                    time.sleep(0.1)
+                self._fatal(f"still running {self.grace:.0f}s after peer failure ({err})")
+                return
+            st = self._step_started
+            if self.step_timeout is not None and st is not None and time.monotonic() - st > self.step_timeout:
+                self._fatal(f"step exceeded SMP_STEP_TIMEOUT_S={self.step_timeout:g}s")
+                return
+
+
 def _env_int(*names, default=None):
     for n in names:
         v = os.environ.get(n)
@@ -78,6 +155,7 @@ class ModelParallelCore:
         self.comm = None
         self.timeline = None
         self.exit_hook = None
+        self.watchdog = None
         self._initialized = False
         self._rank = 0
         self._size = 1
@@ -156,6 +234,8 @@ class ModelParallelCore:
         self.exit_hook = ExitHook()
         self.exit_hook.hook()
         atexit.register(self.shutdown)
+        self.watchdog = Watchdog(self)
+        self.watchdog.start()
         self._initialized = True
 
     def shutdown(self):
@@ -169,10 +249,14 @@ class ModelParallelCore:
         try:
             if self.timeline is not None:
                 self.timeline.flush()
+            if self.watchdog is not None:
+                self.watchdog.stop()
             if self.mailbox is not None:
                 if success:
                     self.mailbox.flush()
-                self.mailbox.shutdown()
+                self.mailbox.shutdown(success)
+            if self.watchdog is not None:
+                self.watchdog.join()
         except Exception as e:  # pragma: no cover - best effort at exit
             logger.debug(f"shutdown: {e}")
 
@@ -262,10 +346,14 @@ class ModelParallelCore:
         self.comm.barrier(CommGroup.WORLD)
 
     def timeline_start_step(self, step):
+        if self.watchdog is not None:
+            self.watchdog.step_started()
         if self.timeline is not None:
             self.timeline.start_step(step)
 
     def timeline_end_step(self):
+        if self.watchdog is not None:
+            self.watchdog.step_finished()
         if self.timeline is not None:
             self.timeline.end_step()
 

@@ -73,7 +73,12 @@ PYBIND11_MODULE(_smprt, m) {
           },
           py::arg("timeout") = 0.0)
       .def("flush", &Mailbox::flush, py::call_guard<py::gil_scoped_release>())
-      .def("shutdown", &Mailbox::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("shutdown", &Mailbox::shutdown, py::arg("success") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def("error", &Mailbox::error)
+      .def("failed_rank", &Mailbox::failed_rank)
+      .def("wait_error", &Mailbox::wait_error, py::arg("timeout") = -1.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("stats", &Mailbox::stats)
       .def_property_readonly("rank", &Mailbox::rank)
       .def_property_readonly("world", &Mailbox::world);

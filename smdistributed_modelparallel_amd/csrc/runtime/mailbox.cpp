@@ -78,6 +78,7 @@ double now_s() {
 Mailbox::Mailbox(int rank, int world) : rank_(rank), world_(world) {
   peers_.resize(world);
   for (int i = 0; i < world; ++i) peers_[i] = std::make_unique<Peer>();
+  goodbye_.assign(world, 0);
 }
 
 Mailbox::~Mailbox() {
@@ -151,6 +152,8 @@ void Mailbox::connect(const std::vector<std::string>& hosts, const std::vector<i
   }
   ::close(listen_fd_);
   listen_fd_ = -1;
+  // The wake pipe exists before any thread that reads or writes it starts.
+  if (::pipe(wake_pipe_) != 0) throw std::runtime_error("mailbox: pipe() failed");
   for (int p = 0; p < world_; ++p) {
     if (p == rank_) continue;
     peers_[p]->sender = std::thread(&Mailbox::send_loop, this, p);
@@ -255,10 +258,8 @@ void Mailbox::recv_loop() {
     fds.push_back(pollfd{peers_[p]->fd, POLLIN, 0});
     owner.push_back(p);
   }
-  if (::pipe(wake_pipe_) == 0) {
-    fds.push_back(pollfd{wake_pipe_[0], POLLIN, 0});
-    owner.push_back(-1);
-  }
+  fds.push_back(pollfd{wake_pipe_[0], POLLIN, 0});
+  owner.push_back(-1);
   std::vector<bool> closed(fds.size(), false);
   while (!stop_.load()) {
     int n = ::poll(fds.data(), fds.size(), 200);
@@ -271,9 +272,26 @@ void Mailbox::recv_loop() {
         if (!read_all(fds[i].fd, reinterpret_cast<char*>(&h), sizeof(h))) {
           closed[i] = true;
           fds[i].fd = -1;
+          bool orderly;
+          {
+            std::lock_guard<std::mutex> g(in_mu_);
+            orderly = goodbye_[owner[i]] != 0;
+          }
+          if (!orderly && !stop_.load())
+            record_failure(owner[i], "rank " + std::to_string(owner[i]) +
+                                         " closed its connection without shutdown (process died?)");
           continue;
         }
         if (h.magic != kMagic) throw std::runtime_error("mailbox: corrupt frame");
+        if (h.channel == CONTROL) {
+          if (h.tid == ABORT) {
+            record_failure(h.src, "rank " + std::to_string(h.src) + " aborted (shutdown with failure)");
+          } else {
+            std::lock_guard<std::mutex> g(in_mu_);
+            goodbye_[h.src] = 1;
+          }
+          continue;
+        }
         Message m;
         m.src = h.src;
         m.tid = h.tid;
@@ -283,14 +301,43 @@ void Mailbox::recv_loop() {
         deliver(std::move(m));
       } catch (const std::exception& e) {
         if (stop_.load()) return;
-        std::lock_guard<std::mutex> g(in_mu_);
-        if (error_.empty()) error_ = e.what();
         closed[i] = true;
         fds[i].fd = -1;
-        in_cv_.notify_all();
+        record_failure(owner[i], e.what());
       }
     }
   }
+}
+
+void Mailbox::record_failure(int rank, const std::string& what) {
+  {
+    std::lock_guard<std::mutex> g(in_mu_);
+    if (error_.empty()) {
+      error_ = what;
+      failed_rank_ = rank;
+    }
+  }
+  in_cv_.notify_all();
+}
+
+std::string Mailbox::error() {
+  std::lock_guard<std::mutex> g(in_mu_);
+  return error_;
+}
+
+int Mailbox::failed_rank() {
+  std::lock_guard<std::mutex> g(in_mu_);
+  return failed_rank_;
+}
+
+std::string Mailbox::wait_error(double timeout_s) {
+  std::unique_lock<std::mutex> lk(in_mu_);
+  auto ready = [&] { return !error_.empty() || stop_.load(); };
+  if (timeout_s < 0)
+    in_cv_.wait(lk, ready);
+  else
+    in_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), ready);
+  return error_;
 }
 
 void Mailbox::deliver(Message&& m) {
@@ -370,7 +417,22 @@ void Mailbox::flush() {
   }
 }
 
-void Mailbox::shutdown() {
+void Mailbox::shutdown(bool success) {
+  if (stop_.load()) return;
+  // Tell every connected peer how this rank ends; senders drain their queues (this
+  // frame included) before they exit below.
+  if (listen_fd_ < 0) {
+    auto f = frame(success ? GOODBYE : ABORT, CONTROL, std::string());
+    for (int d = 0; d < world_; ++d) {
+      if (d == rank_ || peers_[d]->fd < 0) continue;
+      Peer& p = *peers_[d];
+      {
+        std::lock_guard<std::mutex> g(p.mu);
+        p.outq.push_back(f);
+      }
+      p.cv.notify_all();
+    }
+  }
   if (stop_.exchange(true)) return;
   for (auto& p : peers_) {
     {

@@ -9,6 +9,12 @@
 // "server=True" routing).  One receiver thread multiplexes all peer sockets with
 // poll(2); one sender thread per peer drains an outgoing queue so a Python send never
 // blocks the caller on a slow peer (async send semantics of smp_async_send).
+//
+// Coordinated shutdown (reference smp_shutdown(success), smp/backend/core.py:227-259):
+// shutdown() sends every peer a CONTROL frame -- GOODBYE on success, ABORT on failure --
+// before closing.  A peer that receives ABORT, or sees a connection close without a
+// GOODBYE (the process died), records the failure: every blocked or later receive then
+// throws instead of waiting forever, and wait_error() wakes the watchdog thread.
 #pragma once
 
 #include <atomic>
@@ -26,7 +32,8 @@
 
 namespace smprt {
 
-enum Channel : uint8_t { USER = 0, SERVER = 1 };
+enum Channel : uint8_t { USER = 0, SERVER = 1, CONTROL = 2 };
+enum ControlTid : int64_t { GOODBYE = 0, ABORT = 1 };
 
 struct Message {
   int32_t src = -1;
@@ -66,7 +73,15 @@ class Mailbox {
 
   // Wait until every queued outgoing message has been written to its socket.
   void flush();
-  void shutdown();
+  // success=false tells every peer that this rank failed (ABORT).
+  void shutdown(bool success = true);
+  // First recorded transport failure ("" if none).
+  std::string error();
+  // Rank that aborted or vanished (-1 if none / unknown).
+  int failed_rank();
+  // Block until a failure is recorded or the mailbox stops; returns error() ("" on
+  // timeout or orderly stop).  timeout_s < 0 waits forever.
+  std::string wait_error(double timeout_s);
   TransportStats stats();
   int rank() const { return rank_; }
   int world() const { return world_; }
@@ -84,6 +99,7 @@ class Mailbox {
   void recv_loop();
   void send_loop(int peer);
   void deliver(Message&& m);
+  void record_failure(int rank, const std::string& what);
   std::shared_ptr<const std::string> frame(int64_t tid, uint8_t channel, const std::string& p);
 
   int rank_, world_;
@@ -98,6 +114,8 @@ class Mailbox {
   std::map<std::pair<int, int64_t>, std::deque<std::string>> matched_;
   std::deque<Message> server_q_;
   std::string error_;
+  int failed_rank_ = -1;
+  std::vector<uint8_t> goodbye_;  // peer said GOODBYE (orderly close follows)
 
   std::mutex stats_mu_;
   TransportStats stats_;
