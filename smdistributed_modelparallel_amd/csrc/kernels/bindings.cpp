@@ -142,9 +142,12 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> re
   return {y, mean, rstd};
 }
 
+// dw_out/db_out given (both): dgamma/dbeta accumulated into them in place (flat-buffer
+// grad views) and returned; otherwise fresh tensors.
 std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> w, at::Tensor mean,
                                       at::Tensor rstd, bool need_wgrad, bool need_bgrad,
-                                      c10::optional<at::Tensor> dres) {
+                                      c10::optional<at::Tensor> dres, c10::optional<at::Tensor> dw_out,
+                                      c10::optional<at::Tensor> db_out) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
@@ -174,11 +177,20 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
         "layernorm_bwd");
   if (dwp.defined()) {
     auto wo = w.has_value() ? w->options() : x.options();
-    dw = at::empty({cols}, wo);
-    db = at::empty({cols}, wo);
+    const bool acc = dw_out.has_value() && db_out.has_value();
+    if (acc) {
+      for (const at::Tensor* t : {&*dw_out, &*db_out})
+        TORCH_CHECK(t->is_contiguous() && t->numel() == cols && dt_code(*t) == wdt,
+                    "layernorm_bwd: dw_out/db_out must be contiguous [cols] tensors of the weight dtype");
+      dw = *dw_out;
+      db = *db_out;
+    } else {
+      dw = at::empty({cols}, wo);
+      db = at::empty({cols}, wo);
+    }
     auto work = at::empty({smpk::kLnReduceSlices, 2, cols}, x.options().dtype(at::kFloat));
     check(smpk::layernorm_bwd_reduce(wdt, dwp.data_ptr<float>(), dbp.data_ptr<float>(), dw.data_ptr(), db.data_ptr(),
-                                     parts, cols, work.data_ptr<float>(), stream()),
+                                     parts, cols, work.data_ptr<float>(), stream(), acc),
           "layernorm_bwd_reduce");
   }
   return {dx, dw, db};
@@ -220,19 +232,27 @@ at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> 
   return dx;
 }
 
-at::Tensor col_sum(at::Tensor x) {
+// out=None: fresh [cols] tensor; out given: out += colsum(x) in place (bias .grad views).
+at::Tensor col_sum(at::Tensor x, c10::optional<at::Tensor> out_opt) {
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / cols;
   const int64_t parts = smpk::col_sum_parts(rows);
   auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
-  auto out = at::empty({cols}, x.options());
-  check(smpk::col_sum(dt_code(x), x.data_ptr(), out.data_ptr(), ws.data_ptr<float>(), rows, cols, stream()), "col_sum");
+  const bool acc = out_opt.has_value();
+  at::Tensor out = acc ? *out_opt : at::empty({cols}, x.options());
+  if (acc)
+    TORCH_CHECK(out.is_contiguous() && out.numel() == cols && out.scalar_type() == x.scalar_type(),
+                "col_sum: out must be a contiguous [cols] tensor of x's dtype");
+  check(smpk::col_sum(dt_code(x), x.data_ptr(), out.data_ptr(), ws.data_ptr<float>(), rows, cols, stream(), acc),
+        "col_sum");
   return out;
 }
 
 // (dx, dbias) of gelu(x + bias) in one pass; falls back to bwd + col_sum for odd shapes.
-std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Tensor bias) {
+// dbias_out given: dbias accumulated into it in place (and returned).
+std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Tensor bias,
+                                            c10::optional<at::Tensor> dbias_out) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   check_gpu(bias, "bias");
@@ -240,14 +260,18 @@ std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Ten
   const int64_t rows = x.numel() / cols;
   TORCH_CHECK(bias.numel() == cols && bias.scalar_type() == x.scalar_type(), "bias mismatch");
   auto dx = at::empty_like(x);
-  auto db = at::empty({cols}, x.options());
+  const bool acc = dbias_out.has_value();
+  at::Tensor db = acc ? *dbias_out : at::empty({cols}, x.options());
+  if (acc)
+    TORCH_CHECK(db.is_contiguous() && db.numel() == cols && db.scalar_type() == x.scalar_type(),
+                "bias_gelu_bwd_dbias: dbias_out must be a contiguous [cols] tensor of x's dtype");
   const int64_t parts = smpk::col_sum_parts(rows);
   auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
   const int rc = smpk::bias_gelu_bwd_dbias(dt_code(x), dy.data_ptr(), x.data_ptr(), bias.data_ptr(), dx.data_ptr(),
-                                           db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream());
+                                           db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream(), acc);
   if (rc == -2) {
     dx = bias_gelu_bwd(dy, x, bias);
-    return {dx, col_sum(dx.view({rows, cols}))};
+    return {dx, col_sum(dx.view({rows, cols}), dbias_out)};
   }
   check(rc, "bias_gelu_bwd_dbias");
   return {dx, db};
@@ -434,13 +458,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("axpby_", &axpby_);
   m.def("cast_copy_", &cast_copy_);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
+        py::arg("need_wgrad"), py::arg("need_bgrad"), py::arg("dres"), py::arg("dw_out") = py::none(),
+        py::arg("db_out") = py::none());
   m.def("layernorm_apply_stats", &layernorm_apply_stats);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
-  m.def("col_sum", &col_sum);
+  m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
   m.def("rope_apply", &rope_apply);
-  m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias);
+  m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),
+        py::arg("dbias_out") = py::none());
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);
   m.def("scaled_upper_triang_softmax_fwd", &scaled_upper_triang_softmax_fwd);
   m.def("scaled_softmax_bwd", &scaled_softmax_bwd);

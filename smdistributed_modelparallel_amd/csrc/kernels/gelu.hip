@@ -25,6 +25,24 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }
 
+// tanh(u) = 1 - 2 / (1 + e^{2u}) on the transcendental unit (v_exp_f32 + v_rcp_f32):
+// saturates correctly at +-inf, ~1e-6 relative error -- far below bf16/fp16 rounding.
+__device__ __forceinline__ float tanh_fast(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * u));
+}
+
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float u = kC0 * (x + kC1 * x * x * x);
+  return 0.5f * x * (1.f + tanh_fast(u));
+}
+
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float x2 = x * x;
+  const float t = tanh_fast(kC0 * x * (1.f + kC1 * x2));
+  const float du = kC0 * (1.f + 3.f * kC1 * x2);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
+}
+
 template <typename T, bool VEC>
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
                                                             T* __restrict__ y, int64_t rows, int64_t cols) {
@@ -85,7 +103,85 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
   }
 }
 
-// Column sums: grid (ceil(cols/64), parts); 64 columns x 4 row lanes per block.
+// ---------------------------------------------------------------- column walker
+// Layout shared by the column-reduction kernels: each lane owns one 16-byte column
+// vector (8 bf16) and walks rows; a 256-thread block is CVB column vectors x RL row
+// lanes (CVB divides the column-vector count when possible, so no lanes idle on e.g.
+// 1600 / 4800 / 6400 columns); grid = (column-vector groups, row parts).  The bias stays
+// in registers, no per-element index division, and U independent 16-byte loads per lane
+// are in flight before any arithmetic (HBM latency hiding at 4+ waves/SIMD).
+struct ColWalk {
+  int cvb, rl;
+  int64_t groups;
+};
+
+inline ColWalk col_walk(int64_t cv) {
+  ColWalk w{64, 4, (cv + 63) / 64};
+  if (cv < 64) {
+    w.cvb = static_cast<int>(cv);
+    w.rl = 256 / w.cvb;
+    w.groups = 1;
+    return w;
+  }
+  for (int d = 64; d >= 32; --d)
+    if (cv % d == 0) {
+      w.cvb = d;
+      w.rl = 256 / d;
+      w.groups = cv / d;
+      return w;
+    }
+  return w;
+}
+
+constexpr int kUnroll = 4;
+
+// Column partial sums of x [rows, cols] -> part[blockIdx.y][cols] (fp32).
+template <typename T>
+__global__ void __launch_bounds__(256) col_sum_vec(const T* __restrict__ x, float* __restrict__ part, int64_t rows,
+                                                   int64_t cols, int64_t rows_per_part, int cvb, int rl) {
+  constexpr int N = Vec16<T>::N;
+  __shared__ float s[256 * N];
+  const int cvl = threadIdx.x % cvb, r_l = threadIdx.x / cvb;
+  const int64_t c = (static_cast<int64_t>(blockIdx.x) * cvb + cvl) * N;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
+  const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
+  float acc[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) acc[j] = 0.f;
+  const bool active = r_l < rl && c < cols;
+  if (active) {
+    int64_t r = r0 + r_l;
+    for (; r + (kUnroll - 1) * rl < r1; r += kUnroll * rl) {
+      Vec16<T> v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = load16(x + (r + u * rl) * cols + c);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int j = 0; j < N; ++j) acc[j] += to_f32(v[u].v[j]);
+    }
+    for (; r < r1; r += rl) {
+      Vec16<T> v = load16(x + r * cols + c);
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc[j] += to_f32(v.v[j]);
+    }
+  }
+  // combine the row lanes through LDS: s[r_l][cvl*N + j]
+  const int width = cvb * N;
+  if (r_l < rl)
+#pragma unroll
+    for (int j = 0; j < N; ++j) s[r_l * width + cvl * N + j] = acc[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < width; k += 256) {
+    const int64_t col = static_cast<int64_t>(blockIdx.x) * width + k;
+    if (col >= cols) continue;
+    float a = 0.f;
+    for (int q = 0; q < rl; ++q) a += s[q * width + k];
+    part[static_cast<int64_t>(blockIdx.y) * cols + col] = a;
+  }
+}
+
+// Scalar fallback (odd column counts / unaligned): 64 columns x 4 row lanes per block.
 template <typename T>
 __global__ void __launch_bounds__(256) col_sum_partial(const T* __restrict__ x, float* __restrict__ part,
                                                        int64_t rows, int64_t cols, int64_t rows_per_part) {
@@ -102,40 +198,113 @@ __global__ void __launch_bounds__(256) col_sum_partial(const T* __restrict__ x, 
   if (rl == 0 && c < cols) part[static_cast<int64_t>(blockIdx.y) * cols + c] = s[0][cl] + s[1][cl] + s[2][cl] + s[3][cl];
 }
 
-// Fused backward + bias gradient: each thread owns one 16-byte column vector and walks
-// `rows_per_part` rows, so dbias partial sums stay in registers (dx is never re-read).
+// Fused backward + bias gradient over the column walker: dx = dy * gelu'(x + b) is
+// written once and its column sums (dbias partials) never re-read dx.
 template <typename T>
 __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                   const T* __restrict__ bias, T* __restrict__ dx,
                                                                   float* __restrict__ part, int64_t rows, int64_t cols,
-                                                                  int64_t rows_per_part) {
+                                                                  int64_t rows_per_part, int cvb, int rl) {
   constexpr int N = Vec16<T>::N;
-  const int64_t c = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * N;
-  if (c >= cols) return;
+  constexpr int U = 2;
+  __shared__ float s[256 * N];
+  const int cvl = threadIdx.x % cvb, r_l = threadIdx.x / cvb;
+  const int64_t c = (static_cast<int64_t>(blockIdx.x) * cvb + cvl) * N;
   const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
   const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
-  float bb[N], acc[N];
-  Vec16<T> bv = load16(bias + c);
+  float acc[N], bb[N];
 #pragma unroll
-  for (int j = 0; j < N; ++j) {
-    bb[j] = to_f32(bv.v[j]);
-    acc[j] = 0.f;
+  for (int j = 0; j < N; ++j) acc[j] = 0.f;
+  const bool active = r_l < rl && c < cols;
+  if (active) {
+    Vec16<T> bv = load16(bias + c);
+#pragma unroll
+    for (int j = 0; j < N; ++j) bb[j] = to_f32(bv.v[j]);
+    int64_t r = r0 + r_l;
+    for (; r + (U - 1) * rl < r1; r += U * rl) {
+      Vec16<T> a[U], d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a[u] = load16(x + (r + u * rl) * cols + c);
+        d[u] = load16(dy + (r + u * rl) * cols + c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        Vec16<T> o;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          o.v[j] = from_f32<T>(to_f32(d[u].v[j]) * gelu_grad_fast(to_f32(a[u].v[j]) + bb[j]));
+          acc[j] += to_f32(o.v[j]);
+        }
+        store16(dx + (r + u * rl) * cols + c, o);
+      }
+    }
+    for (; r < r1; r += rl) {
+      Vec16<T> a = load16(x + r * cols + c);
+      Vec16<T> d = load16(dy + r * cols + c);
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad_fast(to_f32(a.v[j]) + bb[j]));
+        acc[j] += to_f32(o.v[j]);
+      }
+      store16(dx + r * cols + c, o);
+    }
   }
-#pragma unroll 4
-  for (int64_t r = r0; r < r1; ++r) {
-    const int64_t i = r * cols + c;
-    Vec16<T> a = load16(x + i);
-    Vec16<T> d = load16(dy + i);
+  const int width = cvb * N;
+  if (r_l < rl)
+#pragma unroll
+    for (int j = 0; j < N; ++j) s[r_l * width + cvl * N + j] = acc[j];
+  __syncthreads();
+  for (int k = threadIdx.x; k < width; k += 256) {
+    const int64_t col = static_cast<int64_t>(blockIdx.x) * width + k;
+    if (col >= cols) continue;
+    float a = 0.f;
+    for (int q = 0; q < rl; ++q) a += s[q * width + k];
+    part[static_cast<int64_t>(blockIdx.y) * cols + col] = a;
+  }
+}
+
+// Forward over the column walker: bias in registers, U rows of 16-byte loads in flight.
+template <typename T>
+__global__ void __launch_bounds__(256) bias_gelu_fwd_walk(const T* __restrict__ x, const T* __restrict__ bias,
+                                                          T* __restrict__ y, int64_t rows, int64_t cols,
+                                                          int64_t rows_per_part, int cvb, int rl) {
+  constexpr int N = Vec16<T>::N;
+  const int cvl = threadIdx.x % cvb, r_l = threadIdx.x / cvb;
+  const int64_t c = (static_cast<int64_t>(blockIdx.x) * cvb + cvl) * N;
+  if (r_l >= rl || c >= cols) return;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
+  const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
+  float bb[N];
+  if (bias) {
+    Vec16<T> bv = load16(bias + c);
+#pragma unroll
+    for (int j = 0; j < N; ++j) bb[j] = to_f32(bv.v[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) bb[j] = 0.f;
+  }
+  int64_t r = r0 + r_l;
+  for (; r + (kUnroll - 1) * rl < r1; r += kUnroll * rl) {
+    Vec16<T> a[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = load16(x + (r + u * rl) * cols + c);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(gelu_fast(to_f32(a[u].v[j]) + bb[j]));
+      store16(y + (r + u * rl) * cols + c, o);
+    }
+  }
+  for (; r < r1; r += rl) {
+    Vec16<T> a = load16(x + r * cols + c);
     Vec16<T> o;
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad(to_f32(a.v[j]) + bb[j]));
-      acc[j] += to_f32(o.v[j]);
-    }
-    store16(dx + i, o);
+    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(gelu_fast(to_f32(a.v[j]) + bb[j]));
+    store16(y + r * cols + c, o);
   }
-#pragma unroll
-  for (int j = 0; j < N; ++j) part[static_cast<int64_t>(blockIdx.y) * cols + c + j] = acc[j];
 }
 
 // [parts, cols] fp32 -> [cols] in two deterministic stages (slices of parts, then slices).
@@ -156,10 +325,10 @@ __global__ void __launch_bounds__(256) parts_reduce_stage1(const float* __restri
 
 template <typename T>
 __global__ void __launch_bounds__(256) parts_reduce_stage2(const float* __restrict__ part, T* __restrict__ out,
-                                                           int slices, int64_t cols) {
+                                                           int slices, int64_t cols, bool accumulate) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (c >= cols) return;
-  float a = 0.f;
+  float a = accumulate ? to_f32(out[c]) : 0.f;
   for (int p = 0; p < slices; ++p) a += part[static_cast<int64_t>(p) * cols + c];
   out[c] = from_f32<T>(a);
 }
@@ -167,11 +336,13 @@ __global__ void __launch_bounds__(256) parts_reduce_stage2(const float* __restri
 constexpr int kReduceSlices = 32;
 
 template <typename T>
-void reduce_parts(const float* part, int parts, int64_t cols, float* work, T* out, hipStream_t s) {
+void reduce_parts(const float* part, int parts, int64_t cols, float* work, T* out, hipStream_t s,
+                  bool accumulate = false) {
   const int slices = parts < kReduceSlices ? parts : kReduceSlices;
   dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(slices));
   parts_reduce_stage1<<<g, 256, 0, s>>>(part, work, parts, cols, slices);
-  parts_reduce_stage2<T><<<static_cast<unsigned>((cols + 255) / 256), 256, 0, s>>>(work, out, slices, cols);
+  parts_reduce_stage2<T><<<static_cast<unsigned>((cols + 255) / 256), 256, 0, s>>>(work, out, slices, cols,
+                                                                                   accumulate);
 }
 
 inline int elt_grid(int64_t total, int per_thread) {
@@ -190,12 +361,21 @@ int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows
     constexpr int N = Vec16<T>::N;
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
                                           reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
-    if (vec)
-      bias_gelu_fwd_kernel<T, true><<<elt_grid(total, N), 256, 0, s>>>(
-          static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
-    else
+    if (vec) {
+      const ColWalk w = col_walk(cols / N);
+      // ~2048+ blocks, >= 4 x unroll rows per lane
+      int64_t parts = (2048 + w.groups - 1) / w.groups;
+      const int64_t max_parts = rows / (static_cast<int64_t>(w.rl) * kUnroll);
+      if (parts > max_parts) parts = max_parts;
+      if (parts < 1) parts = 1;
+      const int64_t rpp = (rows + parts - 1) / parts;
+      dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
+      bias_gelu_fwd_walk<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
+                                              static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
+    } else {
       bias_gelu_fwd_kernel<T, false><<<elt_grid(total, 1), 256, 0, s>>>(
           static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
+    }
   });
   return static_cast<int>(hipGetLastError());
 }
@@ -228,14 +408,24 @@ int col_sum_parts(int64_t rows) {
   return static_cast<int>(parts < 1 ? 1 : parts);
 }
 
-int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
+int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s,
+            bool accumulate) {
   if (rows <= 0 || cols <= 0) return 0;
   const int parts = col_sum_parts(rows);
   const int64_t rpp = (rows + parts - 1) / parts;
   SMPK_DISPATCH(dt, T, {
-    dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(parts));
-    col_sum_partial<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), workspace, rows, cols, rpp);
-    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(out), s);
+    constexpr int N = Vec16<T>::N;
+    const bool vec = (cols % N == 0) && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (vec) {
+      const ColWalk w = col_walk(cols / N);
+      dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
+      col_sum_vec<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), workspace, rows, cols, rpp, w.cvb, w.rl);
+    } else {
+      dim3 g(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(parts));
+      col_sum_partial<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), workspace, rows, cols, rpp);
+    }
+    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(out), s,
+                    accumulate);
   });
   return static_cast<int>(hipGetLastError());
 }
@@ -243,7 +433,7 @@ int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, in
 // dx = dy * gelu'(x + bias) and dbias = colsum(dx) in one pass over dy/x.
 // Returns -2 when the shape/alignment needs the unfused path.  workspace as col_sum.
 int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
-                        float* workspace, int64_t rows, int64_t cols, hipStream_t s) {
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate) {
   if (rows <= 0 || cols <= 0) return 0;
   const int parts = col_sum_parts(rows);
   const int64_t rpp = (rows + parts - 1) / parts;
@@ -253,11 +443,13 @@ int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias,
                      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                        reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
     if (!vec) return -2;
-    dim3 g(static_cast<unsigned>((cols / N + 255) / 256), static_cast<unsigned>(parts));
+    const ColWalk w = col_walk(cols / N);
+    dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
     bias_gelu_bwd_dbias_kernel<T><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
                                                     static_cast<const T*>(bias), static_cast<T*>(dx), workspace,
-                                                    rows, cols, rpp);
-    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(dbias), s);
+                                                    rows, cols, rpp, w.cvb, w.rl);
+    reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(dbias), s,
+                    accumulate);
   });
   return static_cast<int>(hipGetLastError());
 }

@@ -46,7 +46,7 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
 // dgamma/dbeta from the per-block partials; work = [kLnReduceSlices][2][cols] fp32 scratch.
 constexpr int kLnReduceSlices = 32;
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
-                         int64_t cols, float* work, hipStream_t s);
+                         int64_t cols, float* work, hipStream_t s, bool accumulate = false);
 // Distributed-LN pieces (hidden sharded across TP): apply with global stats, local sums.
 int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const void* b, const float* mean,
                           const float* var, void* y, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);
@@ -60,10 +60,12 @@ int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows
 int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
                   hipStream_t s);
 // Column sums of a [rows, cols] matrix into fp32 partials then final (for bias grads).
-int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s);
+// accumulate: out += colsum(x) (bias gradients bound into the flat grad buffer).
+int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s,
+            bool accumulate = false);
 int col_sum_parts(int64_t rows);
 int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
-                        float* workspace, int64_t rows, int64_t cols, hipStream_t s);
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate = false);
 
 // --------------------------------------------------------------- softmax (softmax.hip)
 int scaled_masked_softmax_fwd(int dt, const void* x, const uint8_t* mask, void* y, int64_t batch, int64_t heads,

@@ -315,10 +315,12 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce_stage1(const float* __restr
 // Stage 2: one thread per column adds the slice sums (fixed order: deterministic).
 template <typename W>
 __global__ void __launch_bounds__(256) ln_bwd_reduce_stage2(const float* __restrict__ part2, W* __restrict__ dw,
-                                                            W* __restrict__ db, int64_t cols, int slices) {
+                                                            W* __restrict__ db, int64_t cols, int slices,
+                                                            bool accumulate) {
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (c >= cols) return;
-  float a = 0.f, b = 0.f;
+  float a = (accumulate && dw) ? to_f32(dw[c]) : 0.f;
+  float b = (accumulate && db) ? to_f32(db[c]) : 0.f;
   for (int s = 0; s < slices; ++s) {
     a += part2[static_cast<int64_t>(s) * 2 * cols + c];
     b += part2[static_cast<int64_t>(s) * 2 * cols + cols + c];
@@ -431,14 +433,14 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
 }
 
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
-                         int64_t cols, float* work, hipStream_t s) {
+                         int64_t cols, float* work, hipStream_t s, bool accumulate) {
   // work: [kLnReduceSlices][2][cols] fp32
   const int slices = parts < kLnReduceSlices ? parts : kLnReduceSlices;
   dim3 g1(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>(slices));
   ln_bwd_reduce_stage1<<<g1, 256, 0, s>>>(dw_part, db_part, work, parts, cols, slices);
   SMPK_DISPATCH(wdt, W, {
     ln_bwd_reduce_stage2<W><<<static_cast<int>((cols + 255) / 256), 256, 0, s>>>(
-        work, static_cast<W*>(dw), static_cast<W*>(db), cols, slices);
+        work, static_cast<W*>(dw), static_cast<W*>(db), cols, slices, accumulate);
   });
   return static_cast<int>(hipGetLastError());
 }

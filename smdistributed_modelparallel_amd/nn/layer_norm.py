@@ -12,7 +12,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..ops.layernorm import add_layer_norm, layer_norm
+from ..ops.layernorm import add_layer_norm, layer_norm, layer_norm_passthrough
 from .utils import get_local_channels, get_start_pos_for_slicing, tp_group, tp_size
 
 
@@ -43,6 +43,13 @@ class FusedLayerNorm(nn.Module):
     def forward_add(self, x, residual):
         """(LN(x + residual), x + residual) in one kernel."""
         return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
+
+    def forward_passthrough(self, x):
+        """(LN(x), x) where x's two gradient paths (LN input, residual branch) are summed
+        inside the LN backward kernel."""
+        if type(self).forward is not FusedLayerNorm.forward or len(self.normalized_shape) != 1:
+            return self(x), x
+        return layer_norm_passthrough(x, self.weight, self.bias, self.eps)
 
     def extra_repr(self):
         return f"{self.normalized_shape}, eps={self.eps}, elementwise_affine={self.elementwise_affine}"

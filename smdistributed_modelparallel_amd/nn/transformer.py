@@ -507,7 +507,11 @@ class DistributedTransformerLayer(DistributedModule):
             mlp = out.core(m)
             hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:
-            a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
+            if at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
+                # hidden feeds LN1 and the residual add: its two gradients meet in the LN kernel
+                a, hidden = at.pre_layernorm_module.forward_passthrough(hidden)
+            else:
+                a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
             attn = at.dropout(at.core(a, mask))
             if at.post_layernorm:
                 hidden = at.layernorm(attn + hidden)

@@ -4,6 +4,7 @@ import math
 import torch
 
 from ._ext import ext
+from .linear import _fusable
 
 
 def _gelu_tanh_ref(x):
@@ -24,7 +25,11 @@ class _BiasGeLU(torch.autograd.Function):
         x, bias = ctx.saved_tensors
         C = ext()
         if ctx.has_bias and ctx.needs_input_grad[1]:
-            # one pass: dx and its column sums (the bias gradient) together
+            # one pass: dx and its column sums (the bias gradient) together; a bias bound
+            # to the flat grad buffer gets them accumulated in place (no temp + add)
+            if _fusable(bias):
+                dx, _ = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias, bias.grad)
+                return dx, None
             dx, db = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias)
             return dx, db
         return C.bias_gelu_bwd(dy.contiguous(), x, bias), None

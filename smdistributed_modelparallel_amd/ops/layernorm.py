@@ -8,6 +8,18 @@ input / weight dtypes.
 import torch
 
 from ._ext import ext
+from .linear import _fusable
+
+
+def _ln_bwd(dy, x, w, b, mean, rstd, need_w, need_b, dres):
+    """LayerNorm backward; dgamma/dbeta of parameters bound to the flat grad buffer are
+    accumulated in place by the reduce kernel (autograd then gets None for them, and the
+    params' post-accumulate hooks still fire)."""
+    if need_w and need_b and _fusable(w) and _fusable(b):
+        dx, _, _ = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres, w.grad, b.grad)
+        return dx, None, None
+    dx, dw, db = ext().layernorm_bwd(dy, x, w, mean, rstd, need_w, need_b, dres)
+    return dx, (dw if need_w else None), (db if need_b else None)
 
 
 class _FusedLayerNorm(torch.autograd.Function):
@@ -17,6 +29,7 @@ class _FusedLayerNorm(torch.autograd.Function):
         x2 = x.contiguous()
         y, mean, rstd = ext().layernorm_fwd(x2, None, weight, bias, eps)
         ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.bias = bias
         ctx.has_w = weight is not None
         ctx.has_b = bias is not None
         return y.view(shape)
@@ -26,8 +39,36 @@ class _FusedLayerNorm(torch.autograd.Function):
         x, w, mean, rstd = ctx.saved_tensors
         need_w = ctx.has_w and ctx.needs_input_grad[1]
         need_b = ctx.has_b and ctx.needs_input_grad[2]
-        dx, dw, db = ext().layernorm_bwd(dy.contiguous(), x, w, mean, rstd, need_w, need_b, None)
-        return dx, (dw if need_w else None), (db if need_b else None), None
+        dx, dw, db = _ln_bwd(dy.contiguous(), x, w, ctx.bias, mean, rstd, need_w, need_b, None)
+        return dx, dw, db, None
+
+
+class _FusedLayerNormPassthrough(torch.autograd.Function):
+    """(LN(x), x) -- the second output is the residual branch.  Backward sums the two
+    gradient paths of x inside the LN backward kernel (dres) instead of leaving autograd
+    to add them with a separate full-size elementwise pass."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x2 = x.contiguous()
+        y, mean, rstd = ext().layernorm_fwd(x2, None, weight, bias, eps)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.bias = bias
+        ctx.has_w = weight is not None
+        ctx.has_b = bias is not None
+        ctx.set_materialize_grads(False)
+        return y.view(x.shape), x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        x, w, mean, rstd = ctx.saved_tensors
+        need_w = ctx.has_w and ctx.needs_input_grad[1]
+        need_b = ctx.has_b and ctx.needs_input_grad[2]
+        if dy is None:
+            return dres, None, None, None
+        dres = dres.contiguous() if dres is not None else None
+        dx, dw, db = _ln_bwd(dy.contiguous(), x, w, ctx.bias, mean, rstd, need_w, need_b, dres)
+        return dx.view(dy.shape), dw, db, None
 
 
 class _FusedAddLayerNorm(torch.autograd.Function):
@@ -38,6 +79,7 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         x2, r2 = x.contiguous(), residual.contiguous()
         y, mean, rstd, s = ext().layernorm_fwd(x2, r2, weight, bias, eps)
         ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.bias = bias
         ctx.has_w = weight is not None
         ctx.has_b = bias is not None
         return y.view(x.shape), s.view(x.shape)
@@ -48,14 +90,21 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         need_w = ctx.has_w and ctx.needs_input_grad[2]
         need_b = ctx.has_b and ctx.needs_input_grad[3]
         dres = ds.contiguous() if ds is not None else None
-        dx, dw, db = ext().layernorm_bwd(dy.contiguous(), s, w, mean, rstd, need_w, need_b, dres)
-        return dx, dx, (dw if need_w else None), (db if need_b else None), None
+        dx, dw, db = _ln_bwd(dy.contiguous(), s, w, ctx.bias, mean, rstd, need_w, need_b, dres)
+        return dx, dx, dw, db, None
 
 
 def layer_norm(x, weight, bias, eps=1e-5):
     if x.is_cuda:
         return _FusedLayerNorm.apply(x, weight, bias, eps)
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
+
+
+def layer_norm_passthrough(x, weight, bias, eps=1e-5):
+    """Returns (LN(x), x) with the two backward paths of x summed inside the LN kernel."""
+    if x.is_cuda:
+        return _FusedLayerNormPassthrough.apply(x, weight, bias, eps)
+    return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps), x
 
 
 def add_layer_norm(x, residual, weight, bias, eps=1e-5):

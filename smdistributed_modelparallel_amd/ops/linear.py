@@ -15,12 +15,15 @@ import torch
 import torch.nn.functional as F
 
 
-def _col_sum(x2):
-    """Bias gradient: HIP two-stage column sum on GPU (HBM-rate), torch elsewhere."""
+def _col_sum(x2, out=None):
+    """Bias gradient: HIP two-stage column sum on GPU (HBM-rate), torch elsewhere.
+    With ``out`` the sums are accumulated into it in place (and ``out`` is returned)."""
     if x2.is_cuda and x2.dtype in (torch.float16, torch.bfloat16, torch.float32) and x2.is_contiguous():
         from ._ext import ext
 
-        return ext().col_sum(x2)
+        return ext().col_sum(x2, out)
+    if out is not None:
+        return out.add_(x2.sum(0).to(out.dtype))
     return x2.sum(0)
 
 
@@ -35,6 +38,7 @@ class _LinearWGradAccum(torch.autograd.Function):
     def forward(ctx, x, weight, bias):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
+        ctx.bias = bias
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -45,7 +49,10 @@ class _LinearWGradAccum(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.matmul(dy, w)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _col_sum(dy2)
+            if _fusable(ctx.bias) and dy2.is_cuda:
+                _col_sum(dy2, ctx.bias.grad)  # into the bound flat-buffer view (no temp + add)
+            else:
+                db = _col_sum(dy2)
         if ctx.needs_input_grad[1]:
             if _fusable(w):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the

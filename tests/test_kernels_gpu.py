@@ -67,13 +67,13 @@ def test_add_layernorm(C, dt):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("rows", [33, 5000])
-def test_bias_gelu(C, dt, rows):
+@pytest.mark.parametrize("rows,cols", [(33, 6400), (5000, 6400), (777, 1600), (1031, 4800), (300, 40), (129, 1001)])
+def test_bias_gelu(C, dt, rows, cols):
     from smdistributed_modelparallel_amd.ops.gelu import _gelu_tanh_ref, bias_gelu
 
     torch.manual_seed(2)
-    x = torch.randn(rows, 6400, device="cuda", dtype=dt, requires_grad=True)
-    b = torch.randn(6400, device="cuda", dtype=dt, requires_grad=True)
+    x = torch.randn(rows, cols, device="cuda", dtype=dt, requires_grad=True)
+    b = torch.randn(cols, device="cuda", dtype=dt, requires_grad=True)
     y = bias_gelu(x, b)
     xr, br = x.detach().float().requires_grad_(), b.detach().float().requires_grad_()
     yr = _gelu_tanh_ref(xr + br)
@@ -84,6 +84,37 @@ def test_bias_gelu(C, dt, rows):
     yr.backward(g)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
     assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50 * max(1, rows // 200) ** 0.5, rtol=tol * 4)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("rows,cols", [(32768, 1600), (4097, 4800), (100, 6400), (7, 40), (515, 1001), (64, 8)])
+def test_col_sum_and_accumulate(C, dt, rows, cols):
+    torch.manual_seed(5)
+    x = torch.randn(rows, cols, device="cuda", dtype=dt)
+    ref = x.double().sum(0)
+    out = C.col_sum(x)
+    tol = {torch.float32: 1e-4, torch.float16: 2e-3, torch.bfloat16: 1e-2}[dt]
+    scale = max(1.0, rows ** 0.5)
+    assert torch.allclose(out.double(), ref, atol=tol * scale, rtol=tol)
+    # in-place accumulation into an existing gradient view (flat-buffer bias grads)
+    base = torch.randn(cols, device="cuda", dtype=dt)
+    acc = base.clone()
+    r = C.col_sum(x, acc)
+    assert r.data_ptr() == acc.data_ptr()
+    assert torch.allclose(acc.double(), base.double() + ref, atol=tol * scale, rtol=tol)
+    # fused gelu backward accumulating its dbias
+    if cols % 8 == 0 and dt != torch.float32:
+        from smdistributed_modelparallel_amd.ops.gelu import _gelu_tanh_ref
+
+        b = torch.randn(cols, device="cuda", dtype=dt)
+        dy = torch.randn_like(x)
+        db = base.clone()
+        dx, db2 = C.bias_gelu_bwd_dbias(dy, x, b, db)
+        assert db2.data_ptr() == db.data_ptr()
+        xr = (x.float() + b.float()).requires_grad_()
+        _gelu_tanh_ref(xr).backward(dy.float())
+        assert torch.allclose(dx.float(), xr.grad, atol=tol * 4, rtol=tol * 4)
+        assert torch.allclose(db.double(), base.double() + xr.grad.double().sum(0), atol=tol * 4 * scale, rtol=tol * 4)
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
@@ -185,6 +216,50 @@ def test_gpt_step_gpu(C):
     assert abs(loss_gpu.item() - loss_cpu.item()) < 1e-3
     for n, p in m.named_parameters():
         assert torch.allclose(p.grad.cpu(), g_cpu[n], atol=2e-3, rtol=1e-2), n
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_gpt_fused_grad_accumulation_gpu(C, dt):
+    """Gradients bound to pre-allocated views (the flat-buffer layout: `_smp_fused_grad`)
+    are accumulated in place by the kernels -- weight GEMMs with beta=1, bias column sums,
+    GeLU dbias, LayerNorm dgamma/dbeta -- and the residual stream's two gradient paths meet
+    inside the LN backward.  Two accumulated backwards must equal autograd's."""
+    from smdistributed_modelparallel_amd.models import build_gpt
+
+    torch.manual_seed(11)
+    kw = dict(dropout=0.0, hidden_size=128, num_attention_heads=2, attention_head_size=64, intermediate_size=512)
+    ref = build_gpt("gpt2-tiny", **kw).cuda().to(dt)
+    fused = build_gpt("gpt2-tiny", **kw).cuda().to(dt)
+    fused.load_state_dict(ref.state_dict())
+    for p in fused.parameters():
+        p.grad = torch.zeros_like(p)
+        p._smp_fused_grad = True
+    ids = torch.randint(0, 512, (2, 64), device="cuda")
+    for _ in range(2):
+        for m in (ref, fused):
+            loss, _ = m((ids, None, None, None, ids))
+            loss.float().backward()
+    tol = 2e-4 if dt == torch.float32 else 3e-2
+    for (n, p), (_, q) in zip(ref.named_parameters(), fused.named_parameters()):
+        assert torch.allclose(q.grad.float(), p.grad.float(), atol=tol, rtol=tol * 5), n
+
+
+def test_layer_norm_passthrough_gpu(C):
+    from smdistributed_modelparallel_amd.ops.layernorm import layer_norm_passthrough
+
+    torch.manual_seed(3)
+    x = torch.randn(4, 33, 1600, device="cuda", requires_grad=True)
+    w = torch.randn(1600, device="cuda", requires_grad=True)
+    b = torch.randn(1600, device="cuda", requires_grad=True)
+    y, r = layer_norm_passthrough(x, w, b)
+    gy, gr = torch.randn_like(y), torch.randn_like(r)
+    (y * gy).sum().add_((r * gr).sum()).backward()
+    xr, wr, br = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (1600,), wr, br)
+    ((yr * gy).sum() + (xr * gr).sum()).backward()
+    assert torch.allclose(y, yr, atol=1e-4)
+    for a, c in ((x, xr), (w, wr), (b, br)):
+        assert torch.allclose(a.grad, c.grad, atol=1e-3, rtol=1e-3)
 
 
 def test_offloaded_checkpoint_gpu():

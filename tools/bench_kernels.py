@@ -55,6 +55,7 @@ def bench_attention(b, s, h, d, causal=True):
 
 def bench_memory_bound():
     from smdistributed_modelparallel_amd.ops import layernorm, gelu, multi_tensor
+    from smdistributed_modelparallel_amd.ops._ext import ext
 
     res = {}
     x = torch.randn(16384, 1600, device="cuda", dtype=torch.bfloat16)
@@ -62,10 +63,27 @@ def bench_memory_bound():
     bb = torch.zeros(1600, device="cuda", dtype=torch.bfloat16)
     t = timeit(lambda: layernorm.layer_norm(x, w, bb))
     res["layernorm_fwd_GBps"] = 2 * x.numel() * 2 / t / 1e6
-    xg = torch.randn(16384, 6400, device="cuda", dtype=torch.bfloat16)
+    C = ext()
+    xg = torch.randn(32768, 6400, device="cuda", dtype=torch.bfloat16)
     bg = torch.randn(6400, device="cuda", dtype=torch.bfloat16)
     t = timeit(lambda: gelu.bias_gelu(xg, bg))
     res["bias_gelu_fwd_GBps"] = 2 * xg.numel() * 2 / t / 1e6
+    res["bias_gelu_fwd_us"] = t * 1e3
+    t = timeit(lambda: torch.nn.functional.gelu(xg, approximate="tanh"))
+    res["torch_gelu_tanh_fwd_GBps"] = 2 * xg.numel() * 2 / t / 1e6
+    t = timeit(lambda: xg.clone())
+    res["torch_clone_GBps"] = 2 * xg.numel() * 2 / t / 1e6
+    dg = torch.randn_like(xg)
+    t = timeit(lambda: C.bias_gelu_bwd_dbias(dg, xg, bg))
+    res["bias_gelu_bwd_dbias_GBps"] = 3 * xg.numel() * 2 / t / 1e6
+    res["bias_gelu_bwd_dbias_us"] = t * 1e3
+    del dg
+    for cols in (1600, 4800):
+        xc = torch.randn(32768, cols, device="cuda", dtype=torch.bfloat16)
+        t = timeit(lambda: C.col_sum(xc))
+        res[f"col_sum_32768x{cols}_GBps"] = xc.numel() * 2 / t / 1e6
+        res[f"col_sum_32768x{cols}_us"] = t * 1e3
+    del xg
     n = 200_000_000
     p = torch.randn(n, device="cuda", dtype=torch.bfloat16)
     gr = torch.randn(n, device="cuda", dtype=torch.bfloat16)
