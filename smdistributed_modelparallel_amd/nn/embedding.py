@@ -47,10 +47,14 @@ class DistributedEmbedding(nn.Module):
             self.vocab_start_idx, self.vocab_end_idx = 0, num_embeddings
             shape = (num_embeddings, self.local_dim)
         self.weight = nn.Parameter(torch.empty(shape, dtype=dtype))
-        with torch.no_grad():
-            self.weight.normal_(0.0, initializer_range)
+        self.initializer_range = initializer_range
+        self.reset_parameters()
         mark_scaled_batch(self.weight)
         mark_tp(self.weight, 0 if vocab_parallel else 1)
+
+    def reset_parameters(self):
+        with torch.no_grad():
+            self.weight.normal_(0.0, self.initializer_range)
 
     def forward(self, ids):
         if tp_size() == 1:

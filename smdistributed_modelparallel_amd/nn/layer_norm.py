@@ -40,6 +40,12 @@ class FusedLayerNorm(nn.Module):
                        self.bias, self.eps)
         return y.view(shape)
 
+    def reset_parameters(self):
+        if self.weight is not None:
+            with torch.no_grad():
+                self.weight.fill_(1.0)
+                self.bias.zero_()
+
     def forward_add(self, x, residual):
         """(LN(x + residual), x + residual) in one kernel."""
         return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
@@ -119,6 +125,12 @@ class DistributedLayerNorm(nn.Module):
         else:
             self.register_parameter("weight", None)
             self.register_parameter("bias", None)
+
+    def reset_parameters(self):
+        if self.weight is not None:
+            with torch.no_grad():
+                self.weight.fill_(1.0)
+                self.bias.zero_()
 
     def forward(self, x):
         group = tp_group() if tp_size() > 1 else None

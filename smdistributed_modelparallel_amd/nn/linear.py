@@ -37,16 +37,21 @@ class DistributedLinear(nn.Module):
             self.bias = nn.Parameter(torch.empty(out_features, dtype=dtype))
         else:
             self.register_parameter("bias", None)
-        init_weight_(self.weight, in_features, out_features)
-        if self.bias is not None:
-            bound = 1.0 / math.sqrt(in_features)
-            with torch.no_grad():
-                self.bias.uniform_(-bound, bound)
+        self.reset_parameters()
         for p in self.parameters():
             mark_scaled_batch(p)
         mark_tp(self.weight, 1)
         if self.bias is not None:
             mark_tp(self.bias, None, rank0_only=True)
+
+    def reset_parameters(self):
+        """nn.Linear initialisation of the full (unsharded) layer; also run by delayed
+        parameter initialisation when the module is materialised."""
+        init_weight_(self.weight, self.in_features, self.out_features)
+        if self.bias is not None:
+            bound = 1.0 / math.sqrt(self.in_features)
+            with torch.no_grad():
+                self.bias.uniform_(-bound, bound)
 
     def forward(self, x):
         if tp_size() == 1:

@@ -173,6 +173,19 @@ class _Dropout(nn.Module):
         return F.dropout(x, self.p, True)
 
 
+def _normal_init(emb, std):
+    """N(0, std) for an nn.Embedding, now and again when delayed parameter initialisation
+    materialises it (nn.Embedding.reset_parameters would use N(0, 1))."""
+    from ..torch.state_mod import state
+
+    def init(m):
+        with torch.no_grad():
+            m.weight.normal_(0.0, std)
+
+    init(emb)
+    state.param_initializers[emb] = init
+
+
 def _activation(x, kind, bias=None, fused=False):
     if kind == "gelu":
         return bias_gelu(x, bias)
@@ -620,12 +633,10 @@ class DistributedTransformerLMHead(DistributedModule):
                                                        vocab_parallel=True)
         else:
             self.word_embedding = nn.Embedding(self.vocab_size, h, dtype=dtype)
-            with torch.no_grad():
-                self.word_embedding.weight.normal_(0.0, self.initializer_range)
+            _normal_init(self.word_embedding, self.initializer_range)
         if self.use_positional_embedding:
             self.position_embedding = nn.Embedding(self.num_positions, h, dtype=dtype)
-            with torch.no_grad():
-                self.position_embedding.weight.normal_(0.0, self.initializer_range)
+            _normal_init(self.position_embedding, self.initializer_range)
         if self.num_token_types > 0:
             self.token_type_embedding = nn.Embedding(self.num_token_types, h, dtype=dtype)
         self.dropout = _Dropout(self.embedding_dropout_prob)

@@ -34,32 +34,49 @@ def _has_meta(m):
         b is not None and b.is_meta for b in m.buffers(recurse=False))
 
 
-def materialize_local(model):
+def materialize_local(model, owner=None, me=None):
+    """Allocate the meta parameters of ``model``: local ones on the device (then re-init),
+    non-local ones as empty tensors.  A meta tensor cannot take real storage through
+    ``.data``, so every meta Parameter is *replaced* (attributes carried over, tied
+    parameters kept tied).  Returns {old Parameter: new Parameter}."""
     root = model.module
     mm = state.module_manager
     device = state.device
-    me = state.core.pp_rank()
+    if me is None:
+        me = state.core.pp_rank()
+    mapping = {}
+    to_init = []
     for m in root.modules():
         if not _has_meta(m):
             continue
-        local = mm.get_partition(m) == me or mm.get_partition(m) is None
+        mod_local = mm.get_partition(m) == me or mm.get_partition(m) is None
+        fresh = False
         for name, p in list(m._parameters.items()):
             if p is None or not p.is_meta:
                 continue
-            if local:
-                p.data = torch.empty(p.shape, dtype=p.dtype, device=device)
-            else:
-                p.data = torch.empty(0, dtype=p.dtype, device=device)
+            if p in mapping:
+                m._parameters[name] = mapping[p]
+                continue
+            local = (owner.get(p) == me) if owner is not None and p in owner else mod_local
+            t = torch.empty(p.shape if local else (0,), dtype=p.dtype, device=device)
+            new = torch.nn.Parameter(t, requires_grad=p.requires_grad and local)
+            new.__dict__.update({k: v for k, v in p.__dict__.items() if k != "_cdata"})
+            mapping[p] = new
+            m._parameters[name] = new
+            fresh = fresh or local
         for name, b in list(m._buffers.items()):
             if b is not None and b.is_meta:
-                m._buffers[name] = torch.zeros(b.shape, dtype=b.dtype, device=device) if local else \
+                m._buffers[name] = torch.zeros(b.shape, dtype=b.dtype, device=device) if mod_local else \
                     torch.empty(0, dtype=b.dtype, device=device)
-        if local:
-            init = state.param_initializers.get(m)
-            with torch.no_grad():
-                if init is not None:
-                    init(m)
-                elif hasattr(m, "reset_parameters") and callable(m.reset_parameters):
-                    m.reset_parameters()
-                elif hasattr(root, "_init_weights"):
-                    root._init_weights(m)
+        if fresh:
+            to_init.append(m)
+    for m in to_init:
+        init = state.param_initializers.get(m)
+        with torch.no_grad():
+            if init is not None:
+                init(m)
+            elif hasattr(m, "reset_parameters") and callable(m.reset_parameters):
+                m.reset_parameters()
+            elif hasattr(root, "_init_weights"):
+                root._init_weights(m)
+    return mapping

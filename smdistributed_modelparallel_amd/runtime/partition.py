@@ -21,7 +21,7 @@ from collections import defaultdict
 import torch
 
 from ..backend.collectives import CommGroup
-from ..backend.exceptions import PartitionError, TracingEnd
+from ..backend.exceptions import PartitionError, SMPRuntimeError, TracingEnd
 from ..backend.logger import get_logger
 from ..torch.state_mod import state
 
@@ -77,17 +77,19 @@ def trace_model(model, step_fn, mb_args, mb_kwargs, device):
         if m is root:
             raise TracingEnd()
 
-    for m in root.modules():
-        handles.append(m.register_forward_pre_hook(pre))
-        handles.append(m.register_forward_hook(post))
+    if any(p.is_meta for p in root.parameters()):
+        raise SMPRuntimeError("parameters are on the meta device (delayed initialisation): nothing to trace")
     orig_device = next((p.device for p in root.parameters()), torch.device("cpu"))
     moved = False
-    if device != orig_device:
-        root.to(device)
-        moved = True
-    args = _to_device((mb_args, mb_kwargs), device)
-    state.is_tracing = True
     try:
+        for m in root.modules():
+            handles.append(m.register_forward_pre_hook(pre))
+            handles.append(m.register_forward_hook(post))
+        if device != orig_device:
+            moved = True
+            root.to(device)
+        args = _to_device((mb_args, mb_kwargs), device)
+        state.is_tracing = True
         for trial in range(5 if device.type == "cuda" else 1):
             mm._exec_order.clear()
             with mm.enable_measurement(trial == (4 if device.type == "cuda" else 0)), torch.no_grad():

@@ -180,16 +180,21 @@ class DistributedModel(nn.Module):
         for m in self.module.modules():
             for name, p in list(m.named_parameters(recurse=False)):
                 if p in local_params:
-                    if p.device != device:
+                    if p.device != device and not p.is_meta:  # meta: materialised below
                         p.data = p.data.to(device)
                 else:
                     p.requires_grad_(False)
-                    p.data = torch.empty(0, dtype=p.dtype, device=device)
+                    if not p.is_meta:  # meta: replaced by an empty tensor below
+                        p.data = torch.empty(0, dtype=p.dtype, device=device)
             if mm.get_partition(m) == me:
                 for name, b in list(m.named_buffers(recurse=False)):
-                    if b is not None and b.device != device:
+                    if b is not None and b.device != device and not b.is_meta:
                         m._buffers[name] = b.to(device)
-        self._init_deferred_params()
+        mapping = self._init_deferred_params(owner, me)
+        if mapping:
+            owner = {mapping.get(p, p): part for p, part in owner.items()}
+            self._param_owner = owner
+            local_params = {mapping.get(p, p) for p in local_params}
         self._local_params = [p for p in self._ordered_params() if p in local_params]
         self._update_transformer_boundaries()
         if state.cfg.zero2d_enabled():
@@ -214,10 +219,10 @@ class DistributedModel(nn.Module):
         if state.cfg.delayed_parameter_initialization:
             pass
 
-    def _init_deferred_params(self):
+    def _init_deferred_params(self, owner=None, me=None):
         from ..parallel.delayed_init import materialize_local
 
-        materialize_local(self)
+        return materialize_local(self, owner, me)
 
     def _ordered_params(self):
         seen, out = set(), []

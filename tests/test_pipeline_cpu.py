@@ -127,3 +127,15 @@ def test_sharded_dp2_gradient_clipping():
 @pytest.mark.parametrize("world,pp,tp", [(2, 1, 1), (2, 1, 2), (2, 2, 1), (4, 2, 2)])
 def test_clip_master_grads_global_norm(world, pp, tp):
     _run(world, pp, tp, 2, extra={"opt_clip": 0.05})
+
+
+@pytest.mark.parametrize("auto", [0, 1])
+def test_pp2_delayed_parameter_initialization(auto):
+    """Parameters built on `meta` under smp.delay_param_initialization(): only each stage's
+    own parameters are allocated after partitioning (non-local ones stay empty), the
+    deferred load_state_dict fills them, and training matches the reference."""
+    _run(2, 2, 1, 2, auto=auto, extra={"delayed": True, "cfg": {"delayed_parameter_initialization": True}})
+
+
+def test_dp2_delayed_parameter_initialization():
+    _run(2, 1, 1, 2, extra={"delayed": True, "cfg": {"delayed_parameter_initialization": True}})

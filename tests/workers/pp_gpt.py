@@ -29,9 +29,13 @@ def main():
     kw.update(extra.get("model", {}))
     ref = build_gpt("gpt2-tiny", dropout=0.0, **kw)  # built before init: unsharded reference
     smp.init(cfg)
-    with smp.model_creation(tensor_parallelism=tp > 1):
-        net = build_gpt("gpt2-tiny", dropout=0.0, **kw)
-    if tp == 1:
+    delayed = bool(extra.get("delayed"))
+    with smp.delay_param_initialization(enabled=delayed):
+        with smp.model_creation(tensor_parallelism=tp > 1):
+            net = build_gpt("gpt2-tiny", dropout=0.0, **kw)
+    if delayed:
+        assert all(p.is_meta for p in net.parameters())
+    elif tp == 1:
         net.load_state_dict(ref.state_dict())
     else:
         from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
@@ -51,6 +55,9 @@ def main():
         for i, layer in enumerate(layers):
             smp.set_partition(layer, (i * pp) // len(layers))
     model = smp.DistributedModel(net)
+    if delayed:
+        # meta parameters: the reference weights load once the partition has materialised them
+        model.load_state_dict(ref.state_dict())
     if extra.get("jitter"):
         # perturb message timing differently on every rank: TP peers must still agree on order
         import random
