@@ -211,23 +211,24 @@ at::Tensor layernorm_apply_stats(at::Tensor x, c10::optional<at::Tensor> w, c10:
 }
 
 // ------------------------------------------------------------------------ gelu
-at::Tensor bias_gelu_fwd(at::Tensor x, c10::optional<at::Tensor> bias) {
+at::Tensor bias_gelu_fwd(at::Tensor x, c10::optional<at::Tensor> bias, bool exact) {
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   if (bias.has_value()) TORCH_CHECK(bias->numel() == cols && bias->scalar_type() == x.scalar_type(), "bias mismatch");
   auto y = at::empty_like(x);
-  check(smpk::bias_gelu_fwd(dt_code(x), x.data_ptr(), opt_ptr(bias), y.data_ptr(), x.numel() / cols, cols, stream()),
+  check(smpk::bias_gelu_fwd(dt_code(x), x.data_ptr(), opt_ptr(bias), y.data_ptr(), x.numel() / cols, cols, stream(),
+                            exact),
         "bias_gelu_fwd");
   return y;
 }
 
-at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> bias) {
+at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> bias, bool exact) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   auto dx = at::empty_like(x);
   check(smpk::bias_gelu_bwd(dt_code(x), dy.data_ptr(), x.data_ptr(), opt_ptr(bias), dx.data_ptr(), x.numel() / cols,
-                            cols, stream()),
+                            cols, stream(), exact),
         "bias_gelu_bwd");
   return dx;
 }
@@ -252,7 +253,7 @@ at::Tensor col_sum(at::Tensor x, c10::optional<at::Tensor> out_opt) {
 // (dx, dbias) of gelu(x + bias) in one pass; falls back to bwd + col_sum for odd shapes.
 // dbias_out given: dbias accumulated into it in place (and returned).
 std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Tensor bias,
-                                            c10::optional<at::Tensor> dbias_out) {
+                                            c10::optional<at::Tensor> dbias_out, bool exact) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   check_gpu(bias, "bias");
@@ -268,9 +269,9 @@ std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Ten
   const int64_t parts = smpk::col_sum_parts(rows);
   auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
   const int rc = smpk::bias_gelu_bwd_dbias(dt_code(x), dy.data_ptr(), x.data_ptr(), bias.data_ptr(), dx.data_ptr(),
-                                           db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream(), acc);
+                                           db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream(), acc, exact);
   if (rc == -2) {
-    dx = bias_gelu_bwd(dy, x, bias);
+    dx = bias_gelu_bwd(dy, x, bias, exact);
     return {dx, col_sum(dx.view({rows, cols}), dbias_out)};
   }
   check(rc, "bias_gelu_bwd_dbias");
@@ -462,12 +463,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("need_wgrad"), py::arg("need_bgrad"), py::arg("dres"), py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none());
   m.def("layernorm_apply_stats", &layernorm_apply_stats);
-  m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("bias"), py::arg("exact") = false);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("exact") = false);
   m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
   m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),
-        py::arg("dbias_out") = py::none());
+        py::arg("dbias_out") = py::none(), py::arg("exact") = false);
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);
   m.def("scaled_upper_triang_softmax_fwd", &scaled_upper_triang_softmax_fwd);
   m.def("scaled_softmax_bwd", &scaled_softmax_bwd);

@@ -43,7 +43,28 @@ __device__ __forceinline__ float gelu_grad_fast(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * du;
 }
 
-template <typename T, bool VEC>
+// Exact (erf) GeLU: F.gelu's default, which the reference uses unless fused_bias_gelu or
+// SMP_USE_HF_GELU selects the tanh form (`smp/torch/nn/transformer.py:994,1106-1127`).
+constexpr float kInvSqrt2 = 0.7071067811865476f;
+constexpr float kInvSqrt2Pi = 0.3989422804014327f;
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * kInvSqrt2)); }
+
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  return 0.5f * (1.f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+
+// ACT 0: tanh approximation, ACT 1: exact erf.
+template <int ACT>
+__device__ __forceinline__ float act_fwd(float x) {
+  return ACT == 1 ? gelu_erf(x) : gelu_fast(x);
+}
+template <int ACT>
+__device__ __forceinline__ float act_grad(float x) {
+  return ACT == 1 ? gelu_erf_grad(x) : gelu_grad_fast(x);
+}
+
+template <typename T, bool VEC, int ACT>
 __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict__ x, const T* __restrict__ bias,
                                                             T* __restrict__ y, int64_t rows, int64_t cols) {
   constexpr int N = Vec16<T>::N;
@@ -59,7 +80,7 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict_
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         float v = to_f32(a.v[j]) + (bias ? to_f32(bb.v[j]) : 0.f);
-        o.v[j] = from_f32<T>(gelu_f(v));
+        o.v[j] = from_f32<T>(act_fwd<ACT>(v));
       }
       store16(y + i, o);
     }
@@ -67,12 +88,12 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_kernel(const T* __restrict_
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * 256) {
       float v = to_f32(x[i]) + (bias ? to_f32(bias[i % cols]) : 0.f);
-      y[i] = from_f32<T>(gelu_f(v));
+      y[i] = from_f32<T>(act_fwd<ACT>(v));
     }
   }
 }
 
-template <typename T, bool VEC>
+template <typename T, bool VEC, int ACT>
 __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                             const T* __restrict__ bias, T* __restrict__ dx,
                                                             int64_t rows, int64_t cols) {
@@ -90,7 +111,7 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         float v = to_f32(a.v[j]) + (bias ? to_f32(bb.v[j]) : 0.f);
-        o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad(v));
+        o.v[j] = from_f32<T>(to_f32(d.v[j]) * act_grad<ACT>(v));
       }
       store16(dx + i, o);
     }
@@ -98,7 +119,7 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const T* __restrict_
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * 256) {
       float v = to_f32(x[i]) + (bias ? to_f32(bias[i % cols]) : 0.f);
-      dx[i] = from_f32<T>(to_f32(dy[i]) * gelu_grad(v));
+      dx[i] = from_f32<T>(to_f32(dy[i]) * act_grad<ACT>(v));
     }
   }
 }
@@ -200,7 +221,7 @@ __global__ void __launch_bounds__(256) col_sum_partial(const T* __restrict__ x, 
 
 // Fused backward + bias gradient over the column walker: dx = dy * gelu'(x + b) is
 // written once and its column sums (dbias partials) never re-read dx.
-template <typename T>
+template <typename T, int ACT>
 __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                   const T* __restrict__ bias, T* __restrict__ dx,
                                                                   float* __restrict__ part, int64_t rows, int64_t cols,
@@ -233,7 +254,7 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __res
         Vec16<T> o;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-          o.v[j] = from_f32<T>(to_f32(d[u].v[j]) * gelu_grad_fast(to_f32(a[u].v[j]) + bb[j]));
+          o.v[j] = from_f32<T>(to_f32(d[u].v[j]) * act_grad<ACT>(to_f32(a[u].v[j]) + bb[j]));
           acc[j] += to_f32(o.v[j]);
         }
         store16(dx + (r + u * rl) * cols + c, o);
@@ -245,7 +266,7 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __res
       Vec16<T> o;
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        o.v[j] = from_f32<T>(to_f32(d.v[j]) * gelu_grad_fast(to_f32(a.v[j]) + bb[j]));
+        o.v[j] = from_f32<T>(to_f32(d.v[j]) * act_grad<ACT>(to_f32(a.v[j]) + bb[j]));
         acc[j] += to_f32(o.v[j]);
       }
       store16(dx + r * cols + c, o);
@@ -266,7 +287,7 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __res
 }
 
 // Forward over the column walker: bias in registers, U rows of 16-byte loads in flight.
-template <typename T>
+template <typename T, int ACT>
 __global__ void __launch_bounds__(256) bias_gelu_fwd_walk(const T* __restrict__ x, const T* __restrict__ bias,
                                                           T* __restrict__ y, int64_t rows, int64_t cols,
                                                           int64_t rows_per_part, int cvb, int rl) {
@@ -294,7 +315,7 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_walk(const T* __restrict__ 
     for (int u = 0; u < kUnroll; ++u) {
       Vec16<T> o;
 #pragma unroll
-      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(gelu_fast(to_f32(a[u].v[j]) + bb[j]));
+      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a[u].v[j]) + bb[j]));
       store16(y + (r + u * rl) * cols + c, o);
     }
   }
@@ -302,7 +323,7 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_walk(const T* __restrict__ 
     Vec16<T> a = load16(x + r * cols + c);
     Vec16<T> o;
 #pragma unroll
-    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(gelu_fast(to_f32(a.v[j]) + bb[j]));
+    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a.v[j]) + bb[j]));
     store16(y + r * cols + c, o);
   }
 }
@@ -352,9 +373,19 @@ inline int elt_grid(int64_t total, int per_thread) {
   return static_cast<int>(b);
 }
 
+template <typename T, bool V, int A>
+void launch_gelu_bwd(const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
+                     hipStream_t s) {
+  constexpr int N = Vec16<T>::N;
+  bias_gelu_bwd_kernel<T, V, A><<<elt_grid(rows * cols, V ? N : 1), 256, 0, s>>>(
+      static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(dx), rows,
+      cols);
+}
+
 }  // namespace
 
-int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s) {
+int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s,
+                  bool exact) {
   const int64_t total = rows * cols;
   if (total <= 0) return 0;
   SMPK_DISPATCH(dt, T, {
@@ -370,18 +401,26 @@ int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows
       if (parts < 1) parts = 1;
       const int64_t rpp = (rows + parts - 1) / parts;
       dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
-      bias_gelu_fwd_walk<T><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
-                                              static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
+      if (exact)
+        bias_gelu_fwd_walk<T, 1><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
+                                                   static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
+      else
+        bias_gelu_fwd_walk<T, 0><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
+                                                   static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
     } else {
-      bias_gelu_fwd_kernel<T, false><<<elt_grid(total, 1), 256, 0, s>>>(
-          static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
+      if (exact)
+        bias_gelu_fwd_kernel<T, false, 1><<<elt_grid(total, 1), 256, 0, s>>>(
+            static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
+      else
+        bias_gelu_fwd_kernel<T, false, 0><<<elt_grid(total, 1), 256, 0, s>>>(
+            static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows, cols);
     }
   });
   return static_cast<int>(hipGetLastError());
 }
 
 int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
-                  hipStream_t s) {
+                  hipStream_t s, bool exact) {
   const int64_t total = rows * cols;
   if (total <= 0) return 0;
   SMPK_DISPATCH(dt, T, {
@@ -389,14 +428,14 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                                           reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) &
                                          15) == 0;
-    if (vec)
-      bias_gelu_bwd_kernel<T, true><<<elt_grid(total, N), 256, 0, s>>>(
-          static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(dx), rows,
-          cols);
+    if (vec && exact)
+      launch_gelu_bwd<T, true, 1>(dy, x, bias, dx, rows, cols, s);
+    else if (vec)
+      launch_gelu_bwd<T, true, 0>(dy, x, bias, dx, rows, cols, s);
+    else if (exact)
+      launch_gelu_bwd<T, false, 1>(dy, x, bias, dx, rows, cols, s);
     else
-      bias_gelu_bwd_kernel<T, false><<<elt_grid(total, 1), 256, 0, s>>>(
-          static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(dx), rows,
-          cols);
+      launch_gelu_bwd<T, false, 0>(dy, x, bias, dx, rows, cols, s);
   });
   return static_cast<int>(hipGetLastError());
 }
@@ -433,7 +472,8 @@ int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, in
 // dx = dy * gelu'(x + bias) and dbias = colsum(dx) in one pass over dy/x.
 // Returns -2 when the shape/alignment needs the unfused path.  workspace as col_sum.
 int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
-                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate) {
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate,
+                        bool exact) {
   if (rows <= 0 || cols <= 0) return 0;
   const int parts = col_sum_parts(rows);
   const int64_t rpp = (rows + parts - 1) / parts;
@@ -445,9 +485,14 @@ int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias,
     if (!vec) return -2;
     const ColWalk w = col_walk(cols / N);
     dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
-    bias_gelu_bwd_dbias_kernel<T><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
-                                                    static_cast<const T*>(bias), static_cast<T*>(dx), workspace,
-                                                    rows, cols, rpp, w.cvb, w.rl);
+    if (exact)
+      bias_gelu_bwd_dbias_kernel<T, 1><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                         static_cast<const T*>(bias), static_cast<T*>(dx), workspace,
+                                                         rows, cols, rpp, w.cvb, w.rl);
+    else
+      bias_gelu_bwd_dbias_kernel<T, 0><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                         static_cast<const T*>(bias), static_cast<T*>(dx), workspace,
+                                                         rows, cols, rpp, w.cvb, w.rl);
     reduce_parts<T>(workspace, parts, cols, workspace + static_cast<int64_t>(parts) * cols, static_cast<T*>(dbias), s,
                     accumulate);
   });

@@ -55,17 +55,20 @@ int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned);
 
 // ------------------------------------------------------------- elementwise (gelu.hip)
 // y = gelu_tanh(x + bias) ; bias broadcast over the last dim (may be null).
-int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s);
+// exact: erf GeLU (F.gelu) instead of the tanh approximation.
+int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows, int64_t cols, hipStream_t s,
+                  bool exact = false);
 // dx = dy * gelu'(x + bias) ; dbias partial sums per row-chunk (fp32) when dbias_part != null.
 int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void* dx, int64_t rows, int64_t cols,
-                  hipStream_t s);
+                  hipStream_t s, bool exact = false);
 // Column sums of a [rows, cols] matrix into fp32 partials then final (for bias grads).
 // accumulate: out += colsum(x) (bias gradients bound into the flat grad buffer).
 int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s,
             bool accumulate = false);
 int col_sum_parts(int64_t rows);
 int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
-                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate = false);
+                        float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate = false,
+                        bool exact = false);
 
 // --------------------------------------------------------------- softmax (softmax.hip)
 int scaled_masked_softmax_fwd(int dt, const void* x, const uint8_t* mask, void* y, int64_t batch, int64_t heads,

@@ -42,7 +42,6 @@ def build_gpt(name, dropout=0.1, **overrides):
     cfg = dict(GPT_CONFIGS[name])
     cfg.update(attention_dropout_prob=dropout, hidden_dropout_prob=dropout, embedding_dropout_prob=dropout)
     cfg["causal_mask_size"] = cfg["num_positions"]
-    cfg.pop("fused_bias_gelu", None)
     cfg.update(overrides)
     return DistributedTransformerLMHead(**cfg)
 

@@ -23,6 +23,7 @@ MI355X choices:
 """
 import functools
 import math
+import os
 import warnings
 from collections import OrderedDict
 
@@ -186,15 +187,18 @@ def _normal_init(emb, std):
     state.param_initializers[emb] = init
 
 
-def _activation(x, kind, bias=None, fused=False):
+def _activation(x, kind, bias=None, tanh_gelu=False):
+    """"gelu" follows the reference (`smp/torch/nn/transformer.py:994,1096-1127`): the exact
+    erf GeLU (F.gelu) unless fused_bias_gelu or SMP_USE_HF_GELU=1 select the tanh form
+    (HF "gelu_new"); "gelu_exact" is always erf.  Both run as one fused bias+GeLU kernel."""
     if kind == "gelu":
-        return bias_gelu(x, bias)
+        return bias_gelu(x, bias, exact=not tanh_gelu)
+    if kind == "gelu_exact":
+        return bias_gelu(x, bias, exact=True)
     if bias is not None:
         x = x + bias
     if kind == "relu":
         return F.relu(x)
-    if kind == "gelu_exact":
-        return F.gelu(x)
     raise SMPInvalidArgumentError(f"unsupported activation {kind}")
 
 
@@ -408,6 +412,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
     def __init__(self, *args, **kwargs):
         super().__init__()
         parse_args(self, args, kwargs, self._KEYS)
+        self._tanh_gelu = bool(self.fused_bias_gelu) or os.environ.get("SMP_USE_HF_GELU") == "1"
         self.local_inter = get_local_channels(self.intermediate_size)
         h, li = self.hidden_size, self.local_inter
         dtype = _param_dtype()
@@ -458,12 +463,12 @@ class DistributedTransformerOutputLayer(DistributedModule):
             # m: [B, s, h/tp]; partial products reduce-scattered on the output channels
             x = linear(m, self.dense1_weight, self.dense1_bias)
             x = reduce_scatter_for_tp(x, 2, get_merge_shapes(self.intermediate_size))
-            x = _activation(x, self.activation, None)
+            x = _activation(x, self.activation, None, self._tanh_gelu)
             out = linear(x, self.dense2_weight, self.dense2_bias)
             return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
         m = (bwd_allreduce_for_tp(m) if self._tp > 1 else m)
         x = linear(m, self.dense1_weight)
-        x = _activation(x, self.activation, self.dense1_bias)
+        x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu)
         out = linear(x, self.dense2_weight, self.dense2_bias)
         return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
 

@@ -11,13 +11,18 @@ def _gelu_tanh_ref(x):
     return 0.5 * x * (1.0 + torch.tanh(math.sqrt(2.0 / math.pi) * (x + 0.044715 * torch.pow(x, 3.0))))
 
 
+def _gelu_erf_ref(x):
+    return torch.nn.functional.gelu(x)
+
+
 class _BiasGeLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, bias):
+    def forward(ctx, x, bias, exact):
         x = x.contiguous()
-        y = ext().bias_gelu_fwd(x, bias)
+        y = ext().bias_gelu_fwd(x, bias, exact)
         ctx.save_for_backward(x, bias)
         ctx.has_bias = bias is not None
+        ctx.exact = exact
         return y
 
     @staticmethod
@@ -28,18 +33,19 @@ class _BiasGeLU(torch.autograd.Function):
             # one pass: dx and its column sums (the bias gradient) together; a bias bound
             # to the flat grad buffer gets them accumulated in place (no temp + add)
             if _fusable(bias):
-                dx, _ = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias, bias.grad)
-                return dx, None
-            dx, db = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias)
-            return dx, db
-        return C.bias_gelu_bwd(dy.contiguous(), x, bias), None
+                dx, _ = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias, bias.grad, ctx.exact)
+                return dx, None, None
+            dx, db = C.bias_gelu_bwd_dbias(dy.contiguous(), x, bias, None, ctx.exact)
+            return dx, db, None
+        return C.bias_gelu_bwd(dy.contiguous(), x, bias, ctx.exact), None, None
 
 
-def bias_gelu(x, bias=None):
-    """gelu_tanh(x + bias)."""
+def bias_gelu(x, bias=None, exact=False):
+    """gelu(x + bias): tanh approximation, or the exact erf form (F.gelu) with exact=True."""
     if x.is_cuda:
-        return _BiasGeLU.apply(x, bias)
-    return _gelu_tanh_ref(x + bias if bias is not None else x)
+        return _BiasGeLU.apply(x, bias, bool(exact))
+    v = x + bias if bias is not None else x
+    return _gelu_erf_ref(v) if exact else _gelu_tanh_ref(v)
 
 
 def gelu_tanh(x):

@@ -3,10 +3,16 @@ HF models' outputs with the smp distributed modules (single process, fp32, CPU),
 TP=2 gloo run of an HF GPT-2 auto-replaced through ``smp.model_creation`` matches HF.
 (The reference pins the same through `test/torch/mpi/test_translate_state_dict.py` and
 its model zoo; parity here is against the installed transformers 5.x models.)"""
+import os
+
 import pytest
 import torch
 
 transformers = pytest.importorskip("transformers")
+
+# HF GPT-2/J/Neo use the tanh GeLU ("gelu_new"); like the reference, the smp "gelu"
+# activation is the exact erf form unless SMP_USE_HF_GELU=1 (read at module construction)
+os.environ["SMP_USE_HF_GELU"] = "1"
 
 from smdistributed_modelparallel_amd.nn import DistributedTransformer, DistributedTransformerLMHead  # noqa: E402
 from tests.dist_utils import run_workers  # noqa: E402
@@ -111,5 +117,32 @@ def test_encoder_parity(family):
 
 
 def test_hf_gpt2_auto_tp2_matches_hf():
-    outs = run_workers("hf_gpt2_tp", 2, [], timeout=240)
+    outs = run_workers("hf_gpt2_tp", 2, [], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
     assert all("OK" in o for o in outs)
+
+
+def test_gelu_selection_follows_reference():
+    """activation="gelu": erf GeLU by default, tanh with fused_bias_gelu or SMP_USE_HF_GELU=1."""
+    from smdistributed_modelparallel_amd.nn import DistributedTransformerOutputLayer
+
+    kw = dict(hidden_size=16, intermediate_size=64, hidden_dropout_prob=0.0, pre_layernorm=False, post_layernorm=False)
+    old = os.environ.pop("SMP_USE_HF_GELU", None)
+    try:
+        assert not DistributedTransformerOutputLayer(**kw)._tanh_gelu
+        assert DistributedTransformerOutputLayer(fused_bias_gelu=True, **kw)._tanh_gelu
+        os.environ["SMP_USE_HF_GELU"] = "1"
+        layer = DistributedTransformerOutputLayer(**kw)
+        assert layer._tanh_gelu
+        os.environ.pop("SMP_USE_HF_GELU")
+        exact = DistributedTransformerOutputLayer(**kw)
+        exact.load_state_dict(layer.state_dict())
+        x = torch.randn(2, 5, 16)
+        ln = getattr(exact, "pre_layernorm_module", None) if exact.pre_layernorm else None
+        m = torch.nn.functional.layer_norm(x, (16,), ln.weight, ln.bias) if ln is not None else x
+        h = torch.nn.functional.linear(m, exact.dense1_weight, exact.dense1_bias)
+        ref = torch.nn.functional.linear(torch.nn.functional.gelu(h), exact.dense2_weight, exact.dense2_bias) + x
+        assert torch.allclose(exact(x), ref, atol=1e-5)
+        assert not torch.allclose(layer(x), ref, atol=1e-7)
+    finally:
+        if old is not None:
+            os.environ["SMP_USE_HF_GELU"] = old
