@@ -345,6 +345,45 @@ class ModelParallelCore:
     def barrier(self):
         self.comm.barrier(CommGroup.WORLD)
 
+    # ------------------------------------------------------------ metrics
+    def get_and_reset_memory_metrics(self):
+        """Reference `smp_get_and_reset_memory_metrics` (`smp/backend/core.py:538-550`):
+        receive-pool peak allocated/reserved and device free/total memory, in MB.  The
+        pipeline's receive buffers live in the caching allocator here (no separate D2D
+        pool), so its peaks are the allocator's; free/total come from hipMemGetInfo.
+        Peaks are reset."""
+        import torch
+
+        out = {"d2d_peak_allocated_mb": 0.0, "d2d_peak_reserved_mb": 0.0, "gpu_free_mb": 0.0, "gpu_total_mb": 0.0}
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            dev = torch.cuda.current_device()
+            out["d2d_peak_allocated_mb"] = torch.cuda.max_memory_allocated(dev) / 2**20
+            out["d2d_peak_reserved_mb"] = torch.cuda.max_memory_reserved(dev) / 2**20
+            free, total = torch.cuda.mem_get_info(dev)
+            out["gpu_free_mb"], out["gpu_total_mb"] = free / 2**20, total / 2**20
+            torch.cuda.reset_peak_memory_stats(dev)
+        return out
+
+    def get_and_reset_alloc_metrics(self):
+        """Reference `smp_get_and_reset_alloc_metrics` (`core.py:552-562`): allocation
+        success / failure counters since the last call (allocator retries and OOMs count
+        as failures), plus control-plane message counts of the native mailbox."""
+        import torch
+
+        out = {"alloc_success": 0, "alloc_fail": 0}
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            st = torch.cuda.memory_stats()
+            allocs = st.get("allocation.all.allocated", 0)
+            fails = st.get("num_alloc_retries", 0) + st.get("num_ooms", 0)
+            prev = getattr(self, "_alloc_prev", (0, 0))
+            out["alloc_success"], out["alloc_fail"] = allocs - prev[0], fails - prev[1]
+            self._alloc_prev = (allocs, fails)
+        if self.mailbox is not None:
+            ms = self.mailbox.stats()
+            out.update(msgs_sent=ms.msgs_sent, msgs_recv=ms.msgs_recv, bytes_sent=ms.bytes_sent,
+                       bytes_recv=ms.bytes_recv)
+        return out
+
     def timeline_start_step(self, step):
         if self.watchdog is not None:
             self.watchdog.step_started()

@@ -13,6 +13,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.layernorm import add_layer_norm, layer_norm, layer_norm_passthrough
+from ..parallel.throttle import throttler
 from .utils import get_local_channels, get_start_pos_for_slicing, tp_group, tp_size
 
 
@@ -77,11 +78,13 @@ class _DistLNStats(torch.autograd.Function):
         xf = x.float()
         s1 = xf.sum(-1, keepdim=True)
         if group is not None:
-            dist.all_reduce(s1, group=group)
+            with throttler().throttle(s1):
+                dist.all_reduce(s1, group=group)
         mean = s1 / full_dim
         s2 = (xf - mean).pow(2).sum(-1, keepdim=True)
         if group is not None:
-            dist.all_reduce(s2, group=group)
+            with throttler().throttle(s2):
+                dist.all_reduce(s2, group=group)
         var = s2 / full_dim
         ctx.save_for_backward(xf, mean)
         ctx.full_dim, ctx.group = full_dim, group
@@ -94,7 +97,8 @@ class _DistLNStats(torch.autograd.Function):
         if ctx.group is not None:
             # every rank's local y depends on the shared statistics: sum their grads
             g = torch.cat([gmean, gvar], dim=-1).contiguous()
-            dist.all_reduce(g, group=ctx.group)
+            with throttler().throttle(g):
+                dist.all_reduce(g, group=ctx.group)
             gmean, gvar = g[..., :1], g[..., 1:]
         # d mean / dx = 1/n ; d var / dx = 2 (x - mean) / n  (the mean term sums to zero)
         gx = gmean / n + gvar * 2.0 * (xf - mean) / n

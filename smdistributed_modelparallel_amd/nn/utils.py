@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ..torch.state_mod import state
+from ..parallel.throttle import throttler
 
 
 # --------------------------------------------------------------------- topology
@@ -72,7 +73,8 @@ def _allgather(x, dim, sizes=None):
     mx = max(sizes)
     xp = _pad_to(x, dim, mx).movedim(dim, 0).contiguous()
     out = xp.new_empty((ws * mx,) + tuple(xp.shape[1:]))
-    dist.all_gather_into_tensor(out, xp, group=group)
+    with throttler().throttle(xp):
+        dist.all_gather_into_tensor(out, xp, group=group)
     if any(s != mx for s in sizes):
         out = torch.cat([p[:s] for p, s in zip(out.split(mx, dim=0), sizes)], dim=0)
     return out.movedim(0, dim).contiguous() if dim != 0 else out
@@ -92,7 +94,8 @@ def _reduce_scatter(x, dim, sizes=None):
     padded = [_pad_to(p, dim, mx).movedim(dim, 0) for p in parts]
     inp = torch.cat(padded, dim=0).contiguous()
     out = inp.new_empty((mx,) + tuple(inp.shape[1:]))
-    dist.reduce_scatter_tensor(out, inp, group=group)
+    with throttler().throttle(inp):
+        dist.reduce_scatter_tensor(out, inp, group=group)
     out = out[: sizes[tp_rank()]]
     return out.movedim(0, dim).contiguous()
 
@@ -101,7 +104,8 @@ def _allreduce(x):
     if tp_size() == 1:
         return x
     x = x.contiguous()
-    dist.all_reduce(x, group=tp_group())
+    with throttler().throttle(x):
+        dist.all_reduce(x, group=tp_group())
     return x
 
 
@@ -138,7 +142,8 @@ def _all_to_all(x, split_dim, merge_dim, split_sizes=None, merge_sizes=None):
     # each received piece r has this rank's split slice and rank r's merge extent
     group = tp_group()
     if x.is_cuda:
-        dist.all_to_all(outs, pieces, group=group)  # RCCL all-to-all over xGMI
+        with throttler().throttle(x):
+            dist.all_to_all(outs, pieces, group=group)  # RCCL all-to-all over xGMI
     else:
         # gloo has no all-to-all: pairwise exchange
         ops = []

@@ -42,14 +42,17 @@ class StepMemoryMetricsCollector:
             return
         if self.path is None:
             self.path = f"smp_step_memory_metrics_rank{state.core.rank()}.txt"
-        dev = state.device
+        core = state.core
+        mem = core.get_and_reset_memory_metrics()  # resets the peaks
+        alloc = core.get_and_reset_alloc_metrics()
         line = (
-            f"step={step} peak_allocated_MB={torch.cuda.max_memory_allocated(dev) / 2**20:.1f} "
-            f"peak_reserved_MB={torch.cuda.max_memory_reserved(dev) / 2**20:.1f}"
+            f"step={step} peak_allocated_MB={mem['d2d_peak_allocated_mb']:.1f} "
+            f"peak_reserved_MB={mem['d2d_peak_reserved_mb']:.1f} gpu_free_MB={mem['gpu_free_mb']:.1f} "
+            f"gpu_total_MB={mem['gpu_total_mb']:.1f} alloc_success={alloc['alloc_success']} "
+            f"alloc_fail={alloc['alloc_fail']}"
         )
         with open(self.path, "a") as f:
             f.write(line + "\n")
-        torch.cuda.reset_peak_memory_stats(dev)
 
 
 class StepFunction:
