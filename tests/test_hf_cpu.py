@@ -146,3 +146,40 @@ def test_gelu_selection_follows_reference():
     finally:
         if old is not None:
             os.environ["SMP_USE_HF_GELU"] = old
+
+
+def test_vit_layer_parity():
+    """HF ViT (transformers 5.x: ViTModel.layers of ViTLayer) with every layer replaced by a
+    DistributedTransformerLayer through the registry hooks reproduces the HF outputs;
+    state-dict translation round-trips (reference `smp/torch/nn/huggingface/vit.py`)."""
+    import copy
+
+    from transformers import ViTConfig, ViTModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import vit
+    from smdistributed_modelparallel_amd.torch.tp_registry import TensorParallelismRegistry
+
+    reg = TensorParallelismRegistry()
+    vit.register_vit(reg)
+    try:
+        torch.manual_seed(0)
+        cfg = ViTConfig(hidden_size=64, num_hidden_layers=3, num_attention_heads=4, intermediate_size=128,
+                        image_size=32, patch_size=8, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+        hf = ViTModel(cfg).eval()
+        smp_model = copy.deepcopy(hf)
+        hf_sd = hf.state_dict()
+        for i, layer in enumerate(list(smp_model.layers)):
+            smp_model.layers[i] = reg.distribute(layer)
+        missing, unexpected = smp_model.load_state_dict(vit.hf_to_smp(hf_sd), strict=True)
+        assert not missing and not unexpected
+        px = torch.randn(2, 3, 32, 32)
+        with torch.no_grad():
+            ref = hf(pixel_values=px).last_hidden_state
+            out = smp_model.eval()(pixel_values=px).last_hidden_state
+        assert torch.allclose(out, ref, atol=2e-5), (out - ref).abs().max()
+        back = vit.smp_to_hf(smp_model.state_dict())
+        assert set(back) == set(hf_sd)
+        for k, v in hf_sd.items():
+            assert torch.equal(back[k], v), k
+    finally:
+        reg.unpatch()
