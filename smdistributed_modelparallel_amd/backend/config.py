@@ -18,7 +18,7 @@ import os
 
 import yaml
 
-from .exceptions import SMPConfigError, SMPConfigTypeError, SMPInvalidArgumentError
+from .exceptions import SMPUnsupportedError, SMPConfigError, SMPConfigTypeError, SMPInvalidArgumentError
 from .logger import get_logger
 
 logger = get_logger()
@@ -134,6 +134,15 @@ class ModelParallelConfig:
             logger.info(
                 "Simple pipeline requires active_microbatches == microbatches; using interleaved pipeline."
             )
+        if self.herring:
+            # reference: the herring reducer raises SMPUnsupportedError (`torch/allreduce/herring.py:35-39`)
+            raise SMPUnsupportedError("herring is not supported; use ddp: True (RCCL over xGMI)")
+        if self.horovod:
+            # the reference's PyTorch Horovod reducer (`torch/allreduce/horovod.py`) has the same
+            # gradient semantics as its DDP reducer; Horovod itself is not part of this stack
+            logger.warning("horovod: True -- data parallelism runs on the native RCCL reducer (as ddp: True)")
+            self.ddp = True
+            values["ddp"] = True
         if self.pipeline_parallel_degree > 1 and self.checkpoint_attentions:
             logger.warning("Attention checkpointing is disabled when pipeline_parallel_degree > 1.")
             self.checkpoint_attentions = False

@@ -88,6 +88,8 @@ class TensorParallelismRegistry:
                 if accepted is None or k in accepted:
                     kwargs[k] = v
         dist_mod = e.dist_cls(*args, **kwargs)
+        if _match_weights_enabled():
+            match_weights(module, dist_mod, e.translate_functions)
         if e.translate_functions is not None and e.translate_functions not in self.translate_functions:
             self.translate_functions.append(e.translate_functions)
         if e.forward_hook is not None or e.return_hook is not None:
@@ -103,6 +105,42 @@ class TensorParallelismRegistry:
             dist_mod.forward = wrapped
         dist_mod.training = module.training
         return dist_mod
+
+
+def _match_weights_enabled():
+    from .state_mod import state
+
+    return state.cfg is not None and bool(getattr(state.cfg, "_match_weights", False))
+
+
+def match_weights(module, dist_mod, translate_functions=None):
+    """``_match_weights`` (reference `tp_registry.py:47-161,237-242`): give the distributed
+    module this rank's slices of the original module's weights, so a TP model starts
+    numerically identical to the model the user constructed.  The original state dict is
+    mapped into the distributed module's key space by its hf_to_smp translator (identity
+    for nn.Linear / nn.Embedding) and sliced per parameter by its TP layout."""
+    import torch
+
+    from .checkpoint_utils import slice_for_param
+    from .state_mod import state
+
+    sd = module.state_dict()
+    if translate_functions is not None and translate_functions[1] is not None:
+        sd = translate_functions[1](sd)
+    tp_r, tp_n = state.core.tp_rank(), state.core.tp_size()
+    matched = 0
+    with torch.no_grad():
+        for n, p in dist_mod.named_parameters():
+            full = sd.get(n)
+            if full is None or p.numel() == 0:
+                continue
+            t = slice_for_param(full, p, tp_r, tp_n)
+            if tuple(t.shape) != tuple(p.shape):
+                raise ValueError(f"_match_weights: {n}: slice {tuple(t.shape)} != parameter {tuple(p.shape)}")
+            p.copy_(t)
+            matched += 1
+    logger.debug(f"_match_weights: copied {matched} parameters into {type(dist_mod).__name__}")
+    return matched
 
 
 def _accepted_kwargs(cls):

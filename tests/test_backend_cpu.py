@@ -386,3 +386,13 @@ def test_native_grad_counter():
     assert gc.is_grad_ready("b")
     gc.clear_minibatch_state()
     assert gc.get_seen_grad_count("w") == 0
+
+
+def test_config_legacy_dp_backends():
+    from smdistributed_modelparallel_amd.backend.config import ModelParallelConfig
+    from smdistributed_modelparallel_amd.backend.exceptions import SMPUnsupportedError
+
+    with pytest.raises(SMPUnsupportedError):
+        ModelParallelConfig({"herring": True})
+    c = ModelParallelConfig({"horovod": True})
+    assert c.ddp and c.horovod  # Horovod configs run on the native RCCL reducer

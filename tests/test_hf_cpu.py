@@ -119,6 +119,9 @@ def test_encoder_parity(family):
 def test_hf_gpt2_auto_tp2_matches_hf():
     outs = run_workers("hf_gpt2_tp", 2, [], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
     assert all("OK" in o for o in outs)
+    # _match_weights: no explicit load -- the replaced modules start from the HF weights
+    outs = run_workers("hf_gpt2_tp", 2, ["match"], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
+    assert all("OK" in o for o in outs)
 
 
 def test_gelu_selection_follows_reference():

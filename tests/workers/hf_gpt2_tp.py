@@ -10,16 +10,22 @@ from smdistributed_modelparallel_amd.nn.huggingface import gpt2
 
 
 def main():
+    import sys
+
+    match = len(sys.argv) > 1 and sys.argv[1] == "match"
     cfg = GPT2Config(n_layer=2, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0,
                      resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
     torch.manual_seed(0)
     ref = GPT2LMHeadModel(cfg)
-    smp.init({"tensor_parallel_degree": 2, "ddp": True})
+    smp.init({"tensor_parallel_degree": 2, "ddp": True, "_match_weights": match})
+    torch.manual_seed(0)
     with smp.model_creation(tensor_parallelism=True):
-        net = GPT2LMHeadModel(cfg)
+        net = GPT2LMHeadModel(cfg)  # same seed: the same initial weights as ref
     model = smp.DistributedModel(net)
     assert isinstance(model.get_module(), DistributedTransformerLMHead), type(model.get_module())
-    model.load_state_dict(ref.state_dict(), translate_function=gpt2.hf_to_smp)
+    if not match:
+        model.load_state_dict(ref.state_dict(), translate_function=gpt2.hf_to_smp)
+    # (match: _match_weights already gave every TP rank its slices of the HF weights)
     opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1))
     ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
 
