@@ -174,6 +174,16 @@ class _Dropout(nn.Module):
         return F.dropout(x, self.p, True)
 
 
+class _LMHeadLinear(nn.Linear):
+    """nn.Linear (same parameters / state-dict keys) whose forward goes through
+    ``ops.linear``: the [V, h] weight gradient is accumulated by the GEMM into the flat
+    buffer (no 160 MB temporary + add for GPT-2 XL) and the input gradient runs in the
+    forward layout against a cached W^T."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)
+
+
 def _normal_init(emb, std):
     """N(0, std) for an nn.Embedding, now and again when delayed parameter initialisation
     materialises it (nn.Embedding.reset_parameters would use N(0, 1))."""
@@ -654,7 +664,7 @@ class DistributedTransformerLMHead(DistributedModule):
             if self.distribute_embedding:
                 self.lm_head_weight_local = None  # tied to the vocab-parallel embedding shard
             else:
-                self.lm_head = nn.Linear(h, self.vocab_size, bias=self.use_lm_head_bias, dtype=dtype)
+                self.lm_head = _LMHeadLinear(h, self.vocab_size, bias=self.use_lm_head_bias, dtype=dtype)
                 if self.tie_input_output_embedding:
                     self.lm_head.weight = self.word_embedding.weight
 

@@ -10,6 +10,8 @@ import os
 
 import torch
 
+from ..ops.linear import bump_weight_epoch
+
 from ..backend.exceptions import DistributedModelNotWrappedError, SMPInvalidArgumentError
 from ..backend.logger import get_logger
 from ..backend.split import StepOutput, TensorSplitter
@@ -74,6 +76,7 @@ class StepFunction:
         if state.model is None:
             raise DistributedModelNotWrappedError("the model must be wrapped in smp.DistributedModel before calling an smp.step function")
         state.current_step_fn_id = self.id
+        bump_weight_epoch()  # weights are constant within a step: W^T copies refresh once
         core = state.core
         core.timeline_start_step(state.step_count)
         if state.current_offloader is not None:

@@ -245,6 +245,41 @@ def test_gpt_fused_grad_accumulation_gpu(C, dt):
         assert torch.allclose(q.grad.float(), p.grad.float(), atol=tol, rtol=tol * 5), n
 
 
+def test_transposed_dgrad_gpu(C, monkeypatch):
+    """Input gradients computed against the cached W^T (forward GEMM layout) equal
+    autograd's; the cache refreshes when the weight epoch advances."""
+    import smdistributed_modelparallel_amd.ops.linear as L
+    from smdistributed_modelparallel_amd.models import build_gpt
+
+    monkeypatch.setattr(L, "_use_transposed", lambda w: w.is_cuda and w.dim() == 2)
+    torch.manual_seed(13)
+    kw = dict(dropout=0.0, hidden_size=128, num_attention_heads=2, attention_head_size=64, intermediate_size=512)
+    ref = build_gpt("gpt2-tiny", **kw).cuda()
+    fused = build_gpt("gpt2-tiny", **kw).cuda()
+    fused.load_state_dict(ref.state_dict())
+    for p in fused.parameters():
+        p.grad = torch.zeros_like(p)
+        p._smp_fused_grad = True
+    ids = torch.randint(0, 512, (2, 64), device="cuda")
+    for step in range(2):
+        L.bump_weight_epoch()
+        for m in (ref, fused):
+            m.zero_grad(set_to_none=(m is ref))
+            loss, _ = m((ids, None, None, None, ids))
+            loss.backward()
+        for (n, p), (_, q) in zip(ref.named_parameters(), fused.named_parameters()):
+            assert torch.allclose(q.grad, p.grad, atol=2e-4, rtol=1e-3), (step, n)
+        with torch.no_grad():  # an "optimizer step" on both: W^T must follow
+            for p, q in zip(ref.parameters(), fused.parameters()):
+                p.add_(p.grad, alpha=-0.5)
+                q.add_(q.grad, alpha=-0.5)
+    w = fused.transformer.seq_layers[0].output.dense1_weight
+    assert not torch.equal(w.__dict__["_smp_wt"][1], w.detach().t())  # lazily refreshed on next use
+    L.bump_weight_epoch()
+    fused((ids, None, None, None, ids))
+    assert torch.equal(w.__dict__["_smp_wt"][1], w.detach().t())
+
+
 def test_layer_norm_passthrough_gpu(C):
     from smdistributed_modelparallel_amd.ops.layernorm import layer_norm_passthrough
 
