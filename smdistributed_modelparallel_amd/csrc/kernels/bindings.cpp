@@ -278,6 +278,19 @@ std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Ten
   return {dx, db};
 }
 
+// -------------------------------------------------------------------- transpose
+// dst <- src^T for a contiguous 2-D src; dst must be a contiguous [cols, rows] tensor.
+at::Tensor transpose_into(at::Tensor src, at::Tensor dst) {
+  check_gpu(src, "src");
+  check_gpu(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && src.is_contiguous() && dst.is_contiguous(), "transpose_into: contiguous 2-D tensors");
+  TORCH_CHECK(dst.size(0) == src.size(1) && dst.size(1) == src.size(0) && dst.scalar_type() == src.scalar_type(),
+              "transpose_into: dst must be [cols, rows] of src's dtype");
+  check(smpk::transpose2d(dt_code(src), src.data_ptr(), dst.data_ptr(), src.size(0), src.size(1), stream()),
+        "transpose2d");
+  return dst;
+}
+
 // ------------------------------------------------------------------------ rope
 at::Tensor rope_apply(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, int64_t rotary_dim, bool neox, bool inverse,
                       int64_t pos_offset) {
@@ -465,6 +478,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layernorm_apply_stats", &layernorm_apply_stats);
   m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("bias"), py::arg("exact") = false);
   m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("exact") = false);
+  m.def("transpose_into", &transpose_into);
   m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
   m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),

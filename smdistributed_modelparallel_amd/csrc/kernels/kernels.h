@@ -70,6 +70,10 @@ int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias,
                         float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate = false,
                         bool exact = false);
 
+// ------------------------------------------------------------- transpose (transpose.hip)
+// dst[cols][rows] = src[rows][cols] (row-major, contiguous).
+int transpose2d(int dt, const void* src, void* dst, int64_t rows, int64_t cols, hipStream_t s);
+
 // --------------------------------------------------------------- softmax (softmax.hip)
 int scaled_masked_softmax_fwd(int dt, const void* x, const uint8_t* mask, void* y, int64_t batch, int64_t heads,
                               int64_t sq, int64_t sk, int64_t mask_batch, float scale, hipStream_t s);

@@ -46,7 +46,11 @@ def _transposed(w):
     buf = ent[1] if ent is not None and ent[1].dtype == w.dtype and ent[1].shape == (w.shape[1], w.shape[0]) else None
     with torch.no_grad():
         if buf is None:
-            buf = w.detach().t().contiguous()
+            buf = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+        if w.is_cuda and w.is_contiguous():
+            from ._ext import ext
+
+            ext().transpose_into(w.detach(), buf)  # LDS-tiled HIP transpose (HBM rate)
         else:
             buf.copy_(w.detach().t())
     w.__dict__["_smp_wt"] = (key, buf)

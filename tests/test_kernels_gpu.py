@@ -280,6 +280,15 @@ def test_transposed_dgrad_gpu(C, monkeypatch):
     assert torch.equal(w.__dict__["_smp_wt"][1], w.detach().t())
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("shape", [(6400, 1600), (1600, 4800), (64, 64), (100, 37), (3, 1000), (1000, 72)])
+def test_transpose_kernel(C, dt, shape):
+    x = torch.randn(*shape, device="cuda").to(dt)
+    out = torch.empty(shape[1], shape[0], device="cuda", dtype=dt)
+    C.transpose_into(x, out)
+    assert torch.equal(out, x.t())
+
+
 def test_layer_norm_passthrough_gpu(C):
     from smdistributed_modelparallel_amd.ops.layernorm import layer_norm_passthrough
 

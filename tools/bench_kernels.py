@@ -84,6 +84,10 @@ def bench_memory_bound():
         res[f"col_sum_32768x{cols}_GBps"] = xc.numel() * 2 / t / 1e6
         res[f"col_sum_32768x{cols}_us"] = t * 1e3
     del xg
+    w = torch.randn(6400, 1600, device="cuda", dtype=torch.bfloat16)
+    wt = torch.empty(1600, 6400, device="cuda", dtype=torch.bfloat16)
+    t = timeit(lambda: C.transpose_into(w, wt))
+    res["transpose_6400x1600_GBps"] = 2 * w.numel() * 2 / t / 1e6
     n = 200_000_000
     p = torch.randn(n, device="cuda", dtype=torch.bfloat16)
     gr = torch.randn(n, device="cuda", dtype=torch.bfloat16)
