@@ -46,7 +46,7 @@ class BucketReducer:
         self._hooks = []
         self._launched_any = False
         self.group_rank = dist.get_rank(group) if (group is not None and dist.is_initialized()) else 0
-        if overlap:
+        if overlap or flat.fp32_accumulation:
             self._install_hooks()
 
     # ------------------------------------------------------------------ hooks
@@ -61,6 +61,8 @@ class BucketReducer:
         self._hooks.clear()
 
     def _on_grad(self, p):
+        if self.flat.fp32_accumulation:
+            self.flat.fold_grad(p)  # every microbatch: low-precision grad -> fp32 main_grad
         if not (self.final and self.sync_enabled):
             return
         b = self.flat.bucket_of.get(p)
@@ -112,6 +114,9 @@ class BucketReducer:
 
     def synchronize(self):
         """Launch whatever is left (unused params / non-overlapped mode) and wait."""
+        if self.flat.fp32_accumulation:
+            for p in self.flat.params():
+                self.flat.fold_grad(p)
         if not self.sync_enabled:
             return
         for b in self.flat.buckets:

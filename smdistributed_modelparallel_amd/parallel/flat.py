@@ -116,14 +116,37 @@ class FlatParamGroup:
         o = self.offsets[p]
         return buf[o : o + p.numel()].view(p.shape)
 
+    @property
+    def fp32_accumulation(self):
+        """Gradient buffer wider than the parameters (``_fp32_grad_accumulation``): each
+        microbatch's low-precision gradient lands in ``param.grad`` and is folded into the
+        fp32 ``param.main_grad`` view by the reducer's hook."""
+        return self.grad_dtype != self.dtype
+
     def bind(self):
-        """Point every param's .data and .grad at the flat buffers."""
+        """Point every param's .data and .grad (or .main_grad) at the flat buffers."""
         for p in self.offsets:
             p.data = self.view(p, self.data)
-            p.grad = self.view(p, self.grad)
-            p._smp_fused_grad = True  # ops.linear may accumulate dW straight into the view
+            if self.fp32_accumulation:
+                p.grad = None
+                p.main_grad = self.view(p, self.grad)
+                p._smp_fused_grad = False
+            else:
+                p.grad = self.view(p, self.grad)
+                p._smp_fused_grad = True  # ops.linear may accumulate dW straight into the view
+
+    def fold_grad(self, p):
+        """main_grad += grad (fp32 accumulation); frees the low-precision grad."""
+        g = p.grad
+        if g is not None:
+            p.main_grad.add_(g)
+            p.grad = None
 
     def rebind_grads(self):
+        if self.fp32_accumulation:
+            for p in self.offsets:
+                self.fold_grad(p)
+            return
         base, es = self.grad.data_ptr(), self.grad.element_size()
         for p, o in self.offsets.items():
             g = p.grad

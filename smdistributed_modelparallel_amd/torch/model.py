@@ -40,6 +40,24 @@ def _is_scaled_batch(p):
     return getattr(p, "_smp_scaled_batch", False)
 
 
+def _compress_hook(dt):
+    """Bucket all-reduce in a narrower dtype (torch DDP's fp16/bf16 compress hooks; the
+    reference's fp32-grad-accumulation hook): cast, all-reduce, copy back on wait."""
+
+    def compress(b, buf, group):
+        tmp = buf.to(dt)
+        w = dist.all_reduce(tmp, group=group, async_op=True)
+
+        class _W:
+            def wait(self_inner):
+                w.wait()
+                buf.copy_(tmp)
+
+        return _W()
+
+    return compress
+
+
 class DistributedModel(nn.Module):
     def __init__(
         self,
@@ -282,12 +300,17 @@ class DistributedModel(nn.Module):
             if len(dtypes) != 1:
                 raise SMPInvalidArgumentError(f"mixed parameter dtypes {dtypes} are not supported in one model")
             dtype = dtypes.pop()
+            fp32_acc = bool(cfg._fp32_grad_accumulation) and dtype in (torch.float16, torch.bfloat16)
             flat = FlatParamGroup(members, device, dtype, cap, _FIRST_BUCKET_BYTES, align=64 * max(1, gsize),
-                                  segments=segments)
+                                  segments=segments, grad_dtype=torch.float32 if fp32_acc else None)
             self.flat_groups[key] = flat
+            hook = self._comm_hook
+            if fp32_acc and hook is None:
+                # reference `ddp_model.py:188-229`: fp32-accumulated buckets travel as fp16
+                hook = _compress_hook(torch.float16)
             self.reducers[key] = BucketReducer(flat, group if gsize > 1 else None, gsize, divisor,
                                                overlap=self.overlapping_allreduce, shard=shard,
-                                               comm_hook=self._comm_hook, name=key)
+                                               comm_hook=hook, name=key)
 
     def _build_sharded_dp(self):
         from ..parallel.sharded_dp import ShardedDataParallel, _NoReducer
@@ -529,19 +552,7 @@ class DistributedModel(nn.Module):
     def _register_builtin_comm_hook(self, comm_hook_type):
         name = str(comm_hook_type)
         if "FP16" in name.upper() or "BF16" in name.upper():
-            dt = torch.bfloat16 if "BF16" in name.upper() else torch.float16
-
-            def compress(b, buf, group):
-                tmp = buf.to(dt)
-                w = dist.all_reduce(tmp, group=group, async_op=True)
-
-                class _W:
-                    def wait(self_inner):
-                        w.wait()
-                        buf.copy_(tmp)
-
-                return _W()
-
+            compress = _compress_hook(torch.bfloat16 if "BF16" in name.upper() else torch.float16)
             self._comm_hook = compress
             for r in self.reducers.values():
                 r.comm_hook = compress

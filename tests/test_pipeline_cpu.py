@@ -139,3 +139,8 @@ def test_pp2_delayed_parameter_initialization(auto):
 
 def test_dp2_delayed_parameter_initialization():
     _run(2, 1, 1, 2, extra={"delayed": True, "cfg": {"delayed_parameter_initialization": True}})
+
+
+def test_dp2_fp16_fp32_grad_accumulation():
+    outs = run_workers("fp32_accum", 2, [], timeout=200)
+    assert all("OK" in o for o in outs)
