@@ -255,6 +255,107 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
   }
 }
 
+// Backward, block-per-row-group form for rows of <= 256 (VB=1) or 512 (VB=2) 16-byte
+// vectors (e.g. hidden 1600 / 4096 in bf16): the 256 threads of a block share each row
+// (thread t owns vectors t and t+256), so a thread's dgamma/dbeta accumulators cover only
+// its own columns for all the block's rows -- 8*VB floats each instead of a wave's whole
+// row -- and need no LDS combine: the block writes its fp32 partial row directly.  Row
+// sums go through one LDS exchange per row (double-buffered: one barrier per row); the
+// next row's x / dy / dres vectors are loaded before the current row's reduction.
+// Low register use (high occupancy) is what the one-wave-per-row kernel lacked at 1600.
+template <typename T, typename W, int VB>
+__global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, const T* __restrict__ x,
+                                                  const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                  const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                  float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                  int64_t rows, int cols, const T* __restrict__ dres,
+                                                  int64_t rows_per_block) {
+  constexpr int N = Vec16<T>::N;
+  __shared__ float red[2][2][4];  // [parity][s1|s2][wave]
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int nvec = cols / N;
+  float wv[VB][N], dwacc[VB][N], dbacc[VB][N];
+  bool act[VB];
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    const int v = t + 256 * k;
+    act[k] = v < nvec;
+    if (act[k] && w != nullptr) {
+      load_wn<W, N>(w + v * N, wv[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; ++j) wv[k][j] = 1.f;
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) dwacc[k][j] = dbacc[k][j] = 0.f;
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  Vec16<T> xa[VB], da[VB], ra[VB];
+  auto load_row = [&](int64_t row) {
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+      if (act[k]) {
+        const int64_t off = row * cols + static_cast<int64_t>(t + 256 * k) * N;
+        xa[k] = load16(x + off);
+        da[k] = load16(dy + off);
+        if (dres != nullptr) ra[k] = load16(dres + off);
+      }
+    }
+  };
+  if (r0 < r1) load_row(r0);
+  int parity = 0;
+  for (int64_t row = r0; row < r1; ++row) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[VB][N], g[VB][N], rr[VB][N];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float dyv = act[k] ? to_f32(da[k].v[j]) : 0.f;
+        xh[k][j] = act[k] ? (to_f32(xa[k].v[j]) - mean) * rstd : 0.f;
+        rr[k][j] = (act[k] && dres != nullptr) ? to_f32(ra[k].v[j]) : 0.f;
+        g[k][j] = dyv * wv[k][j];
+        s1 += g[k][j];
+        s2 += g[k][j] * xh[k][j];
+        dwacc[k][j] += dyv * xh[k][j];
+        dbacc[k][j] += dyv;
+      }
+    }
+    if (row + 1 < r1) load_row(row + 1);  // prefetch under the reduction
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      red[parity][0][wid] = s1;
+      red[parity][1][wid] = s2;
+    }
+    __syncthreads();
+    s1 = (red[parity][0][0] + red[parity][0][1] + red[parity][0][2] + red[parity][0][3]) / cols;
+    s2 = (red[parity][1][0] + red[parity][1][1] + red[parity][1][2] + red[parity][1][3]) / cols;
+    parity ^= 1;
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+      if (!act[k]) continue;
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(rstd * (g[k][j] - s1 - xh[k][j] * s2) + rr[k][j]);
+      store16(dx + row * cols + static_cast<int64_t>(t + 256 * k) * N, o);
+    }
+  }
+  if (dw_part == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    if (!act[k]) continue;
+    const int64_t c = static_cast<int64_t>(t + 256 * k) * N;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      dw_part[static_cast<int64_t>(blockIdx.x) * cols + c + j] = dwacc[k][j];
+      if (db_part) db_part[static_cast<int64_t>(blockIdx.x) * cols + c + j] = dbacc[k][j];
+    }
+  }
+}
+
 template <typename T, typename W>
 __global__ void __launch_bounds__(256) ln_bwd_stream(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ w, const float* __restrict__ mean_in,
@@ -415,7 +516,13 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
       const T* dr = static_cast<const T*>(dres);
       const int c = static_cast<int>(cols);
       const size_t lds = static_cast<size_t>(2 * kRowsPerBlock) * cols * sizeof(float);
-      if (reg && vpt <= 1) {
+      const int64_t nvec = cols / N;
+      const int64_t rpb = (rows + parts - 1) / parts;
+      if (reg && nvec <= 256 && nvec >= 128) {
+        ln_bwd_blk<T, W, 1><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
+      } else if (reg && nvec <= 512 && nvec > 256) {
+        ln_bwd_blk<T, W, 2><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
+      } else if (reg && vpt <= 1) {
         ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
       } else if (reg && vpt <= 2) {
         ln_bwd_reg<T, W, 2><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);

@@ -64,6 +64,15 @@ def bench_memory_bound():
     t = timeit(lambda: layernorm.layer_norm(x, w, bb))
     res["layernorm_fwd_GBps"] = 2 * x.numel() * 2 / t / 1e6
     C = ext()
+    xl = torch.randn(32768, 1600, device="cuda", dtype=torch.bfloat16)
+    dyl = torch.randn_like(xl)
+    wl = torch.randn(1600, device="cuda", dtype=torch.bfloat16)
+    bl = torch.randn(1600, device="cuda", dtype=torch.bfloat16)
+    _, mu, rs = C.layernorm_fwd(xl, None, wl, bl, 1e-5)
+    t = timeit(lambda: C.layernorm_bwd(dyl, xl, wl, mu, rs, True, True, dyl))
+    res["layernorm_bwd_dres_32768x1600_us"] = t * 1e3
+    res["layernorm_bwd_dres_GBps"] = 4 * xl.numel() * 2 / t / 1e6
+    del xl, dyl
     xg = torch.randn(32768, 6400, device="cuda", dtype=torch.bfloat16)
     bg = torch.randn(6400, device="cuda", dtype=torch.bfloat16)
     t = timeit(lambda: gelu.bias_gelu(xg, bg))
