@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--no-flash", action="store_true")
     ap.add_argument("--activation-checkpointing", action="store_true")
     ap.add_argument("--shard-optimizer-state", action="store_true")
+    ap.add_argument("--offload-optimizer-state", action="store_true",
+                    help="fp32 master + Adam moments in pinned host memory (amd_offload_optimizer_state)")
     ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
                     help="hipBLASLt/rocBLAS GEMM solution selection via PyTorch TunableOp: 'use' loads the "
                          "per-shape winners measured on MI355X (configs/tunableop), 'tune' re-measures them "
@@ -103,6 +105,7 @@ def main():
         "bf16": True,
         "amd_fused_attention": not args.no_flash,
         "shard_optimizer_state": args.shard_optimizer_state,
+        "amd_offload_optimizer_state": args.offload_optimizer_state,
     }
     if args.pp > 1:
         cfg["auto_partition"] = True

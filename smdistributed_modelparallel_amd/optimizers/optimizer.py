@@ -56,6 +56,14 @@ class _Domain:
         return self.end - self.start
 
 
+class _Staged:
+    """A domain whose master/m/v are temporarily the HBM staging views."""
+
+    def __init__(self, d, master, m, v):
+        self.key, self.start, self.end, self.group_index, self.params = d.key, d.start, d.end, d.group_index, d.params
+        self.master, self.m, self.v, self.upd, self.vparam = master, m, v, None, None
+
+
 class DistributedOptimizer:
     def __init__(self, optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None):
         if state.model is None:
@@ -84,6 +92,10 @@ class DistributedOptimizer:
         self._clip_coef = None
         self._built = False
         self.overflow = False
+        self.offload = bool(getattr(cfg, "amd_offload_optimizer_state", False)) and state.use_gpu
+        if self.offload and self.kind not in ("adam", "adamw", "sgd", "adagrad"):
+            raise SMPInvalidArgumentError("amd_offload_optimizer_state supports Adam/AdamW/SGD/Adagrad")
+        self._offload = None
         state.optimizer = self
         if model.partitioned:
             self._on_model_partitioned()
@@ -144,21 +156,31 @@ class DistributedOptimizer:
                     s, e = b.start, b.end
                 d = _Domain(key, s, e, gi, b.params)
                 dev = flat.data.device
-                if lowp or flat.data.dtype != torch.float32:
+                if self.offload:
+                    # pinned host copies; the low-precision params stay in HBM
+                    dev = torch.device("cpu")
+                    d.master = torch.empty(e - s, dtype=torch.float32, pin_memory=True)
+                    d.master.copy_(flat.data[s:e].float())
+                elif lowp or flat.data.dtype != torch.float32:
                     d.master = flat.data[s:e].float().clone()
                 else:
                     d.master = flat.data[s:e]  # fp32 model: the parameters are the master copy
+                pin = self.offload
                 if self.kind in ("adam", "adamw", "lamb"):
-                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev)
-                    d.v = torch.zeros(e - s, dtype=torch.float32, device=dev)
+                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
+                    d.v = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
                 elif self.kind in ("sgd",):
-                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev)
+                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
                 elif self.kind == "adagrad":
                     init = self.optimizer.param_groups[gi].get("initial_accumulator_value", 0.0)
-                    d.v = torch.full((e - s,), float(init), dtype=torch.float32, device=dev)
+                    d.v = torch.full((e - s,), float(init), dtype=torch.float32, device=dev, pin_memory=pin)
                 if self.kind == "lamb":
                     d.upd = torch.empty(e - s, dtype=torch.float32, device=dev)
                 self.domains.append(d)
+        if self.offload:
+            from .offload import OptimizerStateOffload
+
+            self._offload = OptimizerStateOffload(self.domains, state.device)
         if self.kind == "generic":
             # inner optimizer sees fp32 virtual parameters (one per domain)
             groups = [[] for _ in self.optimizer.param_groups]
@@ -253,6 +275,8 @@ class DistributedOptimizer:
             self._step_count[gi] += 1
         if self.kind == "generic":
             self._generic_step(gscale, lowp)
+        elif self._offload is not None:
+            self._offload.run(self.domains, lambda d, st: self._fused_step(d, gscale, lowp, st))
         else:
             for d in self.domains:
                 self._fused_step(d, gscale, lowp)
@@ -262,7 +286,11 @@ class DistributedOptimizer:
     def _hp(self, gi):
         return self.optimizer.param_groups[gi]
 
-    def _fused_step(self, d, gscale, lowp):
+    def _fused_step(self, d, gscale, lowp, staged=None):
+        """One fused update of domain d; ``staged`` = HBM (master, m, v) copies when the
+        optimizer state lives in host memory (`optimizers/offload.py`)."""
+        if staged is not None:
+            d = _Staged(d, *staged)
         g = self._hp(d.group_index)
         step = self._step_count[d.group_index]
         grad = self._grad_range(d)
@@ -316,6 +344,8 @@ class DistributedOptimizer:
 
     # ----------------------------------------------------------- state dicts
     def local_optimizer_state_dict(self):
+        if self._offload is not None:
+            self._offload.wait()  # host copies of the last step are complete
         return {
             "kind": self.kind,
             "domains": [
@@ -349,7 +379,8 @@ class DistributedOptimizer:
                     t.copy_(s[k].to(t.device))
             lowp = self.fp16 or self.bf16
             if lowp:
-                mt.cast_copy_(d.master, self._param_range(d))
+                src = d.master.to(self._param_range(d).device, non_blocking=False)
+                mt.cast_copy_(src, self._param_range(d))
         self._step_count = list(sd.get("step_count", self._step_count))
         for g, saved in zip(self.optimizer.param_groups, sd.get("param_groups", [])):
             for k, v in saved.items():

@@ -59,3 +59,49 @@ print("METRICS_OK")
     lines = open(tmp_path / "smp_step_memory_metrics_rank0.txt").read().splitlines()
     assert len(lines) == 3
     assert all("peak_allocated_MB=" in l and "gpu_free_MB=" in l and "alloc_fail=0" in l for l in lines), lines
+
+
+_OFFLOAD_RUN = r"""
+import sys, torch
+import smdistributed_modelparallel_amd.torch as smp
+from smdistributed_modelparallel_amd.models import build_gpt, gpt_inputs
+off = sys.argv[1] == "1"
+smp.init({"bf16": True, "amd_offload_optimizer_state": off})
+torch.manual_seed(0)
+m = smp.DistributedModel(build_gpt("gpt2-tiny", dropout=0.0, num_layers=3))
+opt = smp.DistributedOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=0.1))
+assert (opt._offload is not None) == off
+if off:
+    assert all(d.master.device.type == "cpu" and d.master.is_pinned() for d in opt.domains)
+@smp.step
+def train(model, ids):
+    loss, _ = model((ids, None, None, None, ids))
+    model.backward(loss)
+    return loss
+g = torch.Generator(device="cuda"); g.manual_seed(1)
+losses = []
+for _ in range(4):
+    ids = gpt_inputs(4, 64, 512, smp.state.device, generator=g)[0]
+    opt.zero_grad(); losses.append(float(train(m, ids).reduce_mean())); opt.step()
+sd = opt.local_optimizer_state_dict()
+torch.save({"losses": losses, "params": {n: p.detach().float().cpu() for n, p in m.named_parameters()},
+            "m0": sd["domains"][0]["m"]}, sys.argv[2])
+print("RUN_OK", losses)
+"""
+
+
+def test_optimizer_state_offload_matches_resident(tmp_path):
+    """Optimizer state in pinned host memory, streamed through HBM staging per domain:
+    bitwise the same training trajectory as the resident optimizer."""
+    outs = []
+    for off in ("0", "1"):
+        f = tmp_path / f"r{off}.pt"
+        r = subprocess.run([sys.executable, "-c", _OFFLOAD_RUN, off, str(f)], cwd=ROOT, capture_output=True,
+                           text=True, timeout=180, env=dict(os.environ, PYTHONPATH=ROOT))
+        assert r.returncode == 0 and "RUN_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+        outs.append(torch.load(f, weights_only=True))
+    a, b = outs
+    assert a["losses"] == b["losses"]
+    for n in a["params"]:
+        assert torch.equal(a["params"][n], b["params"][n]), n
+    assert torch.equal(a["m0"], b["m0"])
