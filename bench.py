@@ -50,6 +50,8 @@ def parse():
 
 
 def tunableop_file(args):
+    if os.environ.get("SMP_TUNABLEOP_FILE"):
+        return os.environ["SMP_TUNABLEOP_FILE"]
     root = os.path.dirname(os.path.abspath(__file__))
     return os.path.join(root, "configs", "tunableop",
                         f"{args.model}_mbs{args.mbs}_s{args.seq}_pp{args.pp}_tp{args.tp}.csv")
@@ -77,6 +79,9 @@ def setup_tunableop(args):
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(20)
         tun.set_max_tuning_iterations(30)
+        # rotate operand copies through > the 256 MB MALL: pick solutions for cold caches,
+        # as in the training step (operands arrive from HBM, not from a hot loop)
+        tun.set_rotating_buffer_size(int(os.environ.get("SMP_TUNABLEOP_ROTATING_MB", "0")))
         tun.set_filename(path, insert_device_ordinal=False)
     return mode
 

@@ -350,29 +350,40 @@ at::Tensor scaled_softmax_bwd(at::Tensor dy, at::Tensor y, double scale) {
 }
 
 // --------------------------------------------------------------- cross entropy
-std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor target, int64_t vocab_start, int64_t ignore_index) {
+// vocab in (0, logits.size(1)): rows of stride logits.size(1) whose first `vocab` columns
+// are valid (64-padded LM head); the backward then zero-fills the padding columns.
+std::vector<at::Tensor> xent_fwd(at::Tensor logits, at::Tensor target, int64_t vocab_start, int64_t ignore_index,
+                                 int64_t vocab) {
   check_gpu(logits, "logits");
   check_gpu(target, "target");
   TORCH_CHECK(logits.dim() == 2 && target.dim() == 1 && target.size(0) == logits.size(0), "xent_fwd: shapes");
+  TORCH_CHECK(logits.is_contiguous(), "xent_fwd: logits must be contiguous");
   TORCH_CHECK(target.scalar_type() == at::kLong, "target must be int64");
-  const int64_t rows = logits.size(0), vocab = logits.size(1);
+  const int64_t rows = logits.size(0), ld = logits.size(1);
+  if (vocab <= 0) vocab = ld;
+  TORCH_CHECK(vocab <= ld, "xent_fwd: vocab exceeds the row length");
   auto fo = logits.options().dtype(at::kFloat);
   auto mx = at::empty({rows}, fo), se = at::empty({rows}, fo), tl = at::empty({rows}, fo);
   check(smpk::xent_fwd_stats(dt_code(logits), logits.data_ptr(), target.data_ptr<int64_t>(), rows, vocab, vocab_start,
-                             mx.data_ptr<float>(), se.data_ptr<float>(), tl.data_ptr<float>(), ignore_index, stream()),
+                             mx.data_ptr<float>(), se.data_ptr<float>(), tl.data_ptr<float>(), ignore_index, stream(),
+                             ld),
         "xent_fwd");
   return {mx, se, tl};
 }
 
 at::Tensor xent_bwd(at::Tensor logits, at::Tensor target, at::Tensor lse, at::Tensor grad_rows, int64_t vocab_start,
-                    int64_t ignore_index) {
+                    int64_t ignore_index, int64_t vocab) {
   check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "xent_bwd: logits must be a contiguous 2-D tensor");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && grad_rows.scalar_type() == at::kFloat, "lse/grad must be fp32");
   TORCH_CHECK(grad_rows.is_contiguous() && lse.is_contiguous(), "lse/grad contiguous");
+  const int64_t ld = logits.size(1);
+  if (vocab <= 0) vocab = ld;
+  TORCH_CHECK(vocab <= ld, "xent_bwd: vocab exceeds the row length");
   auto d = at::empty_like(logits);
   check(smpk::xent_bwd(dt_code(logits), logits.data_ptr(), target.data_ptr<int64_t>(), lse.data_ptr<float>(),
-                       grad_rows.data_ptr<float>(), d.data_ptr(), logits.size(0), logits.size(1), vocab_start,
-                       ignore_index, stream()),
+                       grad_rows.data_ptr<float>(), d.data_ptr(), logits.size(0), vocab, vocab_start, ignore_index,
+                       stream(), ld),
         "xent_bwd");
   return d;
 }
@@ -486,8 +497,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);
   m.def("scaled_upper_triang_softmax_fwd", &scaled_upper_triang_softmax_fwd);
   m.def("scaled_softmax_bwd", &scaled_softmax_bwd);
-  m.def("xent_fwd", &xent_fwd);
-  m.def("xent_bwd", &xent_bwd);
+  m.def("xent_fwd", &xent_fwd, py::arg("logits"), py::arg("target"), py::arg("vocab_start"),
+        py::arg("ignore_index"), py::arg("vocab") = -1);
+  m.def("xent_bwd", &xent_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("grad_rows"),
+        py::arg("vocab_start"), py::arg("ignore_index"), py::arg("vocab") = -1);
   m.def("attention_fwd", &attention_fwd);
   m.def("attention_bwd_into", &attention_bwd_into);
 }

@@ -39,11 +39,11 @@ template <typename T>
 __global__ void __launch_bounds__(256) xent_fwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                        int64_t vocab, int64_t vstart, float* __restrict__ rmax,
                                                        float* __restrict__ rsum, float* __restrict__ rtgt,
-                                                       int64_t ignore) {
+                                                       int64_t ignore, int64_t ld) {
   constexpr int N = Vec16<T>::N;
   __shared__ float sm[8], ss[8];
   const int64_t row = blockIdx.x;
-  const T* x = logits + row * vocab;
+  const T* x = logits + row * ld;
   MaxSum acc{-INFINITY, 0.f};
   // head until 16-byte aligned
   const int64_t mis = (reinterpret_cast<uintptr_t>(x) & 15) / sizeof(T);
@@ -85,15 +85,17 @@ template <typename T>
 __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ logits, const int64_t* __restrict__ tgt,
                                                        const float* __restrict__ lse, const float* __restrict__ g,
                                                        T* __restrict__ dl, int64_t vocab, int64_t vstart,
-                                                       int64_t ignore) {
+                                                       int64_t ignore, int64_t ld) {
   constexpr int N = Vec16<T>::N;
   const int64_t row = blockIdx.x;
   const int64_t t = tgt[row];
   const float gr = (t == ignore) ? 0.f : g[row];
   const float l = lse[row];
   const int64_t tl = t - vstart;  // local target column (may be out of range)
-  const T* x = logits + row * vocab;
-  T* d = dl + row * vocab;
+  const T* x = logits + row * ld;
+  T* d = dl + row * ld;
+  // padding columns of a row stride ld > vocab (64-padded LM head): zero gradient
+  for (int64_t c = vocab + threadIdx.x; c < ld; c += 256) d[c] = from_f32<T>(0.f);
   const int64_t mis = (reinterpret_cast<uintptr_t>(x) & 15) / sizeof(T);
   const bool same_align = ((reinterpret_cast<uintptr_t>(x) ^ reinterpret_cast<uintptr_t>(d)) & 15) == 0;
   auto one = [&](int64_t c) {
@@ -123,24 +125,30 @@ __global__ void __launch_bounds__(256) xent_bwd_kernel(const T* __restrict__ log
 
 }  // namespace
 
+// ld: row stride in elements (>= vocab; 0 = vocab).  Rows beyond `vocab` are padding that
+// the forward ignores and the backward zero-fills (64-padded LM head, ops/lm_head.py).
 int xent_fwd_stats(int dt, const void* logits, const int64_t* target, int64_t rows, int64_t vocab, int64_t vocab_start,
-                   float* row_max, float* row_sumexp, float* row_target_logit, int64_t ignore_index, hipStream_t s) {
+                   float* row_max, float* row_sumexp, float* row_target_logit, int64_t ignore_index, hipStream_t s,
+                   int64_t ld) {
   if (rows <= 0) return 0;
+  if (ld < vocab) ld = vocab;
   SMPK_DISPATCH(dt, T, {
     xent_fwd_kernel<T><<<static_cast<unsigned>(rows), 256, 0, s>>>(static_cast<const T*>(logits), target, vocab,
                                                                    vocab_start, row_max, row_sumexp,
-                                                                   row_target_logit, ignore_index);
+                                                                   row_target_logit, ignore_index, ld);
   });
   return static_cast<int>(hipGetLastError());
 }
 
 int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row_lse, const float* grad_rows,
-             void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s) {
+             void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s,
+             int64_t ld) {
   if (rows <= 0) return 0;
+  if (ld < vocab) ld = vocab;
   SMPK_DISPATCH(dt, T, {
     xent_bwd_kernel<T><<<static_cast<unsigned>(rows), 256, 0, s>>>(static_cast<const T*>(logits), target, row_lse,
                                                                    grad_rows, static_cast<T*>(dlogits), vocab,
-                                                                   vocab_start, ignore_index);
+                                                                   vocab_start, ignore_index, ld);
   });
   return static_cast<int>(hipGetLastError());
 }

@@ -129,9 +129,11 @@ int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);
 // target logit (target may be outside the shard -> 0). Fused fwd writes softmax stats;
 // bwd writes dlogits = (softmax - onehot) * grad.
 int xent_fwd_stats(int dt, const void* logits, const int64_t* target, int64_t rows, int64_t vocab, int64_t vocab_start,
-                   float* row_max, float* row_sumexp, float* row_target_logit, int64_t ignore_index, hipStream_t s);
+                   float* row_max, float* row_sumexp, float* row_target_logit, int64_t ignore_index, hipStream_t s,
+                   int64_t ld = 0);
 int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row_lse, const float* grad_rows,
-             void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s);
+             void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s,
+             int64_t ld = 0);
 
 // ---------------------------------------------------------------- pack / unpack (pack.hip)
 // Generic strided 4-D copy: dst[i0,i1,i2,i3] = src[...] with element strides (for the

@@ -36,6 +36,7 @@ from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
 from ..ops.gelu import bias_gelu
+from ..ops import lm_head as lm_head_op
 from ..ops.linear import linear
 from ..ops.rope import apply_rotary
 from ..torch.state_mod import state
@@ -172,6 +173,19 @@ class _Dropout(nn.Module):
         if self.p == 0.0 or not self.training:
             return x
         return F.dropout(x, self.p, True)
+
+
+def _runs_here(module):
+    """The module executes on this pipeline stage and is not activation-checkpointed, so
+    using its parameters directly bypasses neither a remote call nor a checkpoint."""
+    from ..torch.state_mod import state
+
+    mm = state.module_manager
+    if mm is None or state.core is None:
+        return True
+    if state.core.pp_size() > 1 and not mm.is_executor(module):
+        return False
+    return mm.get_checkpoint_activations_config(module) is None
 
 
 class _LMHeadLinear(nn.Linear):
@@ -719,6 +733,14 @@ class DistributedTransformerLMHead(DistributedModule):
                                  group=tp_group() if self._tp > 1 else None, reduction="none")
             return rows.mean(), shift_logits
 
+        if (labels is not None and self.add_lm_head and not prescaled and self.lm_head.bias is None
+                and lm_head_op.usable(self.lm_head.weight, hidden) and _runs_here(self.lm_head)):
+            # odd vocabulary: LM head GEMMs + CE on a 64-padded copy (ops/lm_head.py), same
+            # loss / gradients as the plain path below
+            shift_labels = F.pad(labels[..., 1:], (0, 1), value=-100)
+            rows, logits = lm_head_op.padded_lm_head_cross_entropy(hidden, self.lm_head.weight, shift_labels)
+            count = (shift_labels != -100).sum().clamp(min=1)
+            return rows.sum() / count, logits
         logits = self.lm_head(hidden) if self.add_lm_head else hidden
         if labels is None:
             return logits

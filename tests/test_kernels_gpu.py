@@ -245,6 +245,75 @@ def test_gpt_fused_grad_accumulation_gpu(C, dt):
         assert torch.allclose(q.grad.float(), p.grad.float(), atol=tol, rtol=tol * 5), n
 
 
+@pytest.mark.parametrize("family", ["gptj-6b", "gptneox-20b", "gpt3-175b"])
+def test_model_family_step_gpu(C, family):
+    """The BASELINE model families at reduced width/depth (same architecture flags: GPT-J
+    parallel attention + interleaved RoPE, NeoX half-rotation RoPE, GPT-3 pre-LN with
+    tanh GeLU) through the HIP kernels (bf16 flash attention, RoPE, fused GeLU / LN) match
+    an fp32 CPU forward/backward of the same weights."""
+    from smdistributed_modelparallel_amd.models import build_gpt
+
+    torch.manual_seed(21)
+    kw = dict(dropout=0.0, num_layers=2, hidden_size=256, num_attention_heads=4, attention_head_size=64,
+              intermediate_size=1024, vocab_size=512, num_positions=128)
+    if family != "gpt3-175b":
+        kw["rotary_dim"] = 32 if family == "gptj-6b" else 16
+    cpu = build_gpt(family, **kw)
+    gpu = build_gpt(family, **kw)
+    gpu.load_state_dict(cpu.state_dict())
+    gpu = gpu.cuda().to(torch.bfloat16)
+    ids = torch.randint(0, 512, (2, 128))
+    lc, _ = cpu((ids, None, None, None, ids))
+    lc.backward()
+    lg, _ = gpu((ids.cuda(), None, None, None, ids.cuda()))
+    lg.float().backward()
+    assert abs(lg.item() - lc.item()) < 2e-2, (lg.item(), lc.item())
+    gc = dict(cpu.named_parameters())
+    for n, p in gpu.named_parameters():
+        ref = gc[n].grad
+        err = (p.grad.float().cpu() - ref).norm() / (ref.norm() + 1e-12)
+        assert err < 5e-2, (n, float(err))
+
+
+def test_padded_lm_head_ce_gpu(C, monkeypatch):
+    """LM head + CE through the 64-padded vocabulary (odd V): loss, logits, input and
+    (in-place accumulated) weight gradients equal the plain unpadded computation."""
+    import smdistributed_modelparallel_amd.ops.lm_head as LH
+    from smdistributed_modelparallel_amd.ops.linear import bump_weight_epoch
+
+    torch.manual_seed(4)
+    V, H, T = 1001, 256, 300
+    w = (torch.randn(V, H, device="cuda") * 0.05).to(torch.bfloat16).requires_grad_()
+    x = torch.randn(2, T // 2, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    lab = torch.randint(0, V, (2, T // 2), device="cuda")
+    lab[0, :7] = -100
+    bump_weight_epoch()
+    rows, logits = LH.padded_lm_head_cross_entropy(x, w, lab)
+    assert logits.shape == (2, T // 2, V)
+    gl = torch.randn(logits.shape, device="cuda") * 1e-3
+    (rows.sum() + (logits.float() * gl).sum()).backward()
+    wr, xr = w.detach().float().requires_grad_(), x.detach().float().requires_grad_()
+    lr_ = xr @ wr.t()
+    rr = torch.nn.functional.cross_entropy(lr_.view(-1, V), lab.view(-1), ignore_index=-100, reduction="none")
+    (rr.sum() + (lr_ * gl).sum()).backward()
+    assert torch.allclose(rows.float().view(-1), rr, atol=3e-2, rtol=1e-2)
+    assert torch.allclose(logits.float(), lr_, atol=3e-2, rtol=1e-2)
+    for a, b in ((x.grad, xr.grad), (w.grad, wr.grad)):
+        err = (a.float() - b).norm() / b.norm()
+        assert err < 2e-2, float(err)
+    # in-place accumulation into a bound (flat-buffer style) gradient view
+    base = torch.randn(V, H, device="cuda").to(torch.bfloat16)
+    w2 = w.detach().clone().requires_grad_()
+    w2.grad = base.clone()
+    w2._smp_fused_grad = True
+    rows2, _ = LH.padded_lm_head_cross_entropy(x.detach(), w2, lab)
+    rows2.sum().backward()
+    w3 = w.detach().clone().requires_grad_()
+    rows3, _ = LH.padded_lm_head_cross_entropy(x.detach(), w3, lab)
+    rows3.sum().backward()
+    assert torch.allclose(w2.grad.float(), base.float() + w3.grad.float(), atol=2e-2)
+
+
 def test_transposed_dgrad_gpu(C, monkeypatch):
     """Input gradients computed against the cached W^T (forward GEMM layout) equal
     autograd's; the cache refreshes when the weight epoch advances."""
