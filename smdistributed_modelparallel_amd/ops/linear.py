@@ -17,7 +17,8 @@ faster when both operands are contiguous along the reduction dimension (the forw
 product ``dY @ W`` whose W operand is strided along the reduction (1.18 PFLOP/s for the
 same m/n/k, TunableOp-selected, `configs/tunableop`).  Inside an ``@smp.step`` each
 weight therefore keeps a transposed copy ``W^T`` (refreshed once per step on first use,
-~1 ms per step for GPT-2 XL's 1.5 B weights, +2 B/param of HBM) and the input gradient is
+~1 ms per step for GPT-2 XL's 1.5 B weights, +2 B/param of HBM, capped at 8 % of the device
+by default: ``SMP_TRANSPOSED_DGRAD_BUDGET_GB``) and the input gradient is
 ``F.linear(dY, W^T)`` -- the fast layout.  ``SMP_TRANSPOSED_DGRAD=0`` disables it.
 """
 import os
@@ -28,6 +29,11 @@ import torch.nn.functional as F
 _WT_EPOCH = [0]
 _WT_MIN_NUMEL = 1 << 20
 _WT_ENABLED = os.environ.get("SMP_TRANSPOSED_DGRAD", "1") != "0"
+# HBM spent on W^T copies is capped: by default at min(8 % of the device, 10 % of the memory
+# still free when the first copy is requested -- model, gradients and optimizer state are
+# allocated by then), so models near the memory limit keep their capacity; the first
+# weights up to the cap get a copy, the rest use the strided-layout GEMM
+_WT_BUDGET = [None, 0]  # [cap bytes, bytes in use]
 
 
 def bump_weight_epoch():
@@ -46,7 +52,11 @@ def _transposed(w):
     buf = ent[1] if ent is not None and ent[1].dtype == w.dtype and ent[1].shape == (w.shape[1], w.shape[0]) else None
     with torch.no_grad():
         if buf is None:
-            buf = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+            try:
+                buf = torch.empty((w.shape[1], w.shape[0]), dtype=w.dtype, device=w.device)
+            except torch.OutOfMemoryError:
+                w.__dict__["_smp_wt_ok"] = False  # no room: this weight keeps the strided GEMM
+                return None
         if w.is_cuda and w.is_contiguous():
             from ._ext import ext
 
@@ -55,6 +65,28 @@ def _transposed(w):
             buf.copy_(w.detach().t())
     w.__dict__["_smp_wt"] = (key, buf)
     return buf
+
+
+def _wt_admit(w):
+    """Reserve W^T bytes for w under the HBM cap (decided once per weight)."""
+    ok = w.__dict__.get("_smp_wt_ok")
+    if ok is not None:
+        return ok
+    if _WT_BUDGET[0] is None:
+        gb = os.environ.get("SMP_TRANSPOSED_DGRAD_BUDGET_GB")
+        if gb:
+            _WT_BUDGET[0] = int(float(gb) * 2**30)
+        else:
+            total = torch.cuda.get_device_properties(w.device).total_memory
+            free = torch.cuda.mem_get_info(w.device)[0]
+            free += torch.cuda.memory_reserved(w.device) - torch.cuda.memory_allocated(w.device)
+            _WT_BUDGET[0] = int(min(0.08 * total, 0.10 * free))
+    need = w.numel() * w.element_size()
+    ok = _WT_BUDGET[1] + need <= _WT_BUDGET[0]
+    if ok:
+        _WT_BUDGET[1] += need
+    w.__dict__["_smp_wt_ok"] = ok
+    return ok
 
 
 def _use_transposed(w):
@@ -66,7 +98,7 @@ def _use_transposed(w):
         return False
     from ..torch.state_mod import state
 
-    return bool(getattr(state, "in_step_func", False))
+    return bool(getattr(state, "in_step_func", False)) and _wt_admit(w)
 
 
 def _col_sum(x2, out=None):
