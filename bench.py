@@ -30,9 +30,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-xl")
     ap.add_argument("--seq", type=int, default=2048)
-    ap.add_argument("--mbs", type=int, default=16,
-                    help="per-GPU micro-batch size (16 x 2048 tokens: GEMM M = 32768 keeps the MFMA pipes fed; "
-                         "well inside 288 GB HBM3E)")
+    ap.add_argument("--mbs", type=int, default=32,
+                    help="per-GPU micro-batch size: 32 x 2048 tokens (GEMM M = 65536) amortises the per-step "
+                         "optimizer / LM-head / transposition work and fills the chip with attention blocks; "
+                         "~190 GB of the 288 GB HBM3E (same-box A/B vs 16: +4.4 %% samples/s)")
     ap.add_argument("--microbatches", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--tp", type=int, default=1)
