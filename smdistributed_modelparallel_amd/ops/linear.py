@@ -113,6 +113,91 @@ def _col_sum(x2, out=None):
     return x2.sum(0)
 
 
+# ----------------------------------------------------------------- weight-gradient algorithm
+# dW[N, K] += dY[T, N]^T X[T, K] reduces over all T = batch x sequence tokens: few output
+# tiles (GPT-2 XL: 81-280 of 192-256 for 256 CUs) and both operands strided along the
+# reduction, the layout hipBLASLt runs slowest.  Two alternatives can win, depending on the
+# shape (MI355X, T = 65536, TunableOp-selected kernels; tools/wgrad_probe.py):
+#   "tn"  -- transpose dY and X (HIP LDS transpose, HBM rate) and run the GEMM with both
+#            operands contiguous along T: [4800, 1600] 1.32 -> 0.87 + 0.33 ms (transposes);
+#   "sk8" -- split T into 8 chunks, one batched GEMM into bf16 partials, then their sum:
+#            [1600, 1600] 0.49 -> 0.39 ms;
+# while for [6400, 1600] / [1600, 6400] the plain strided GEMM ("nn") stays fastest.  The
+# choice is made per (T, N, K, dtype) by timing the candidates on the real operands the first
+# time a shape occurs inside a step (gradient restored after each trial), then cached for the
+# process.  SMP_WGRAD_AUTOTUNE=0 keeps "nn" everywhere.
+_WGRAD_TUNE = os.environ.get("SMP_WGRAD_AUTOTUNE", "1") != "0"
+_WGRAD_CHOICE = {}
+_WGRAD_MIN_T = 16384
+_WGRAD_TEMP_CAP = 1 << 30  # bytes of temporaries a candidate may allocate
+
+
+def _wgrad_candidates(T, N, K, esize):
+    out = ["nn"]
+    if T * (N + K) * esize <= _WGRAD_TEMP_CAP:
+        out.append("tn")
+    if T % 8 == 0 and 8 * N * K * esize <= _WGRAD_TEMP_CAP:
+        out.append("sk8")
+    return out
+
+
+def _wgrad_run(method, g, dy2, x2):
+    if method == "tn":
+        from ._ext import ext
+
+        dyt = torch.empty((dy2.shape[1], dy2.shape[0]), dtype=dy2.dtype, device=dy2.device)
+        xt = torch.empty((x2.shape[1], x2.shape[0]), dtype=x2.dtype, device=x2.device)
+        ext().transpose_into(dy2, dyt)
+        ext().transpose_into(x2, xt)
+        g.addmm_(dyt, xt.t())
+    elif method == "sk8":
+        T = dy2.shape[0]
+        parts = torch.bmm(dy2.view(8, T // 8, dy2.shape[1]).transpose(1, 2), x2.view(8, T // 8, x2.shape[1]))
+        g.add_(parts.sum(0, dtype=torch.float32))
+    else:
+        g.addmm_(dy2.t(), x2)
+
+
+def _wgrad_pick(g, dy2, x2):
+    cands = _wgrad_candidates(dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.element_size())
+    if len(cands) == 1:
+        return cands[0]
+    saved = g.clone()
+    best, best_t, times = "nn", float("inf"), {}
+    for m in cands:
+        try:
+            _wgrad_run(m, g, dy2, x2)  # warm-up (kernel selection, allocator)
+            start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            start.record()
+            for _ in range(3):
+                _wgrad_run(m, g, dy2, x2)
+            end.record()
+            end.synchronize()
+            t = start.elapsed_time(end)
+        except torch.OutOfMemoryError:
+            t = float("inf")
+        g.copy_(saved)
+        times[m] = t
+        if t < best_t * 0.97:  # a candidate must beat the current pick by > 3 %
+            best, best_t = m, t
+    del saved
+    if os.environ.get("SMP_WGRAD_LOG") == "1":
+        print(f"wgrad autotune T={dy2.shape[0]} N={dy2.shape[1]} K={x2.shape[1]}: "
+              + ", ".join(f"{m} {t / 3:.3f} ms" for m, t in times.items()) + f" -> {best}", flush=True)
+    return best
+
+
+def _wgrad_accumulate(g, dy2, x2):
+    """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape."""
+    method = "nn"
+    if _WGRAD_TUNE and g.is_cuda and dy2.shape[0] >= _WGRAD_MIN_T and dy2.is_contiguous() and x2.is_contiguous():
+        key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype)
+        method = _WGRAD_CHOICE.get(key)
+        if method is None:
+            method = _WGRAD_CHOICE[key] = _wgrad_pick(g, dy2, x2)
+    _wgrad_run(method, g, dy2, x2)
+
+
 def _fusable(w):
     g = w.grad
     return (getattr(w, "_smp_fused_grad", False) and g is not None and g.dtype == w.dtype and g.shape == w.shape
@@ -145,7 +230,7 @@ class _LinearWGradAccum(torch.autograd.Function):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the
                 # weight's AccumulateGrad node (a no-op), so post-accumulate-grad hooks -- the
                 # reducers' bucket-ready signals -- fire exactly once, after this write
-                w.grad.addmm_(dy2.t(), x.reshape(-1, x.shape[-1]))
+                _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]))
             else:
                 # grad slot re-bound/removed since forward: hand the gradient to autograd
                 return dx, dy2.t().mm(x.reshape(-1, x.shape[-1])), db
