@@ -1,0 +1,45 @@
+"""bench.py driver contract on CPU: launched the way the driver launches it for N > 1
+(torch.distributed.run, one process per rank, 127.0.0.1 rendezvous; gloo here, RCCL on the
+GPU node), rank 0 prints exactly one JSON line with the required keys and whole-job values."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+            "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_bench_json_line(nproc):
+    args = ["bench.py", "--gpus", str(nproc), "--model", "gpt2-tiny", "--seq", "64", "--mbs", "2",
+            "--steps", "2", "--warmup", "1"]
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert REQUIRED <= set(rec)
+    assert rec["n_gpus"] == nproc and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["scaling"] == "weak" and rec["higher_is_better"] is True and rec["dtype"] == "bf16"
+    cfg = rec["config"]
+    assert cfg["global_batch"] == 2 * nproc and cfg["seq_len"] == 64
+    assert cfg["parallelism"] == f"pp1xtp1xdp{nproc}"
+    # value is the whole-job aggregate: global batch x steps / max-over-ranks wall time
+    assert abs(rec["value"] - cfg["global_batch"] / (rec["ms_per_step"] / 1000.0)) < 0.02 * rec["value"] + 1e-3
