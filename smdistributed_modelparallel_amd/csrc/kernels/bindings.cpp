@@ -266,7 +266,7 @@ std::vector<at::Tensor> bias_gelu_bwd_dbias(at::Tensor dy, at::Tensor x, at::Ten
   if (acc)
     TORCH_CHECK(db.is_contiguous() && db.numel() == cols && db.scalar_type() == x.scalar_type(),
                 "bias_gelu_bwd_dbias: dbias_out must be a contiguous [cols] tensor of x's dtype");
-  const int64_t parts = smpk::col_sum_parts(rows);
+  const int64_t parts = smpk::gelu_dbias_parts(rows);
   auto ws = at::empty({parts + 32, cols}, x.options().dtype(at::kFloat));
   const int rc = smpk::bias_gelu_bwd_dbias(dt_code(x), dy.data_ptr(), x.data_ptr(), bias.data_ptr(), dx.data_ptr(),
                                            db.data_ptr(), ws.data_ptr<float>(), rows, cols, stream(), acc, exact);

@@ -66,6 +66,7 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
 int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, int64_t cols, hipStream_t s,
             bool accumulate = false);
 int col_sum_parts(int64_t rows);
+int gelu_dbias_parts(int64_t rows);  // workspace partial rows for bias_gelu_bwd_dbias
 int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias, void* dx, void* dbias,
                         float* workspace, int64_t rows, int64_t cols, hipStream_t s, bool accumulate = false,
                         bool exact = false);

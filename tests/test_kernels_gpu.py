@@ -67,7 +67,8 @@ def test_add_layernorm(C, dt):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("rows,cols", [(33, 6400), (5000, 6400), (777, 1600), (1031, 4800), (300, 40), (129, 1001)])
+@pytest.mark.parametrize("rows,cols", [(33, 6400), (5000, 6400), (777, 1600), (1031, 4800), (300, 40), (129, 1001),
+                                       (3001, 2056), (4097, 4800)])
 @pytest.mark.parametrize("exact", [False, True])
 def test_bias_gelu(C, dt, rows, cols, exact):
     from smdistributed_modelparallel_amd.ops.gelu import _gelu_tanh_ref, bias_gelu
@@ -85,6 +86,23 @@ def test_bias_gelu(C, dt, rows, cols, exact):
     yr.backward(g)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
     assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50 * max(1, rows // 200) ** 0.5, rtol=tol * 4)
+
+
+@pytest.mark.parametrize("rows,cols", [(4097, 6400), (3001, 2056)])
+def test_gelu_row_stream_matches_column_walker(C, rows, cols, monkeypatch):
+    """The row-streaming GeLU kernels (rows >= 2048) against the column walker (SMP_GELU_ROWS=0):
+    the same per-element math, so dx and y are bitwise equal; dbias differs only in summation order."""
+    torch.manual_seed(9)
+    dt = torch.bfloat16
+    x = torch.randn(rows, cols, device="cuda", dtype=dt)
+    b = torch.randn(cols, device="cuda", dtype=dt)
+    dy = torch.randn_like(x)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SMP_GELU_ROWS", mode)
+        out[mode] = (C.bias_gelu_fwd(x, b, False), *C.bias_gelu_bwd_dbias(dy, x, b, None, False))
+    assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
+    assert torch.allclose(out["1"][2].float(), out["0"][2].float(), atol=0.05 * rows ** 0.5, rtol=1e-2)
 
 
 @pytest.mark.parametrize("dt", DT)
