@@ -125,8 +125,11 @@ def _col_sum(x2, out=None):
 # while for [6400, 1600] / [1600, 6400] the plain strided GEMM ("nn") stays fastest.  The
 # choice is made per (T, N, K, dtype) by timing the candidates on the real operands the first
 # time a shape occurs inside a step (gradient restored after each trial), then cached for the
-# process.  SMP_WGRAD_AUTOTUNE=0 keeps "nn" everywhere.
-_WGRAD_TUNE = os.environ.get("SMP_WGRAD_AUTOTUNE", "1") != "0"
+# process.  Opt-in (SMP_WGRAD_AUTOTUNE=1): the isolated wins above did not survive the full
+# step -- same-box A/B of the GPT-2 XL bench, alternating, 766.6 / 770.1 ms/step off vs
+# 770.1 / 765.8 on (tools/gpu_ab_env.sh) -- and a per-rank timing pick can differ across
+# data-parallel ranks, so "nn" stays the default.
+_WGRAD_TUNE = os.environ.get("SMP_WGRAD_AUTOTUNE", "0") == "1"
 _WGRAD_CHOICE = {}
 _WGRAD_MIN_T = 16384
 _WGRAD_TEMP_CAP = 1 << 30  # bytes of temporaries a candidate may allocate

@@ -24,7 +24,8 @@ def test_wgrad_methods_match_fp32(method, shape):
     assert err < 1e-2, (method, err)
 
 
-def test_wgrad_autotune_picks_and_preserves_gradient():
+def test_wgrad_autotune_picks_and_preserves_gradient(monkeypatch):
+    monkeypatch.setattr(L, "_WGRAD_TUNE", True)  # opt-in (SMP_WGRAD_AUTOTUNE=1)
     T, N, K = 16384, 512, 256
     g0 = torch.Generator(device="cuda").manual_seed(1)
     dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
