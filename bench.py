@@ -219,7 +219,7 @@ def main():
                 "parallelism": par,
                 "micro_batch_per_gpu": args.mbs,
                 "microbatches": args.microbatches,
-                "flash_attention": not args.no_flash,
+                "flash_attention": (not args.no_flash) and mc["attention_head_size"] in (64, 128),
                 "dropout": args.dropout,
                 "gemm_selection": "tunableop" if tmode != "off" else "heuristic",
             },

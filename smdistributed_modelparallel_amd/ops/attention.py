@@ -82,7 +82,28 @@ def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, t
                      training=training, use_flash=use_flash)
 
 
+# Score elements per materialised chunk.  On MI355X (torch 2.10 + ROCm 7), the backward of the
+# batched score GEMMs faults with an illegal address once b*h*sq*sk reaches 2^28 (GPT-J 6B
+# head dim 256 at b4 s2048: tools/gptj_isolate.py attn_torch); b1 (2^26) runs.  Chunking over
+# the batch keeps every GEMM at a verified size and bounds the [b, h, sq, sk] score memory.
+_MAX_SCORE_ELEMS = 1 << 26
+
+
 def _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, fp32):
+    b, sq, h = q.shape[0], q.shape[1], q.shape[2]
+    per_b = h * sq * k.shape[1]
+    if b > 1 and b * per_b > _MAX_SCORE_ELEMS:
+        cb = max(1, _MAX_SCORE_ELEMS // per_b)
+        outs = []
+        for i in range(0, b, cb):
+            mi = mask if mask is None or mask.shape[0] == 1 else mask[i:i + cb]
+            outs.append(_materialised_chunk(q[i:i + cb], k[i:i + cb], v[i:i + cb], scale, causal, mi, dropout_p,
+                                            window, training, fp32))
+        return torch.cat(outs, 0)
+    return _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32)
+
+
+def _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32):
     # q,k,v: [b, s, h, d] -> [b, h, s, d]
     qh, kh, vh = (t.transpose(1, 2) for t in (q, k, v))
     if fp32:
