@@ -83,7 +83,7 @@ def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, t
 
 
 # Score elements per materialised chunk.  On MI355X (torch 2.10 + ROCm 7), the backward of the
-# batched score GEMMs faults with an illegal address once b*h*sq*sk reaches 2^28 (GPT-J 6B
+# strided batched score GEMMs faulted with an illegal address at b*h*sq*sk = 2^28 (GPT-J 6B
 # head dim 256 at b4 s2048: tools/gptj_isolate.py attn_torch); b1 (2^26) runs.  Chunking over
 # the batch keeps every GEMM at a verified size and bounds the [b, h, sq, sk] score memory.
 _MAX_SCORE_ELEMS = 1 << 26
@@ -104,8 +104,10 @@ def _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, fp3
 
 
 def _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32):
-    # q,k,v: [b, s, h, d] -> [b, h, s, d]
-    qh, kh, vh = (t.transpose(1, 2) for t in (q, k, v))
+    # q,k,v: [b, s, h, d] -> contiguous [b, h, s, d]: the score GEMMs then run as plain
+    # batched GEMMs.  Strided views of a packed QKV reach library solutions that fault
+    # (TunableOp tuning of GPT-J's score GEMM: profiles/r1_gptj6b_1gpu.md).
+    qh, kh, vh = (t.transpose(1, 2).contiguous() for t in (q, k, v))
     if fp32:
         qh, kh, vh = qh.float(), kh.float(), vh.float()
     scores = torch.matmul(qh, kh.transpose(-1, -2))
