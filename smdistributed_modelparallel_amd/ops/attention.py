@@ -94,11 +94,12 @@ def _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, fp3
     per_b = h * sq * k.shape[1]
     if b > 1 and b * per_b > _MAX_SCORE_ELEMS:
         cb = max(1, _MAX_SCORE_ELEMS // per_b)
-        outs = []
-        for i in range(0, b, cb):
-            mi = mask if mask is None or mask.shape[0] == 1 else mask[i:i + cb]
-            outs.append(_materialised_chunk(q[i:i + cb], k[i:i + cb], v[i:i + cb], scale, causal, mi, dropout_p,
-                                            window, training, fp32))
+        # split(), not slicing: its backward is one concatenation of the chunk grads, where a
+        # slice's backward zero-fills a full-size gradient per chunk and adds them up
+        qs, ks, vs = q.split(cb), k.split(cb), v.split(cb)
+        ms = [mask] * len(qs) if mask is None or mask.shape[0] == 1 else mask.split(cb)
+        outs = [_materialised_chunk(qi, ki, vi, scale, causal, mi, dropout_p, window, training, fp32)
+                for qi, ki, vi, mi in zip(qs, ks, vs, ms)]
         return torch.cat(outs, 0)
     return _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32)
 
