@@ -111,8 +111,9 @@ def build_runtime(jobs=8, verbose=False):
 def build_kernels(jobs=8, verbose=False):
     src_dir = os.path.join(CSRC, "kernels")
     hip_srcs = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
-    cpp_srcs = sorted(glob.glob(os.path.join(src_dir, "*.cpp")))
-    hdrs = sorted(glob.glob(os.path.join(src_dir, "*.h")))
+    rt_dir = os.path.join(CSRC, "torchrt")  # torch-aware runtime (grad tracker, IPC P2P)
+    cpp_srcs = sorted(glob.glob(os.path.join(src_dir, "*.cpp"))) + sorted(glob.glob(os.path.join(rt_dir, "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(src_dir, "*.h"))) + sorted(glob.glob(os.path.join(rt_dir, "*.h")))
     tinc, tlib, abi = _torch_paths()
     common = [
         "-O3",

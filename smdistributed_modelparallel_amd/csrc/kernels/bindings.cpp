@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 
 #include "kernels.h"
+#include "../torchrt/torchrt.h"
 
 namespace {
 
@@ -472,7 +473,8 @@ void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor 
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.doc() = "smdistributed_modelparallel_amd CDNA4 (gfx950) kernels";
+  m.doc() = "smdistributed_modelparallel_amd CDNA4 (gfx950) kernels + torch-aware runtime";
+  smprt_torch::register_bindings(m);
   m.def("fused_adam", &fused_adam);
   m.def("fused_sgd", &fused_sgd);
   m.def("fused_adagrad", &fused_adagrad);

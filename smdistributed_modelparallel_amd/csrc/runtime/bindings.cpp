@@ -87,6 +87,7 @@ PYBIND11_MODULE(_smprt, m) {
       .def(py::init<int>())
       .def("set_output", &Timeline::set_output)
       .def_property_readonly("enabled", &Timeline::enabled)
+      .def_property_readonly("roctx_enabled", &Timeline::roctx_enabled)
       .def("start_step", &Timeline::start_step)
       .def("end_step", &Timeline::end_step)
       .def("record", &Timeline::record)

@@ -19,6 +19,7 @@ class Timeline {
   ~Timeline();
   void set_output(const std::string& path);
   bool enabled() const { return !path_.empty(); }
+  bool roctx_enabled() const { return roctx_push_ != nullptr; }
   void start_step(int64_t step);
   void end_step();
   // Instant-with-duration event: [begin, end) of a pipeline task on microbatch `mb`.

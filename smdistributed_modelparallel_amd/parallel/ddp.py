@@ -42,9 +42,13 @@ class BucketReducer:
         self.name = name
         self.final = False  # current backward produces final grads
         self.sync_enabled = True
+        # pipeline stages: finality comes from the model's GradTracker (set by the model)
+        self.tracker = None
+        self.tindex = None
         self.next_launch = 0
         self._hooks = []
-        self._launched_any = False
+        self.launched_before_sync = 0  # buckets launched while backward was still running
+        self._in_sync = False
         self.group_rank = dist.get_rank(group) if (group is not None and dist.is_initialized()) else 0
         if overlap or flat.fp32_accumulation:
             self._install_hooks()
@@ -63,8 +67,19 @@ class BucketReducer:
     def _on_grad(self, p):
         if self.flat.fp32_accumulation:
             self.flat.fold_grad(p)  # every microbatch: low-precision grad -> fp32 main_grad
+        if self.tracker is not None:
+            # pipeline stage: one accumulation of one backward segment; the tracker knows
+            # how many segments reach p this step (reference reducer.py:92 + GradCounter)
+            if self.tracker.mark_grad(self.tindex[p]) and self.sync_enabled and self.overlap:
+                self.param_final(p)
+            return
         if not (self.final and self.sync_enabled):
             return
+        self.param_final(p)
+
+    def param_final(self, p):
+        """p's gradient will not change any more this step: count it towards its bucket and
+        launch every bucket that is complete, in bucket order."""
         b = self.flat.bucket_of.get(p)
         if b is None:
             return
@@ -83,6 +98,7 @@ class BucketReducer:
         if b.launched:
             return
         b.launched = True
+        self.launched_before_sync += 0 if self._in_sync else 1
         buf = self.flat.grad[b.start : b.end]
         scale = 1.0 / (self.divisor * self.group_size)
         if scale != 1.0:
@@ -108,6 +124,8 @@ class BucketReducer:
             b.work = None
             b.launched = False
         self.next_launch = 0
+        self.launched_before_sync = 0
+        self._in_sync = False
 
     def set_final(self, final):
         self.final = final and self.overlap
@@ -119,6 +137,7 @@ class BucketReducer:
                 self.flat.fold_grad(p)
         if not self.sync_enabled:
             return
+        self._in_sync = True
         for b in self.flat.buckets:
             if not b.launched:
                 self._launch(b)

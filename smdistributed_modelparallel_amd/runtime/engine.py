@@ -119,6 +119,7 @@ class PipelineEngine:
         self._stop = False
         self._root_tokens = {}
         self._local_q = []
+        self._tl = None
 
     def _new_id(self):
         # (pp_rank, n): identical on every TP / DP peer executing the same task sequence
@@ -136,6 +137,22 @@ class PipelineEngine:
     def _send(self, dst, msg):
         stubbed, tensors = stubify(msg)
         self.state.transport.send(dst, stubbed, tensors)
+
+    # ------------------------------------------------------------- tracing
+    def _traced(self, mb, label, fn, *args):
+        """Run one scheduler task; with SMP_TIMELINE_FILE / SMP_ROCTX=1 it becomes a
+        Chrome-trace span and a roctx range (reference `server.py:366-478`
+        timeline_record_pipeline_event around every request/result)."""
+        tl = self._tl
+        if tl is None:
+            return fn(*args)
+        t0 = tl.now_us()
+        tl.range_push(label)
+        try:
+            return fn(*args)
+        finally:
+            tl.range_pop()
+            tl.record(mb, label, t0, tl.now_us())
 
     def _broadcast_pp(self, msg):
         me = self.core.rank()
@@ -169,6 +186,8 @@ class PipelineEngine:
         self.num_mb = n
         leader = self.core.pp_rank() == 0
         self.server = greenlet.getcurrent()
+        tl = self.core.timeline
+        self._tl = tl if (tl is not None and (tl.enabled or tl.roctx_enabled)) else None
         self.step_fn = step_fn
         self.mb_inputs = mb_inputs
         if leader:
@@ -226,10 +245,10 @@ class PipelineEngine:
     def _do_action(self, act):
         kind, mb = act
         if kind == "fwd":
-            self._start_microbatch(mb)
+            self._traced(mb, f"FWD mb{mb} (step fn)", self._start_microbatch, mb)
         else:
             self.pipeline.set_status(mb, MbStatus.BWD)
-            self._resume(self.waiting.pop(("bwd_start", mb)), None)
+            self._traced(mb, f"BWD mb{mb} (loss)", self._resume, self.waiting.pop(("bwd_start", mb)), None)
 
     def _event_key(self, src, stubbed):
         kind = stubbed[0]
@@ -356,6 +375,19 @@ class PipelineEngine:
 
     # ------------------------------------------------------------- dispatch
     def _dispatch(self, src, stubbed, tensors):
+        if self._tl is not None and stubbed[0] in ("fwd", "res", "bwd"):
+            kind = stubbed[0]
+            mb = stubbed[2]
+            if kind == "fwd":
+                label = f"FWD mb{mb} {stubbed[3][1]}" + (f"[{stubbed[3][2]}:]" if stubbed[3][0] == "chain" else "")
+            elif kind == "bwd":
+                label = f"BWD mb{mb} {stubbed[1][0]}{stubbed[1][1]} from r{src}"
+            else:
+                label = f"RESULT mb{mb} from r{src}"
+            return self._traced(mb, label, self._dispatch_impl, src, stubbed, tensors)
+        return self._dispatch_impl(src, stubbed, tensors)
+
+    def _dispatch_impl(self, src, stubbed, tensors):
         kind = stubbed[0]
         if kind == "fwd":
             self._spawn(self._exec_fwd, stubbed[2], "fwd", src, stubbed, tensors)
@@ -365,6 +397,8 @@ class PipelineEngine:
             self._resume(w, (out_stubbed, tensors, holder, out_key))
         elif kind == "bwd":
             _, key, mb, grads_stubbed, remote_token = stubbed
+            # a backward request for mb: its forward is over everywhere (server.py:455)
+            self.state.model._mark_fwd_pass_done(mb)
             grads = unstubify(grads_stubbed, tensors)
             self._process_bwd(src, key, mb, grads, remote_token)
         elif kind == "ack":
@@ -372,6 +406,7 @@ class PipelineEngine:
         elif kind == "mbdone":
             _, mb, out_stubbed = stubbed
             self.results[mb] = unstubify(out_stubbed, tensors)
+            self.state.model._mark_fwd_pass_done(mb)
             self.mbstate.pop(mb, None)
             self.state.model._on_microbatch_done(mb)
             if len(self.results) == self.num_mb:
@@ -424,6 +459,7 @@ class PipelineEngine:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
                 self._mb(mb).sent[rid] = sent
+                st.model._track_segment(sent)
         st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled), tensors)
         out_stubbed, out_tensors, holder, out_key = self._suspend(("res", rid))
         return self._materialize_outputs(out_stubbed, out_tensors, holder, out_key, mb, grad_enabled)
@@ -491,6 +527,7 @@ class PipelineEngine:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
                 self._mb(mb).sent[rid2] = sent
+                self.state.model._track_segment(sent)
         self.state.transport.send(
             nxt, ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled),
             tensors,
@@ -502,6 +539,7 @@ class PipelineEngine:
             rg = [t for t in tensors if t.requires_grad]
             if rg:
                 self._mb(mb).out[rid] = rg
+                self.state.model._track_segment(rg)
         msg = ("res", result_id, mb, stubbed, self.core.rank(), rid, grad_enabled)
         if reply_to == self.core.rank():
             # local delivery (a chain came back to its requester's stage): queue it for the
@@ -515,6 +553,9 @@ class PipelineEngine:
     def backward_root(self, tensors, grads):
         """model.backward() on pp_rank 0 inside a microbatch worker."""
         mb = self.state.microbatch
+        # register the loss segment before the scheduler marks this microbatch's forward
+        # done: the last microbatch's mark must never see an incomplete expected count
+        self.state.model._track_segment([t for t in tensors if t.requires_grad])
         self._suspend(("bwd_start", mb))
         tid = self._new_token(None, None, mb)
         self._root_tokens[mb] = tid

@@ -122,12 +122,16 @@ def init(config=None):
     state.tp_registry.register_builtins()
     seed = cfg.tensor_parallel_seed + 1000 * core.pp_rank() + 100000 * core.rdp_rank()
     state.rng_manager = RngManager(seed, state.device)
+    from ..runtime.transport import choose_mode
+
+    be = dist.get_backend()
+    state.p2p_mode = choose_mode(core, state.device, "nccl" if "nccl" in str(be) else "gloo")
     state.create_process_groups()
     if cfg.offload_activations:
         from ..runtime.offload import create_offloader
 
         state.current_offloader = create_offloader(cfg, state.device)
-    state.transport = PipelineTransport(core, state.pgs, state.device)
+    state.transport = PipelineTransport(core, state.pgs, state.device, mode=state.p2p_mode)
     state.initialized = True
     _patch_module_init()
     if core.rank() == 0:

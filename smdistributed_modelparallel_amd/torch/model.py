@@ -103,6 +103,8 @@ class DistributedModel(nn.Module):
         self.reducers = {}
         self._optimizer = None
         self._step_had_backward = False
+        self.grad_tracker = None
+        self._tracked = []
 
         mm = state.module_manager
         state.model = self
@@ -301,7 +303,7 @@ class DistributedModel(nn.Module):
                 raise SMPInvalidArgumentError(f"mixed parameter dtypes {dtypes} are not supported in one model")
             dtype = dtypes.pop()
             fp32_acc = bool(cfg._fp32_grad_accumulation) and dtype in (torch.float16, torch.bfloat16)
-            flat = FlatParamGroup(members, device, dtype, cap, _FIRST_BUCKET_BYTES, align=64 * max(1, gsize),
+            flat = FlatParamGroup(members, device, dtype, cap, min(cap, _FIRST_BUCKET_BYTES), align=64 * max(1, gsize),
                                   segments=segments, grad_dtype=torch.float32 if fp32_acc else None)
             self.flat_groups[key] = flat
             hook = self._comm_hook
@@ -311,6 +313,41 @@ class DistributedModel(nn.Module):
             self.reducers[key] = BucketReducer(flat, group if gsize > 1 else None, gsize, divisor,
                                                overlap=self.overlapping_allreduce, shard=shard,
                                                comm_hook=hook, name=key)
+        self._build_grad_tracker()
+
+    def _build_grad_tracker(self):
+        """Pipeline stages: gradient finality across microbatches and backward segments
+        (native GradTracker, N1g) drives the bucket launches, so DP reduction overlaps the
+        pipeline's last backward passes instead of waiting for the end of the step
+        (reference `model.py:401-403`, `allreduce/reducer.py:92`, `server.py:410,455`)."""
+        self.grad_tracker = None
+        self._tracked = []
+        if state.core.pp_size() == 1 or not self.reducers:
+            return
+        from ..ops._ext import ext
+
+        params, owners = [], []
+        for r in self.reducers.values():
+            for p in r.flat.params():
+                if p.requires_grad:
+                    params.append(p)
+                    owners.append(r)
+        if not params:
+            return
+        tracker = ext().GradTracker(params, state.cfg.microbatches)
+        index = {p: i for i, p in enumerate(params)}
+        for r in self.reducers.values():
+            r.tracker = tracker
+            r.tindex = index
+        self.grad_tracker = tracker
+        self._tracked = list(zip(params, owners))
+
+    def _track_segment(self, roots):
+        """A backward segment was registered (tensors whose gradients another stage -- or the
+        loss -- will deliver): every parameter reachable from them expects one more
+        accumulation this step."""
+        if self.grad_tracker is not None and roots:
+            self.grad_tracker.add_segment(roots)
 
     def _build_sharded_dp(self):
         from ..parallel.sharded_dp import ShardedDataParallel, _NoReducer
@@ -357,7 +394,14 @@ class DistributedModel(nn.Module):
             r.set_final(final)
 
     def _mark_fwd_pass_done(self, mb):
-        pass
+        """Microbatch `mb` has started its backward on this stage, so its forward is over
+        (reference `server.py:410,455`)."""
+        if self.grad_tracker is None or not (0 <= mb < state.cfg.microbatches):
+            return
+        for i in self.grad_tracker.mark_fwd_done(mb):
+            p, r = self._tracked[i]
+            if r.sync_enabled and r.overlap:
+                r.param_final(p)
 
     def _on_microbatch_done(self, mb):
         pass
@@ -371,6 +415,8 @@ class DistributedModel(nn.Module):
             for r in self.reducers.values():
                 r.sync_enabled = sync
                 r.prepare_for_backward()
+            if getattr(self, "grad_tracker", None) is not None:
+                self.grad_tracker.reset(state.cfg.microbatches)
         self._step_had_backward = False
         yield
         if not self.partitioned:

@@ -80,6 +80,7 @@ class PTModelParallelState:
         self.offloaders = {}
         self.current_offloader = None
         self.transport = None
+        self.p2p_mode = "cpu"
         self.sdp = None
         self.first_step_done = False
         self.skip_graph_validation = os.environ.get("SMP_SKIP_GRAPH_VALIDATION", "0") == "1"
@@ -143,7 +144,7 @@ class PTModelParallelState:
             self.pgs.cpu_tp = mine
         else:
             self.pgs.cpu_tp = self.pgs.tp
-        if self.use_gpu and core.pp_size() > 1:
+        if self.use_gpu and core.pp_size() > 1 and self.p2p_mode == "rccl":
             # one RCCL communicator per directed stage pair inside every PP group
             for ranks in ranker.all_groups("pp"):
                 for a in ranks:

@@ -36,6 +36,13 @@ def test_pp2_dp2():
     _run(4, 2, 1, 2)
 
 
+@pytest.mark.parametrize("pipe", ["interleaved", "simple"])
+def test_pp2_dp2_reduction_overlaps_pipeline_backward(pipe):
+    """GradTracker finality: DP buckets launch during the last microbatches' backward, not
+    at the step-end synchronize (reference GradCounter + Reducer), and results still match."""
+    _run(4, 2, 1, 3, pipe=pipe, extra={"dm_kwargs": {"bucket_cap_mb": 0.02}, "expect_overlap": True})
+
+
 def test_dp2():
     _run(2, 1, 1, 2)
 

@@ -54,7 +54,7 @@ def main():
         layers = list(net.transformer.seq_layers)
         for i, layer in enumerate(layers):
             smp.set_partition(layer, (i * pp) // len(layers))
-    model = smp.DistributedModel(net)
+    model = smp.DistributedModel(net, **extra.get("dm_kwargs", {}))
     if delayed:
         # meta parameters: the reference weights load once the partition has materialised them
         model.load_state_dict(ref.state_dict())
@@ -123,6 +123,13 @@ def main():
         if extra.get("ref_clip") or extra.get("opt_clip"):
             torch.nn.utils.clip_grad_norm_(ref.parameters(), extra.get("ref_clip") or extra["opt_clip"])
         ropt.step()
+        if extra.get("expect_overlap"):
+            # DP buckets must have been launched while the pipeline was still running its
+            # backward passes (GradTracker finality), not all at the step-end synchronize
+            early = sum(r.launched_before_sync for r in model.reducers.values())
+            total = sum(len(r.flat.buckets) for r in model.reducers.values())
+            assert total > 1 and early >= 1, (smp.rank(), early, total)
+            print(f"rank {smp.rank()} overlap: {early}/{total} buckets launched during backward", flush=True)
         my_losses = torch.stack([o.detach().float() for o in out.outputs]).mean()
         mine = torch.tensor([my_losses.item()])
         all_l = smp.allgather(mine.item(), smp.DP_GROUP)
