@@ -1,0 +1,926 @@
+// Flash-style fused attention for CDNA4 (gfx950): forward, and backward as two kernels
+// (dK/dV per key block, dQ per query block -- no fp32 atomics, bitwise reproducible).
+//
+// Replaces the reference's materialised-score path (QK^T GEMM -> fused softmax ->
+// dropout -> PV GEMM, `smp/torch/nn/transformer.py:1617-1835`, capped at sk <= 2048):
+// no [s, s] tensor is ever written, causal blocks above the diagonal are skipped, and
+// there is no sequence-length cap.
+//
+// Layout of the MFMA work (v_mfma_f32_32x32x16_{bf16,f16}, wave64):
+//  * forward / dQ: each wave owns 32 queries.  Scores are computed TRANSPOSED,
+//    S^T = K Q^T, so a lane holds 16 keys of ONE query (its lane & 31): the online-softmax
+//    row max / row sum are lane-local plus one cross-half (lane ^ 32) exchange.  The
+//    probability accumulator is then directly the B operand of O^T = V^T P^T (k order of
+//    the accumulator rows handled by the A-operand fetch), whose output again has the
+//    query on the lane -- the rescale by exp(m_old - m_new) is lane-local, no shuffles.
+//  * V^T / K^T / dO^T / Q^T operands are fetched with ds_read_b64_tr_b16 (hardware
+//    transpose) from row-major LDS tiles; row-major operands with ds_read_b128.
+//  * dK/dV: each wave owns 32 keys with the key on the lane (S = Q K^T, dP = dO V^T); P and
+//    dS accumulators are the B operands of dV^T = dO^T P and dK^T = Q^T dS.
+//  * LDS rows are padded by 16 B (register staging), which makes the 16-byte row reads
+//    conflict-free.
+// 256 threads (4 waves) per block; 128 queries (fwd, dQ) or 128 keys (dK/dV) per block,
+// 64-wide tiles along the reduction axis.  Causal q-blocks are launched heaviest first.
+//
+// Variants (template flags, one instantiation set per head dim in attention_d*.hip):
+//  * BIAS: additive per-key bias [b, sk] (padding masks; reference mask semantics
+//    `smp/torch/nn/transformer.py:403-409,1680-1708`), folded into the score MFMA's initial
+//    accumulator (bias / scale), so it costs no VALU work per score.
+//  * DROP: attention dropout generated in-kernel from a counter-based hash of
+//    (seed, offset, b*h, query, key) -- the backward regenerates exactly the same mask, no
+//    [s, s] mask tensor exists.  A 32-bit hash serves a key PAIR (16-bit uniform each).
+//    The row sums use the undropped P (softmax normalisation), the P.V operand the kept
+//    entries, and 1/(1-p) is applied once to O.  Backward: dV = (P o Z)^T dO and
+//    dS = P o (Z o dP - delta) with Z = keep / (1 - p); delta = rowsum(dO o O) is unchanged.
+//  * head dims 64, 96, 128, 256.  D = 96 uses a 128-element LDS row stride (swizzle needs a
+//    power-of-two chunk count) but runs 6 / 3 MFMA k-steps / tiles, not 8 / 4.
+#include "common.h"
+#include "kernels.h"
+
+namespace smpk {
+namespace attn {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+template <typename T>
+struct MF;
+template <>
+struct MF<bf16> {
+  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ __bf16 cvt(float x) { return static_cast<__bf16>(x); }
+};
+template <>
+struct MF<f16> {
+  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ _Float16 cvt(float x) { return static_cast<_Float16>(x); }
+};
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int kThreads = 256;
+
+// LDS row stride (elements) for head dim D
+template <int D>
+struct LdsStride {
+  static constexpr int v = D == 96 ? 128 : D;
+};
+
+// ---------------------------------------------------------------- dropout hash
+// lowbias32 (a bijective 32-bit mixer): distinct (query, key-pair) inputs under one key give
+// distinct outputs; the two 16-bit halves are the uniforms of the pair's even / odd key.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t drop_key(const AttnParams& p, int64_t bh) {
+  const uint32_t s0 = static_cast<uint32_t>(p.seed), s1 = static_cast<uint32_t>(p.seed >> 32);
+  const uint32_t o0 = static_cast<uint32_t>(p.offset), o1 = static_cast<uint32_t>(p.offset >> 32);
+  return mix32(s0 ^ mix32(s1 + 0x9e3779b9u * static_cast<uint32_t>(bh + 1)) ^ mix32(o0 ^ mix32(o1 + 0x85ebca6bu)));
+}
+
+template <typename T>
+__device__ __forceinline__ typename MF<T>::e8 ld8(const uint16_t* p) {
+  return __builtin_bit_cast(typename MF<T>::e8, *reinterpret_cast<const s16x8*>(p));
+}
+
+// ------------------------------------------------------- XCD-aware block mapping
+// Workgroups are dealt round-robin to the 8 XCDs (each with its own 4 MB L2).  A 1-D grid
+// of tiles x (b*h) blocks is mapped so that all tiles of one (b, h) run on the SAME XCD,
+// consecutively: their shared K/V (fwd, dQ) or Q/dO (dK/dV) tiles stay L2-resident
+// instead of being fetched by all 8 XCDs.  Heads beyond the last multiple of 8 fall back
+// to the linear order.
+__device__ __forceinline__ void xcd_map(int ntiles, int64_t nbh, int& tile, int64_t& bh) {
+  const int64_t L = blockIdx.x;
+  const int64_t full = (nbh / 8) * 8 * ntiles;
+  if (L < full) {
+    const int64_t xcd = L % 8, j = L / 8;
+    bh = xcd + 8 * (j / ntiles);
+    tile = static_cast<int>(j % ntiles);
+  } else {
+    const int64_t r = L - full;
+    bh = (nbh / 8) * 8 + r / ntiles;
+    tile = static_cast<int>(r % ntiles);
+  }
+}
+
+// ------------------------------------------------------------------ LDS tiles
+// Tiles are stored unpadded, [rows][D] bf16, with the 16-byte chunks of each row XOR-
+// swizzled so that BOTH access patterns are bank-conflict free:
+//  * row reads (ds_read_b128, lane = row, 16 rows per LDS cycle group), and
+//  * transposed reads (ds_read_b64_tr_b16: 4 rows x 32 columns per 32-lane group).
+// D = 64 (128-B rows, two rows per 64-bank line): chunk' = chunk ^ (bit1(row)<<2 | bits2-3(row)).
+// D = 128 (256-B rows, one row per line):        chunk' = chunk ^ (bits0-1(row)<<2 | bits2-3(row)).
+// D >= 128 rows (and D = 96 stored at stride 128): chunk' = chunk ^ (bits0-1(row)<<2 | bits2-3(row)).
+template <int D>
+__device__ __forceinline__ int swz(int row, int chunk) {
+  constexpr int DS = LdsStride<D>::v;
+  const int g = DS == 64 ? ((((row >> 1) & 1) << 2) | ((row >> 2) & 3)) : (((row & 3) << 2) | ((row >> 2) & 3));
+  return row * DS + ((chunk ^ g) << 3);
+}
+
+// Per-lane LDS element offsets, swizzle resolved ONCE per kernel (the swizzle depends on
+// row bits 0-3 only, so rows +16/+32/+64 are immediate offsets of these bases).
+//  * RowOff: A/B operand row reads -- row (lane & 31) [+32 j], chunk 2t + (lane >> 5);
+//  * TrOff: transposed reads -- lane 4q+p of each 16-lane group supplies row q (and q + 8)
+//    at columns c0 + 4p..4p+3, c0 = 32 i + 16 * bit4(lane), rows based at 4 * (lane >> 5).
+template <int D>
+struct RowOff {
+  int o[D / 16];
+  __device__ __forceinline__ RowOff(int r, int hh) {
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) o[t] = swz<D>(r, 2 * t + hh);
+  }
+};
+
+template <int D, int NI = D / 32>
+struct TrOff {
+  int lo[NI], hi[NI];
+  // col0: first output column (dK/dV split into column halves for D = 256)
+  __device__ __forceinline__ explicit TrOff(int lane, int col0 = 0) {
+    const int q = (lane & 15) >> 2, pp = lane & 3, hh = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int col = col0 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
+      lo[i] = swz<D>(4 * hh + q, col >> 3) + (col & 7);
+      hi[i] = swz<D>(4 * hh + 8 + q, col >> 3) + (col & 7);
+    }
+  }
+};
+
+// Transposed fetch: elements j=0..3 <- rows k0..k0+3, j=4..7 <- rows k0+8..k0+11 (k0 folded
+// into the offsets), one ds_read_b64_tr_b16 per half.
+template <typename T>
+__device__ __forceinline__ typename MF<T>::e8 ld_tr(const uint16_t* tile, int off_lo, int off_hi) {
+  s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_lo));
+  s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_hi));
+  s16x8 v = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+  return __builtin_bit_cast(typename MF<T>::e8, v);
+}
+
+// Accumulator rows 8s..8s+7 -> one 8-element operand fragment (k-step s of a 32-row tile).
+template <typename T>
+__device__ __forceinline__ typename MF<T>::e8 pack8(const f32x16& a, int s) {
+  typename MF<T>::e8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = MF<T>::cvt(a[8 * s + j]);
+  return r;
+}
+
+__device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 * (reg >> 2) + 4 * hh; }
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// fmaxf on MFMA results makes clang insert a canonicalising v_max per operand; scores are
+// never signalling NaNs, so issue v_max3 directly (2 elements per instruction).
+// hipcc does not pad hazards for an asm statement: an MFMA result read by this VALU needs
+// the XDL->VALU wait states first -- mfma_ready() below provides them.
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  float d;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// Wait states between the last MFMA writing `a`/`b` and an inline-asm VALU reading them
+// (8-pass XDL -> VALU: 12 states; 16 given).  The "+v" operands pin the order: the MFMAs
+// complete-issue before it, every reader comes after.  Without it v_max3 read stale
+// accumulator values on some waves (non-deterministic row maxima, 1-ulp output jitter).
+__device__ __forceinline__ void mfma_ready(f32x16& a, f32x16& b) {
+  asm volatile("s_nop 15" : "+v"(a), "+v"(b));
+}
+
+// value of lane ^ 32 (the other half-wave) without an LDS round trip
+__device__ __forceinline__ float xor32(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const int lane = threadIdx.x & 63;
+  return __builtin_bit_cast(float, lane < 32 ? r[1] : r[0]);
+}
+
+// Register-staged tile copy (issue global loads early, write LDS late: the HBM/L2 latency
+// hides under the MFMA work of the current tile).
+template <int D, int ROWS>
+struct Stage {
+  static constexpr int CH = D / 8;
+  static constexpr int N = ROWS * CH / kThreads;
+  static_assert(N * kThreads == ROWS * CH, "tile must split evenly over the block");
+  // rows advance by RS per register; when RS is a multiple of 16 the swizzle pattern (row
+  // bits 0-3) repeats and every LDS / global offset is base + compile-time/scalar step, so
+  // only one lane offset pair lives in VGPRs (D = 64, 128); D = 256 (RS = 8) alternates two
+  // patterns; D = 96 keeps per-register offsets.
+  static constexpr int RS = (kThreads % CH == 0) ? kThreads / CH : 0;
+  static constexpr int NB = (RS > 0 && RS % 16 == 0) ? 1 : ((RS > 0 && (2 * RS) % 16 == 0) ? 2 : N);
+  uint4 v[N];
+  int goff0, row0;
+  int loffb[NB];
+  int goffa[RS > 0 ? 1 : N], rowa[RS > 0 ? 1 : N];
+  int64_t gs_;
+  __device__ __forceinline__ explicit Stage(int64_t gs) : gs_(gs) {
+    if constexpr (RS > 0) {
+      const int r = threadIdx.x / CH, k = threadIdx.x % CH;
+      row0 = r;
+      goff0 = static_cast<int>(r * gs) + k * 8;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) loffb[i] = swz<D>(r + i * RS, k);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int c = threadIdx.x + i * kThreads, r = c / CH, k = c % CH;
+        rowa[i] = r;
+        goffa[i] = static_cast<int>(r * gs) + k * 8;
+        loffb[i] = swz<D>(r, k);
+      }
+    }
+  }
+  __device__ __forceinline__ int goff(int i) const {
+    if constexpr (RS > 0)
+      return goff0 + static_cast<int>(i * RS * gs_);
+    else
+      return goffa[i];
+  }
+  __device__ __forceinline__ int row(int i) const {
+    if constexpr (RS > 0)
+      return row0 + i * RS;
+    else
+      return rowa[i];
+  }
+  __device__ __forceinline__ int loff(int i) const {
+    constexpr int DS = LdsStride<D>::v;
+    if constexpr (RS > 0)
+      return loffb[i % NB] + (i / NB) * NB * RS * DS;
+    else
+      return loffb[i];
+  }
+  // tile: pointer to the tile's first row; rows >= valid read as zeros
+  __device__ __forceinline__ void load(const uint16_t* tile, int valid) {
+    if (valid >= ROWS) {  // wave-uniform: interior tiles load without per-lane predication
+#pragma unroll
+      for (int i = 0; i < N; ++i) v[i] = *reinterpret_cast<const uint4*>(tile + goff(i));
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      v[i] = row(i) < valid ? *reinterpret_cast<const uint4*>(tile + goff(i)) : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void store(uint16_t* lds) const {
+#pragma unroll
+    for (int i = 0; i < N; ++i) *reinterpret_cast<uint4*>(lds + loff(i)) = v[i];
+  }
+};
+
+template <typename T, int D, int NI = D / 32>
+__device__ __forceinline__ void store_rows(uint16_t* dst, const f32x16* acc, float mul, int hh) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 32 * i + 8 * g + 4 * hh;
+      s16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = __builtin_bit_cast(short, MF<T>::cvt(acc[i][4 * g + j] * mul));
+      *reinterpret_cast<s16x4*>(dst + d0) = w;
+    }
+  }
+}
+
+// Stages the (bias / scale) values of a 64-key tile: thread t < 64 holds key kv0 + t.
+__device__ __forceinline__ float load_bias(const AttnParams& p, int64_t b, int key, float inv_scale) {
+  return key < p.sk ? p.kbias[b * p.kbias_sb + key] * inv_scale : 0.f;
+}
+
+// Accumulator init for a transposed score tile (key rows in registers): bias of the
+// register's key, 4 consecutive keys per float4 (acc_row(4g..4g+3) = 8g + 4hh + 0..3).
+__device__ __forceinline__ void init_from_keys(f32x16& a, const float* sB, int hh, float add) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float4 v = *reinterpret_cast<const float4*>(&sB[8 * g + 4 * hh]);
+    a[4 * g + 0] = v.x + add;
+    a[4 * g + 1] = v.y + add;
+    a[4 * g + 2] = v.z + add;
+    a[4 * g + 3] = v.w + add;
+  }
+}
+
+// Dropout for a transposed tile (query on the lane, 16 keys in registers starting at key
+// `kbase` (even)): register pairs (2j, 2j+1) are the key pairs kbase/2 + acc_row(2j)/2.
+__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t thr16,
+                                          float keepval_scale, bool scale_kept) {
+#pragma unroll
+  for (int reg = 0; reg < 16; reg += 2) {
+    const uint32_t kp = static_cast<uint32_t>(kbase >> 1) + static_cast<uint32_t>(acc_row(reg, hh) >> 1);
+    const uint32_t hsh = mix32(key ^ (qbase + kp));
+    const float k0 = scale_kept ? a[reg] * keepval_scale : a[reg];
+    const float k1 = scale_kept ? a[reg + 1] * keepval_scale : a[reg + 1];
+    a[reg] = (hsh << 16) >= thr16 ? k0 : 0.f;
+    a[reg + 1] = hsh >= thr16 ? k1 : 0.f;
+  }
+}
+
+// ================================================================== forward
+// Block = 4 waves x 32 queries; K/V tiles of 64 keys.  Interior tiles (every key visible
+// to every query of the wave) take a mask-free path.
+// D = 256: the wave's Q fragments (64 VGPRs) live in LDS instead of registers, so the O
+// accumulator, the K/V prefetch and the softmax state fit one wave's register file.
+template <int D>
+struct QInLds {
+  static constexpr bool v = D >= 256;
+};
+
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
+__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
+  constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
+  constexpr bool QLDS = QInLds<D>::v;
+  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * DS];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * DS];
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[QLDS ? BM * DS : 8];
+  __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
+  int tile;
+  int64_t bh;
+  xcd_map(nqb, p.b * p.h, tile, bh);
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;  // heaviest causal blocks first
+  const int q0 = qb * BM + wave * 32;
+  const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
+  const int diag = sk - sq;  // key index allowed up to query + diag
+  const int win = p.window;
+
+  const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
+  const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
+  const uint16_t* V = static_cast<const uint16_t*>(p.v) + b * p.v_sb + h * p.v_sh;
+
+  typename MF<T>::e8 qf[QLDS ? 1 : D / 16];
+  const int qrow = q0 + r;
+  if constexpr (QLDS) {
+    // the block's 128 query rows -> swizzled LDS image (read back per MFMA like K)
+    Stage<D, BM> stQ(p.q_ss);
+    stQ.load(Q + static_cast<int64_t>(qb * BM) * p.q_ss, sq - qb * BM);
+    stQ.store(sQ);
+  } else {
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+      if (qrow < sq) {
+        qf[t] = ld8<T>(Q + static_cast<int64_t>(qrow) * p.q_ss + 16 * t + 8 * hh);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[t][j] = MF<T>::cvt(0.f);
+      }
+    }
+  }
+  const float sl2 = p.scale * kLog2e;
+  const float inv_scale = 1.f / p.scale;
+  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 1) >> 1);
+  const uint32_t thr16 = p.drop_thr << 16;
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) o[i] = f32x16{0};
+
+  int kv_end = sk, kv_begin = 0;
+  if (CAUSAL) {
+    const int lim = (qb + 1) * BM + diag;
+    kv_end = lim < sk ? lim : sk;
+  }
+  if (win > 0) {
+    const int lo = qb * BM + diag - win + 1;
+    kv_begin = lo > 0 ? (lo / BN) * BN : 0;
+  }
+  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D> tro(lane);
+  float bstage = 0.f;
+  if (kv_begin < kv_end) {
+    stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
+    stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
+    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x, inv_scale);
+  }
+  const int wave_last_q = q0 + 31;
+  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
+    __syncthreads();
+    stK.store(sK);
+    stV.store(sV);
+    if (BIAS && threadIdx.x < BN) sB[threadIdx.x] = bstage;
+    __syncthreads();
+    if (kv0 + BN < kv_end) {
+      stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
+      stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
+      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x, inv_scale);
+    }
+    if (CAUSAL && kv0 > wave_last_q + diag) continue;
+    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
+    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
+                          (win <= 0 || kv0 > wave_last_q + diag - win);
+    f32x16 s0, s1;
+    if (BIAS) {
+      init_from_keys(s0, sB, hh, 0.f);
+      init_from_keys(s1, sB + 32, hh, 0.f);
+    } else {
+      s0 = f32x16{0};
+      s1 = f32x16{0};
+    }
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+      const typename MF<T>::e8 qt = QLDS ? ld8<T>(sQ + ro.o[t] + wave * 32 * DS) : qf[t];
+      s0 = MF<T>::mma(ld8<T>(sK + ro.o[t]), qt, s0);
+      s1 = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * DS), qt, s1);
+    }
+    mfma_ready(s0, s1);
+    if (!interior) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k0 = kv0 + acc_row(reg, hh);
+        const int k1 = k0 + 32;
+        if (k0 >= sk || (CAUSAL && k0 > qrow + diag) || (win > 0 && k0 <= qrow + diag - win)) s0[reg] = -INFINITY;
+        if (k1 >= sk || (CAUSAL && k1 > qrow + diag) || (win > 0 && k1 <= qrow + diag - win)) s1[reg] = -INFINITY;
+      }
+    }
+    // raw-score row max (scale > 0 keeps the order), two independent v_max3 chains
+    float mx0 = max3(s0[0], s1[0], s0[1]), mx1 = max3(s1[1], s0[2], s1[2]);
+#pragma unroll
+    for (int reg = 3; reg < 15; reg += 2) {
+      mx0 = max3(mx0, s0[reg], s1[reg]);
+      mx1 = max3(mx1, s0[reg + 1], s1[reg + 1]);
+    }
+    float mx = max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2;
+    mx = fmaxf(mx, xor32(mx));
+    const float m_new = fmaxf(m_i, mx);
+    const float m_use = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
+    const float alpha = fast_exp2(m_i - m_use);
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float e0 = fast_exp2(fmaf(s0[reg], sl2, -m_use));
+      const float e1 = fast_exp2(fmaf(s1[reg], sl2, -m_use));
+      s0[reg] = e0;
+      s1[reg] = e1;
+      rs0 += e0;
+      rs1 += e1;
+    }
+    float rs = rs0 + rs1;
+    rs += xor32(rs);
+    l_i = l_i * alpha + rs;
+    if (__any(m_new != m_i)) {  // rescale only when a row max moved
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
+    }
+    m_i = m_new;
+    if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
+      drop_tile(s0, dkey, qbase, kv0, hh, thr16, 1.f, false);
+      drop_tile(s1, dkey, qbase, kv0 + 32, hh, thr16, 1.f, false);
+    }
+    typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
+#pragma unroll
+    for (int i = 0; i < D / 32; ++i) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
+    }
+  }
+  if (qrow >= sq) return;
+  const float inv = l_i > 0.f ? (DROP ? p.drop_rs : 1.f) / l_i : 0.f;
+  uint16_t* O = static_cast<uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh + static_cast<int64_t>(qrow) * p.o_ss;
+  store_rows<T, D>(O, o, inv, hh);
+  if (hh == 0) p.lse[bh * p.sq + qrow] = (l_i > 0.f) ? (m_i + log2f(l_i)) / kLog2e : -INFINITY;
+}
+
+// ============================================================= delta = rowsum(dO * O)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) attn_delta_kernel(AttnBwdParams p) {
+  // 16 lanes per (b, h, query) row, 8 elements per lane per step (16-byte loads)
+  const int sub = threadIdx.x & 15;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
+  const int64_t total = p.f.b * p.f.h * p.f.sq;
+  const bool valid = row < total;
+  float acc = 0.f;
+  if (valid) {
+    const int64_t q = row % p.f.sq, bh = row / p.f.sq, b = bh / p.f.h, h = bh % p.f.h;
+    const T* O = static_cast<const T*>(p.f.o) + b * p.f.o_sb + h * p.f.o_sh + q * p.f.o_ss;
+    const T* dO = static_cast<const T*>(p.dout) + b * p.do_sb + h * p.do_sh + q * p.do_ss;
+    for (int d = sub * 8; d < p.f.d; d += 128) {
+      Vec16<T> a = load16<T>(O + d), g = load16<T>(dO + d);
+#pragma unroll
+      for (int j = 0; j < Vec16<T>::N; ++j) acc += to_f32(a.v[j]) * to_f32(g.v[j]);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (valid && sub == 0) p.delta[row] = acc;
+}
+
+// ===================================================================== dK / dV
+// Block = 4 waves x 32 keys (key on the MFMA lane); Q/dO tiles of 64 queries, two 32-query
+// sub-steps.  S and dP accumulators start from the per-query row constants
+// (-lse*log2e/(scale*log2e) [+ key bias / scale], -delta), so p = exp2(S' * scale*log2e)
+// and dS = p * dP' (with dropout the delta is applied after the keep mask).
+// D = 256: the dK/dV output columns are split over two blocks (NSPLIT), each recomputing S
+// and dP in full -- 256 accumulator registers for a whole 32-key x 256 dK/dV pair do not fit
+// beside the K/V fragments.
+template <int D>
+struct DkdvSplit {
+  static constexpr int v = D >= 256 ? 2 : 1;
+};
+
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
+__global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kernel(AttnBwdParams P) {
+  constexpr int BKEYS = 128, BQ = 64, DS = LdsStride<D>::v;
+  constexpr int NSPLIT = DkdvSplit<D>::v, DO = D / NSPLIT;
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[BQ * DS];
+  __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * DS];
+  __shared__ __attribute__((aligned(16))) float sL[BQ], sDl[BQ];
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  int kb;
+  int64_t bh;
+  xcd_map(static_cast<int>((p.sk + BKEYS - 1) / BKEYS) * NSPLIT, p.b * p.h, kb, bh);
+  const int col0 = (kb % NSPLIT) * DO;  // first dK/dV column of this block
+  kb /= NSPLIT;
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
+  const int win = p.window;
+  const int k0w = kb * BKEYS + wave * 32;  // wave's first key
+  const int krow = k0w + r;                // this lane's key (as B-operand column)
+
+  const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
+  const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
+  const uint16_t* V = static_cast<const uint16_t*>(p.v) + b * p.v_sb + h * p.v_sh;
+  const uint16_t* dO = static_cast<const uint16_t*>(P.dout) + b * P.do_sb + h * P.do_sh;
+  const float* LSE = p.lse + bh * p.sq;
+  const float* DL = P.delta + bh * p.sq;
+
+  typename MF<T>::e8 kf[D / 16], vf[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) {
+    if (krow < sk) {
+      kf[t] = ld8<T>(K + static_cast<int64_t>(krow) * p.k_ss + 16 * t + 8 * hh);
+      vf[t] = ld8<T>(V + static_cast<int64_t>(krow) * p.v_ss + 16 * t + 8 * hh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        kf[t][j] = MF<T>::cvt(0.f);
+        vf[t][j] = MF<T>::cvt(0.f);
+      }
+    }
+  }
+  f32x16 dv[DO / 32], dk[DO / 32];
+#pragma unroll
+  for (int i = 0; i < DO / 32; ++i) dv[i] = dk[i] = f32x16{0};
+  const float sl2 = p.scale * kLog2e;
+  const float inv_sl2 = 1.f / sl2;
+  const float kbias = BIAS ? load_bias(p, b, krow, 1.f / p.scale) : 0.f;
+  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t npairs = static_cast<uint32_t>((sk + 1) >> 1);
+  const uint32_t kpair = static_cast<uint32_t>(krow >> 1);
+  const int kshift = (krow & 1) * 16;
+  const uint32_t thr = p.drop_thr;
+  const float rsd = p.drop_rs;
+  int q_start = 0, q_end = sq;
+  if (CAUSAL) {
+    q_start = kb * BKEYS - diag;
+    q_start = q_start < 0 ? 0 : (q_start / BQ) * BQ;
+  }
+  if (win > 0) {
+    const int hi = (kb + 1) * BKEYS - 1 - diag + win;  // last query that sees the block's last key
+    q_end = hi + 1 < sq ? hi + 1 : sq;
+  }
+  Stage<D, BQ> stQ(p.q_ss), stO(P.do_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D, DO / 32> tro(lane, col0);
+  float l_stage = 0.f, d_stage = 0.f;
+  if (q_start < q_end) {
+    stQ.load(Q + static_cast<int64_t>(q_start) * p.q_ss, sq - q_start);
+    stO.load(dO + static_cast<int64_t>(q_start) * P.do_ss, sq - q_start);
+    if (threadIdx.x < BQ) {
+      const int qq = q_start + threadIdx.x;
+      l_stage = qq < sq ? LSE[qq] : 0.f;
+      d_stage = qq < sq ? DL[qq] : 0.f;
+    }
+  }
+  const int klast = k0w + 31;
+  for (int qt = q_start; qt < q_end; qt += BQ) {
+    __syncthreads();
+    stQ.store(sQ);
+    stO.store(sdO);
+    if (threadIdx.x < BQ) {
+      // lse == -inf (fully masked row) contributes nothing: any finite constant works
+      sL[threadIdx.x] = l_stage == -INFINITY ? 0.f : -l_stage * kLog2e * inv_sl2;
+      sDl[threadIdx.x] = -d_stage;
+    }
+    __syncthreads();
+    if (qt + BQ < q_end) {
+      stQ.load(Q + static_cast<int64_t>(qt + BQ) * p.q_ss, sq - qt - BQ);
+      stO.load(dO + static_cast<int64_t>(qt + BQ) * P.do_ss, sq - qt - BQ);
+      if (threadIdx.x < BQ) {
+        const int qq = qt + BQ + threadIdx.x;
+        l_stage = qq < sq ? LSE[qq] : 0.f;
+        d_stage = qq < sq ? DL[qq] : 0.f;
+      }
+    }
+#pragma unroll 1
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qs = qt + 32 * sub;  // first query of this sub-step
+      if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
+      if (win > 0 && qs + diag - win + 1 > klast) continue;  // all keys left the window
+      const bool interior = qs + 31 < sq && klast < sk && (!CAUSAL || klast <= qs + diag) &&
+                            (win <= 0 || k0w > qs + 31 + diag - win);
+      // S' = Q K^T - lse/scale [+ bias/scale], dP' = dO V^T - delta (query rows in regs, key on lane)
+      f32x16 s, dp, ndl;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 lv = *reinterpret_cast<const float4*>(&sL[32 * sub + 8 * g + 4 * hh]);
+        const float4 dv4 = *reinterpret_cast<const float4*>(&sDl[32 * sub + 8 * g + 4 * hh]);
+        s[4 * g + 0] = lv.x + kbias; s[4 * g + 1] = lv.y + kbias; s[4 * g + 2] = lv.z + kbias; s[4 * g + 3] = lv.w + kbias;
+        if (DROP) {
+          ndl[4 * g + 0] = dv4.x; ndl[4 * g + 1] = dv4.y; ndl[4 * g + 2] = dv4.z; ndl[4 * g + 3] = dv4.w;
+          dp[4 * g + 0] = dp[4 * g + 1] = dp[4 * g + 2] = dp[4 * g + 3] = 0.f;
+        } else {
+          dp[4 * g + 0] = dv4.x; dp[4 * g + 1] = dv4.y; dp[4 * g + 2] = dv4.z; dp[4 * g + 3] = dv4.w;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < D / 16; ++t) {
+        s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * DS), kf[t], s);
+        dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * DS), vf[t], dp);
+      }
+      auto finish = [&](float pv, int reg, int qq) {
+        if (DROP) {
+          const uint32_t hsh = mix32(dkey ^ (static_cast<uint32_t>(qq) * npairs + kpair));
+          const float z = ((hsh >> kshift) & 0xffffu) >= thr ? rsd : 0.f;
+          s[reg] = pv * z;                             // (P o Z) for dV
+          dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
+        } else {
+          s[reg] = pv;
+          dp[reg] *= pv;
+        }
+      };
+      if (interior) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) finish(fast_exp2(s[reg] * sl2), reg, qs + acc_row(reg, hh));
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int qq = qs + acc_row(reg, hh);
+          float pv = fast_exp2(s[reg] * sl2);
+          if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win))
+            pv = 0.f;
+          finish(pv, reg, qq);
+        }
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
+      typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
+      typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
+#pragma unroll
+      for (int i = 0; i < DO / 32; ++i) {
+        const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
+      }
+    }
+  }
+  if (krow >= sk) return;
+  uint16_t* dK = static_cast<uint16_t*>(P.dk) + b * P.dk_sb + h * P.dk_sh + static_cast<int64_t>(krow) * P.dk_ss;
+  uint16_t* dV = static_cast<uint16_t*>(P.dv) + b * P.dv_sb + h * P.dv_sh + static_cast<int64_t>(krow) * P.dv_ss;
+  store_rows<T, D, DO / 32>(dK + col0, dk, p.scale, hh);
+  store_rows<T, D, DO / 32>(dV + col0, dv, 1.f, hh);
+}
+
+// ========================================================================= dQ
+// Block = 4 waves x 32 queries (query on the lane: S^T = K Q^T, dP^T = V dO^T); K/V tiles
+// of 64 keys; dQ^T += K^T dS^T with K^T from transposed LDS reads.
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
+__global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(AttnBwdParams P) {
+  constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
+  constexpr int NSPLIT = DkdvSplit<D>::v, DO = D / NSPLIT;  // dQ columns per block
+  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * DS];
+  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * DS];
+  __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
+  int tile;
+  int64_t bh;
+  xcd_map(nqb * NSPLIT, p.b * p.h, tile, bh);
+  const int col0 = (tile % NSPLIT) * DO;
+  tile /= NSPLIT;
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;
+  const int q0 = qb * BM + wave * 32;
+  const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk), diag = sk - sq;
+  const int win = p.window;
+  const int qrow = q0 + r;
+  const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
+  const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
+  const uint16_t* V = static_cast<const uint16_t*>(p.v) + b * p.v_sb + h * p.v_sh;
+  const uint16_t* dO = static_cast<const uint16_t*>(P.dout) + b * P.do_sb + h * P.do_sh;
+
+  typename MF<T>::e8 qf[D / 16], df[D / 16];
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) {
+    if (qrow < sq) {
+      qf[t] = ld8<T>(Q + static_cast<int64_t>(qrow) * p.q_ss + 16 * t + 8 * hh);
+      df[t] = ld8<T>(dO + static_cast<int64_t>(qrow) * P.do_ss + 16 * t + 8 * hh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        qf[t][j] = MF<T>::cvt(0.f);
+        df[t][j] = MF<T>::cvt(0.f);
+      }
+    }
+  }
+  float lse = qrow < sq ? p.lse[bh * p.sq + qrow] : 0.f;
+  if (lse == -INFINITY) lse = 0.f;  // fully masked row: every p is masked to 0 below
+  const float sl2 = p.scale * kLog2e;
+  const float inv_scale = 1.f / p.scale;
+  const float s_init = -lse * kLog2e / sl2;
+  const float dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
+  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 1) >> 1);
+  const uint32_t thr16 = p.drop_thr << 16;
+  f32x16 dq[DO / 32];
+#pragma unroll
+  for (int i = 0; i < DO / 32; ++i) dq[i] = f32x16{0};
+  int kv_end = sk, kv_begin = 0;
+  if (CAUSAL) {
+    const int lim = (qb + 1) * BM + diag;
+    kv_end = lim < sk ? lim : sk;
+  }
+  if (win > 0) {
+    const int lo = qb * BM + diag - win + 1;
+    kv_begin = lo > 0 ? (lo / BN) * BN : 0;
+  }
+  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
+  const RowOff<D> ro(r, hh);
+  const TrOff<D, DO / 32> tro(lane, col0);
+  float bstage = 0.f;
+  if (kv_begin < kv_end) {
+    stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
+    stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
+    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x, inv_scale);
+  }
+  const int wave_last_q = q0 + 31;
+  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
+    __syncthreads();
+    stK.store(sK);
+    stV.store(sV);
+    if (BIAS && threadIdx.x < BN) sB[threadIdx.x] = bstage;
+    __syncthreads();
+    if (kv0 + BN < kv_end) {
+      stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
+      stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
+      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x, inv_scale);
+    }
+    if (CAUSAL && kv0 > wave_last_q + diag) continue;
+    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
+    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
+                          (win <= 0 || kv0 > wave_last_q + diag - win);
+    // D <= 128: both 32-key halves' dS^T, then the dQ MFMAs (the two halves' MFMA chains
+    // overlap each other's softmax VALU work).  D = 256: half by half, so only one half's
+    // S / dP accumulators are live next to the 16 Q / dO fragments.
+    constexpr bool SEQ = D >= 256;
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (BIAS) {
+        init_from_keys(s[u], sB + 32 * u, hh, s_init);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s[u][j] = s_init;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dp[u][j] = DROP ? 0.f : -dl;
+#pragma unroll
+      for (int t = 0; t < D / 16; ++t) {
+        s[u] = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * u * DS), qf[t], s[u]);
+        dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[t] + 32 * u * DS), df[t], dp[u]);
+      }
+      if (DROP) {
+        // dp <- Z o dP (raw), then dS = P o (Z o dP - delta)
+        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, thr16, p.drop_rs, true);
+      }
+      if (interior) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const float pv = fast_exp2(s[u][reg] * sl2);
+          dp[u][reg] = DROP ? pv * (dp[u][reg] - dl) : dp[u][reg] * pv;  // dS^T
+        }
+      } else {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          float pv = fast_exp2(s[u][reg] * sl2);
+          const int kk = kv0 + 32 * u + acc_row(reg, hh);
+          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win))
+            pv = 0.f;
+          dp[u][reg] = DROP ? pv * (dp[u][reg] - dl) : dp[u][reg] * pv;
+        }
+      }
+      if (SEQ) {
+        const typename MF<T>::e8 sf0 = pack8<T>(dp[u], 0), sf1 = pack8<T>(dp[u], 1);
+#pragma unroll
+        for (int i = 0; i < DO / 32; ++i) {
+          const int a0 = 32 * u * DS, a1 = (32 * u + 16) * DS;
+          dq[i] = MF<T>::mma(ld_tr<T>(sK, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dq[i]);
+          dq[i] = MF<T>::mma(ld_tr<T>(sK, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dq[i]);
+        }
+      }
+    }
+    if (!SEQ) {
+      typename MF<T>::e8 sf[4] = {pack8<T>(dp[0], 0), pack8<T>(dp[0], 1), pack8<T>(dp[1], 0), pack8<T>(dp[1], 1)};
+#pragma unroll
+      for (int i = 0; i < DO / 32; ++i) {
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          dq[i] = MF<T>::mma(ld_tr<T>(sK, tro.lo[i] + 16 * st * DS, tro.hi[i] + 16 * st * DS), sf[st], dq[i]);
+      }
+    }
+  }
+  if (qrow >= sq) return;
+  uint16_t* dQ = static_cast<uint16_t*>(P.dq) + b * P.dq_sb + h * P.dq_sh + static_cast<int64_t>(qrow) * P.dq_ss;
+  store_rows<T, D, DO / 32>(dQ + col0, dq, p.scale, hh);
+}
+
+// ------------------------------------------------------------------ launchers
+template <typename T, int D, bool C, bool DR, bool BI>
+int launch_fwd_v(const AttnParams& p, hipStream_t s) {
+  const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
+  attn_fwd_kernel<T, D, C, DR, BI><<<grid, kThreads, 0, s>>>(p);
+  return static_cast<int>(hipGetLastError());
+}
+
+template <typename T, int D, bool C, bool DR, bool BI>
+int launch_bwd_v(const AttnBwdParams& p, hipStream_t s) {
+  const int64_t rows = p.f.b * p.f.h * p.f.sq;
+  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
+  const unsigned gk = static_cast<unsigned>(((p.f.sk + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
+  const unsigned gq = static_cast<unsigned>(((p.f.sq + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
+  attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
+  attn_bwd_dq_kernel<T, D, C, DR, BI><<<gq, kThreads, 0, s>>>(p);
+  return static_cast<int>(hipGetLastError());
+}
+
+// runtime flags -> template variant
+template <typename T, int D>
+int launch_fwd(const AttnParams& p, hipStream_t s) {
+  const bool dr = p.drop_thr > 0, bi = p.kbias != nullptr;
+  const int v = (p.causal ? 4 : 0) | (dr ? 2 : 0) | (bi ? 1 : 0);
+  switch (v) {
+    case 0: return launch_fwd_v<T, D, false, false, false>(p, s);
+    case 1: return launch_fwd_v<T, D, false, false, true>(p, s);
+    case 2: return launch_fwd_v<T, D, false, true, false>(p, s);
+    case 3: return launch_fwd_v<T, D, false, true, true>(p, s);
+    case 4: return launch_fwd_v<T, D, true, false, false>(p, s);
+    case 5: return launch_fwd_v<T, D, true, false, true>(p, s);
+    case 6: return launch_fwd_v<T, D, true, true, false>(p, s);
+    default: return launch_fwd_v<T, D, true, true, true>(p, s);
+  }
+}
+
+template <typename T, int D>
+int launch_bwd(const AttnBwdParams& p, hipStream_t s) {
+  const bool dr = p.f.drop_thr > 0, bi = p.f.kbias != nullptr;
+  const int v = (p.f.causal ? 4 : 0) | (dr ? 2 : 0) | (bi ? 1 : 0);
+  switch (v) {
+    case 0: return launch_bwd_v<T, D, false, false, false>(p, s);
+    case 1: return launch_bwd_v<T, D, false, false, true>(p, s);
+    case 2: return launch_bwd_v<T, D, false, true, false>(p, s);
+    case 3: return launch_bwd_v<T, D, false, true, true>(p, s);
+    case 4: return launch_bwd_v<T, D, true, false, false>(p, s);
+    case 5: return launch_bwd_v<T, D, true, false, true>(p, s);
+    case 6: return launch_bwd_v<T, D, true, true, false>(p, s);
+    default: return launch_bwd_v<T, D, true, true, true>(p, s);
+  }
+}
+
+}  // namespace attn
+
+// Instantiates the per-head-dim entry points (one translation unit per head dim, so the
+// 2 dtypes x 8 variants x 3 kernels build in parallel).
+#define SMPK_ATTN_HEAD_DIM(D)                                                   \
+  int attention_fwd_d##D(int dt, const AttnParams& p, hipStream_t s) {          \
+    if (dt == BF16) return attn::launch_fwd<bf16, D>(p, s);                     \
+    if (dt == F16) return attn::launch_fwd<f16, D>(p, s);                       \
+    return -3;                                                                  \
+  }                                                                             \
+  int attention_bwd_d##D(int dt, const AttnBwdParams& p, hipStream_t s) {       \
+    if (dt == BF16) return attn::launch_bwd<bf16, D>(p, s);                     \
+    if (dt == F16) return attn::launch_bwd<f16, D>(p, s);                       \
+    return -3;                                                                  \
+  }
+
+}  // namespace smpk

@@ -398,18 +398,20 @@ void check_bshd(const at::Tensor& t, const char* n) {
 }
 
 smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool causal,
-                             int64_t window) {
+                             int64_t window, const c10::optional<at::Tensor>& kbias, double dropout_p, int64_t seed,
+                             int64_t offset) {
   check_bshd(q, "q");
   check_bshd(k, "k");
   check_bshd(v, "v");
   TORCH_CHECK(k.sizes() == v.sizes() && q.size(0) == k.size(0) && q.size(2) == k.size(2) && q.size(3) == k.size(3),
               "attention: q/k/v shape mismatch");
   TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attention: dtype mismatch");
-  TORCH_CHECK(q.size(3) == 64 || q.size(3) == 128, "attention kernel supports head_dim 64 and 128");
+  TORCH_CHECK(smpk::attention_head_dim_supported(q.size(3)), "attention kernel supports head_dim 64, 96, 128, 256");
   for (const at::Tensor* t : {&q, &k, &v})
     TORCH_CHECK((reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0 && t->stride(1) % 8 == 0 && t->stride(2) % 8 == 0 &&
                     t->stride(0) % 8 == 0,
                 "attention: operands must be 16-byte aligned");
+  TORCH_CHECK(q.size(1) < (1 << 24) && k.size(1) < (1 << 24), "attention: sequence too long");
   smpk::AttnParams p{};
   p.q = q.data_ptr();
   p.k = k.data_ptr();
@@ -425,12 +427,30 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
   p.scale = static_cast<float>(scale);
   p.causal = causal ? 1 : 0;
   p.window = static_cast<int>(window);
+  if (kbias.has_value() && kbias->defined()) {
+    const at::Tensor& kb = *kbias;
+    TORCH_CHECK(kb.is_cuda() && kb.scalar_type() == at::kFloat && kb.dim() == 2 && kb.stride(1) == 1 &&
+                    kb.size(1) == p.sk && (kb.size(0) == p.b || kb.size(0) == 1),
+                "attention: key bias must be a float32 [b or 1, sk] GPU tensor with contiguous rows");
+    p.kbias = kb.data_ptr<float>();
+    p.kbias_sb = kb.size(0) == 1 ? 0 : kb.stride(0);
+  }
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention: dropout_p must be in [0, 1)");
+  if (dropout_p > 0.0) {
+    // dropped iff the element's 16-bit uniform < thr: keep probability 1 - thr / 65536
+    uint32_t thr = static_cast<uint32_t>(dropout_p * 65536.0 + 0.5);
+    p.drop_thr = thr < 1 ? 1 : (thr > 65535 ? 65535 : thr);
+    p.drop_rs = static_cast<float>(1.0 / (1.0 - dropout_p));
+    p.seed = static_cast<uint64_t>(seed);
+    p.offset = static_cast<uint64_t>(offset);
+  }
   return p;
 }
 
 std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale, bool causal,
-                                      int64_t window) {
-  auto p = attn_params(q, k, v, scale, causal, window);
+                                      int64_t window, c10::optional<at::Tensor> kbias, double dropout_p, int64_t seed,
+                                      int64_t offset) {
+  auto p = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   auto o = at::empty({p.b, p.sq, p.h, p.d}, q.options());
   auto lse = at::empty({p.b, p.h, p.sq}, q.options().dtype(at::kFloat));
   p.o = o.data_ptr();
@@ -442,9 +462,10 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
 
 // Writes into the provided dq/dk/dv (may be views of one packed gradient buffer).
 void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
-                        at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window) {
+                        at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window,
+                        c10::optional<at::Tensor> kbias, double dropout_p, int64_t seed, int64_t offset) {
   smpk::AttnBwdParams P{};
-  P.f = attn_params(q, k, v, scale, causal, window);
+  P.f = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   check_bshd(dout, "dout");
   check_bshd(o, "o");
   check_bshd(dq, "dq");
@@ -503,6 +524,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ignore_index"), py::arg("vocab") = -1);
   m.def("xent_bwd", &xent_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("grad_rows"),
         py::arg("vocab_start"), py::arg("ignore_index"), py::arg("vocab") = -1);
-  m.def("attention_fwd", &attention_fwd);
-  m.def("attention_bwd_into", &attention_bwd_into);
+  m.def("attention_fwd", &attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"),
+        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(), py::arg("dropout_p") = 0.0,
+        py::arg("seed") = 0, py::arg("offset") = 0);
+  m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
+        py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
+        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(), py::arg("dropout_p") = 0.0,
+        py::arg("seed") = 0, py::arg("offset") = 0);
 }

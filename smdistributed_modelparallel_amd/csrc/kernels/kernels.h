@@ -108,6 +108,11 @@ struct AttnParams {
   float scale;
   int causal;
   int window;  // >0: local attention window (GPT-Neo)
+  const float* kbias;  // optional additive key bias [b, sk] (padding mask); nullptr = none
+  int64_t kbias_sb;    // its batch stride (0: one row shared by the batch)
+  uint32_t drop_thr;   // dropout: element dropped iff its 16-bit uniform < drop_thr (0 = off)
+  float drop_rs;       // 1 / (1 - p)
+  uint64_t seed, offset;
 };
 struct AttnBwdParams {
   AttnParams f;
@@ -123,6 +128,7 @@ struct AttnBwdParams {
   float* dq_acc;  // [b, h, sq, d] fp32 workspace
 };
 int attention_fwd(int dt, const AttnParams& p, hipStream_t s);
+bool attention_head_dim_supported(int64_t d);
 int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);
 
 // ------------------------------------------------------- cross entropy (cross_entropy.hip)

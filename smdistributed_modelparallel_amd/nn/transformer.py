@@ -332,11 +332,12 @@ class DistributedAttentionLayer(DistributedModule):
             qkv = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
-            if not self.rotary_dim and mask is None and not self.attention_in_fp32:
+            if not self.rotary_dim and not self.attention_in_fp32:
                 ctx = attention_packed(
                     qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
                     window=self.window_size, training=self.training,
                     use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
+                    mask=mask, mask_value=getattr(self, "mask_value", -1e4),
                 )
                 out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
                 return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
@@ -349,6 +350,7 @@ class DistributedAttentionLayer(DistributedModule):
             dropout_p=self.attention_dropout_prob, window=self.window_size, training=self.training,
             attention_in_fp32=self.attention_in_fp32,
             use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
+            mask_value=getattr(self, "mask_value", -1e4),
         )
         ctx = ctx.reshape(B, s, lh * d)
         out = linear(ctx, self.dense_weight, self.dense_bias)
@@ -369,14 +371,16 @@ class DistributedAttentionLayer(DistributedModule):
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
             k = apply_rotary(k, self.rotary_dim, base, self.gpt_neox_type_rotary)
-        if not self.rotary_dim and mask is None and not self.attention_in_fp32:
+        mv = getattr(self, "mask_value", -1e4)
+        if not self.rotary_dim and not self.attention_in_fp32:
             ctx = attention_packed(qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
                                    window=self.window_size, training=self.training,
-                                   use_flash=state.cfg.amd_fused_attention)
+                                   use_flash=state.cfg.amd_fused_attention, mask=mask, mask_value=mv)
         else:
             ctx = attention_op(q, k, v, causal=causal, mask=mask, scale=self._scale(),
                                dropout_p=self.attention_dropout_prob, window=self.window_size, training=self.training,
-                               attention_in_fp32=self.attention_in_fp32, use_flash=state.cfg.amd_fused_attention)
+                               attention_in_fp32=self.attention_in_fp32, use_flash=state.cfg.amd_fused_attention,
+                               mask_value=mv)
         out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
         return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
 
@@ -690,9 +694,15 @@ class DistributedTransformerLMHead(DistributedModule):
             cross_states = cross_mask = None
         B, s = input_ids.shape[0], input_ids.shape[1]
         device = input_ids.device
-        position_ids = torch.arange(0, s, dtype=torch.long, device=device).unsqueeze(0).expand(B, -1)
+        if position_ids is None:
+            position_ids = torch.arange(0, s, dtype=torch.long, device=device).unsqueeze(0).expand(B, -1)
+        elif position_ids.shape[0] != B:
+            position_ids = position_ids.expand(B, -1)
+        # 0/1 padding mask (HF convention, 1 = attend) -> True = masked, per key.  It is applied
+        # TOGETHER with the causal mask (the flash kernel takes both; the reference's fused
+        # causal softmax dropped it with a warning, `transformer.py:1684-1696`).
         mask = None
-        if self.causal_mask_size is None and attention_mask is not None:
+        if attention_mask is not None:
             mask = (attention_mask.view(B, -1) == 0).view(B, 1, 1, -1).expand(B, 1, s, s)
 
         prescaled = _prescaled() and self._tp > 1

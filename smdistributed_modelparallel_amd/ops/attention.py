@@ -19,35 +19,98 @@ from . import softmax as _sm
 from ._ext import ext
 
 _FLASH_OK = None
+FLASH_HEAD_DIMS = (64, 96, 128, 256)
 
 
-def flash_supported(q, dropout_p, mask):
+def key_padding_bias(mask, sq, sk, mask_value=-1e4):
+    """A [b|1, 1, sq, sk] bool/uint8 mask (True = masked) that only depends on the key
+    (the usual padding mask, expanded over queries) -> additive float32 bias [b|1, sk];
+    None when the mask varies over queries (the kernel then cannot take it)."""
+    if mask is None:
+        return None
+    if mask.dim() != 4 or mask.shape[1] != 1 or mask.shape[-1] != sk:
+        return None
+    if mask.shape[2] != 1 and mask.stride(2) != 0:
+        if not mask.is_cuda or not bool((mask == mask[:, :, :1]).all()):  # pragma: no cover - rare
+            return None
+    row = mask[:, 0, 0, :]
+    if row.dtype not in (torch.bool, torch.uint8):
+        return row.float().contiguous()  # already additive
+    return torch.zeros(row.shape, dtype=torch.float32, device=row.device).masked_fill_(row.bool(), mask_value)
+
+
+def flash_supported(q, dropout_p=0.0, mask=None, kbias=None):
+    """Flash kernel covers bf16/fp16, head dims 64/96/128/256, in-kernel dropout, causal /
+    sliding-window masks and per-key additive masks (padding)."""
     global _FLASH_OK
-    if not q.is_cuda or dropout_p > 0.0 or mask is not None:
+    if not q.is_cuda or q.dtype not in (torch.bfloat16, torch.float16):
         return False
-    if q.dtype not in (torch.bfloat16, torch.float16):
+    if q.shape[-1] not in FLASH_HEAD_DIMS:
         return False
-    if q.shape[-1] not in (64, 128):
+    if mask is not None and kbias is None:
         return False
     if _FLASH_OK is None:
         _FLASH_OK = hasattr(ext(), "attention_fwd")
     return _FLASH_OK
 
 
+def dropout_seed_offset(device, increment=4):
+    """(seed, offset) for the in-kernel dropout hash, drawn from the device generator
+    state (so torch.manual_seed, the TP-consistent RNG fork and activation-checkpoint RNG
+    replay all apply) and advanced like a philox consumer; no device synchronisation."""
+    if device.type == "cuda":
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        gen = torch.cuda.default_generators[idx]
+        seed, off = gen.initial_seed(), gen.get_offset()
+        gen.set_offset(off + increment)
+        return int(seed) & ((1 << 63) - 1), int(off)
+    return int(torch.randint(0, 1 << 62, (1,)).item()), 0
+
+
+def _mix32(x):
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    return x ^ (x >> 16)
+
+
+def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu"):
+    """Host reconstruction of the kernel's dropout decisions ([b, h, sq, sk] bool, True =
+    kept): test oracle for the in-kernel hash (csrc/kernels/attention_impl.h drop_key/mix32)."""
+    M = 0xFFFFFFFF
+    thr = max(1, min(65535, int(dropout_p * 65536.0 + 0.5)))
+    s0, s1, o0, o1 = seed & M, (seed >> 32) & M, offset & M, (offset >> 32) & M
+    bh = torch.arange(b * h, dtype=torch.int64, device=device)
+    key = _mix32(torch.full_like(bh, s0) ^ _mix32((s1 + 0x9E3779B9 * (bh + 1)) & M) ^
+                 _mix32(torch.full_like(bh, o0) ^ _mix32(torch.full_like(bh, (o1 + 0x85EBCA6B) & M))))
+    npairs = (sk + 1) // 2
+    q = torch.arange(sq, dtype=torch.int64, device=device).view(1, -1, 1)
+    k = torch.arange(sk, dtype=torch.int64, device=device).view(1, 1, -1)
+    x = (key.view(-1, 1, 1) ^ ((q * npairs + (k >> 1)) & M)) & M
+    hsh = _mix32(x)
+    u = torch.where((k & 1) == 1, hsh >> 16, hsh & 0xFFFF)
+    return (u >= thr).view(b, h, sq, sk)
+
+
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale, causal, window):
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window)
-        ctx.save_for_backward(q, k, v, o, lse)
+    def forward(ctx, q, k, v, scale, causal, window, kbias, dropout_p):
+        seed, off = dropout_seed_offset(q.device) if dropout_p > 0.0 else (0, 0)
+        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, kbias, dropout_p, seed, off)
+        ctx.save_for_backward(q, k, v, o, lse, kbias)
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
+        ctx.drop = (dropout_p, seed, off)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, kbias = ctx.saved_tensors
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window)
-        return dq, dk, dv, None, None, None
+        p, seed, off = ctx.drop
+        ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
+                                 kbias, p, seed, off)
+        return dq, dk, dv, None, None, None, None, None
 
 
 class _FlashAttentionPacked(torch.autograd.Function):
@@ -55,31 +118,37 @@ class _FlashAttentionPacked(torch.autograd.Function):
     the backward writes dQ/dK/dV into one packed gradient (no scatter/zero-fill copies)."""
 
     @staticmethod
-    def forward(ctx, qkv, scale, causal, window):
+    def forward(ctx, qkv, scale, causal, window, kbias, dropout_p):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window)
-        ctx.save_for_backward(qkv, o, lse)
+        seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
+        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, kbias, dropout_p, seed, off)
+        ctx.save_for_backward(qkv, o, lse, kbias)
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
+        ctx.drop = (dropout_p, seed, off)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, kbias = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
+        p, seed, off = ctx.drop
         ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
-                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window)
-        return dqkv, None, None, None
+                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, kbias, p, seed, off)
+        return dqkv, None, None, None, None, None
 
 
-def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, training=True, use_flash=True):
-    """qkv: [b, s, 3, h, d] -> [b, s, h, d]."""
+def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, training=True, use_flash=True,
+                     mask=None, mask_value=-1e4):
+    """qkv: [b, s, 3, h, d] -> [b, s, h, d].  mask: optional [b|1, 1, s, s] bool (True = masked)."""
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
     q = qkv[:, :, 0]
-    if use_flash and flash_supported(q, dropout_p if training else 0.0, None):
-        return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0))
-    return attention(q, qkv[:, :, 1], qkv[:, :, 2], causal=causal, scale=scale, dropout_p=dropout_p, window=window,
-                     training=training, use_flash=use_flash)
+    p = dropout_p if training else 0.0
+    kbias = key_padding_bias(mask, q.shape[1], q.shape[1], mask_value) if mask is not None else None
+    if use_flash and flash_supported(q, p, mask, kbias):
+        return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kbias, float(p))
+    return attention(q, qkv[:, :, 1], qkv[:, :, 2], causal=causal, mask=mask, scale=scale, dropout_p=dropout_p,
+                     window=window, training=training, use_flash=use_flash, mask_value=mask_value)
 
 
 # Score elements per materialised chunk.  On MI355X (torch 2.10 + ROCm 7), the backward of the
@@ -116,7 +185,11 @@ def _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, trainin
     if window is not None and window > 0:
         i = torch.arange(sq, device=q.device).view(-1, 1) + (sk - sq)
         j = torch.arange(sk, device=q.device).view(1, -1)
-        local = (j > i) | (j <= i - window)
+        # same semantics as the flash kernel: keys older than the window are masked, future
+        # keys only when the attention is causal
+        local = j <= i - window
+        if causal:
+            local = local | (j > i)
         mask = local.view(1, 1, sq, sk) if mask is None else (mask.bool() | local.view(1, 1, sq, sk))
         causal = False
     if scores.is_cuda and scores.dtype in (torch.float16, torch.bfloat16):
@@ -140,10 +213,14 @@ def _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, trainin
 
 
 def attention(q, k, v, causal=True, mask=None, scale=None, dropout_p=0.0, window=None, training=True,
-              attention_in_fp32=False, use_flash=True):
-    """q, k, v: [b, s, h, d]. mask: bool/uint8 [b|1, 1, sq, sk] with True = masked."""
+              attention_in_fp32=False, use_flash=True, mask_value=-1e4):
+    """q, k, v: [b, s, h, d]. mask: bool/uint8 [b|1, 1, sq, sk] with True = masked (applied
+    together with the causal / window masks)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
-    if use_flash and not attention_in_fp32 and flash_supported(q, dropout_p if training else 0.0, mask):
-        return _FlashAttention.apply(q, k, v, float(scale), bool(causal), int(window or 0))
+    p = dropout_p if training else 0.0
+    if use_flash and not attention_in_fp32 and q.is_cuda:
+        kbias = key_padding_bias(mask, q.shape[1], k.shape[1], mask_value) if mask is not None else None
+        if flash_supported(q, p, mask, kbias):
+            return _FlashAttention.apply(q, k, v, float(scale), bool(causal), int(window or 0), kbias, float(p))
     return _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, attention_in_fp32)

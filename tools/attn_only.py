@@ -12,7 +12,7 @@ b, s, h, d = int(os.environ.get("B", 8)), int(os.environ.get("S", 2048)), int(os
     int(os.environ.get("D", 64))
 qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
 for _ in range(int(os.environ.get("ITERS", 3))):
-    o = _FlashAttentionPacked.apply(qkv, 1.0 / math.sqrt(d), True, 0)
+    o = _FlashAttentionPacked.apply(qkv, 1.0 / math.sqrt(d), True, 0, None, 0.0)
     o.backward(torch.randn_like(o))
 torch.cuda.synchronize()
 print("done")

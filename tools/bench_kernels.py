@@ -26,14 +26,14 @@ def timeit(fn, iters=20, warm=5):
     return s.elapsed_time(e) / iters
 
 
-def bench_attention(b, s, h, d, causal=True):
+def bench_attention(b, s, h, d, causal=True, dropout=0.0, sdpa=True):
     from smdistributed_modelparallel_amd.ops.attention import _FlashAttentionPacked
 
     qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     scale = 1.0 / math.sqrt(d)
     flops = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
     out = {}
-    fwd = lambda: _FlashAttentionPacked.apply(qkv, scale, causal, 0)  # noqa: E731
+    fwd = lambda: _FlashAttentionPacked.apply(qkv, scale, causal, 0, None, dropout)  # noqa: E731
     out["ours_fwd_ms"] = timeit(fwd)
     o = fwd()
     g = torch.randn_like(o)
@@ -41,6 +41,8 @@ def bench_attention(b, s, h, d, causal=True):
     out["ours_bwd_ms"] = timeit(bwd)
     out["ours_fwd_tflops"] = flops / out["ours_fwd_ms"] / 1e9
     out["ours_bwd_tflops"] = 2.5 * flops / out["ours_bwd_ms"] / 1e9
+    if not sdpa:
+        return out
     try:
         q, k, v = (qkv[:, :, i].transpose(1, 2).detach().contiguous().requires_grad_() for i in range(3))
         sd = lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal)  # noqa: E731
@@ -109,7 +111,13 @@ def bench_memory_bound():
 
 
 if __name__ == "__main__":
-    results = {"attention_gpt2xl_b8_s2048": bench_attention(8, 2048, 25, 64),
-               "attention_b4_s4096_h32_d128": bench_attention(4, 4096, 32, 128)}
-    results.update(bench_memory_bound())
+    only_attn = "--attention" in sys.argv
+    results = {"attention_gpt2xl_b32_s2048": bench_attention(32, 2048, 25, 64, sdpa=False),
+               "attention_gpt2xl_b32_s2048_dropout0.1": bench_attention(32, 2048, 25, 64, dropout=0.1, sdpa=False),
+               "attention_gpt2xl_b8_s2048": bench_attention(8, 2048, 25, 64),
+               "attention_neox_b4_s2048_h16_d96": bench_attention(4, 2048, 16, 96, sdpa=False),
+               "attention_b4_s4096_h32_d128": bench_attention(4, 4096, 32, 128),
+               "attention_gptj_b8_s2048_h16_d256": bench_attention(8, 2048, 16, 256, sdpa=False)}
+    if not only_attn:
+        results.update(bench_memory_bound())
     print(json.dumps(results, indent=1))
