@@ -182,23 +182,10 @@ __device__ __forceinline__ int acc_row(int reg, int hh) { return (reg & 3) + 8 *
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// fmaxf on MFMA results makes clang insert a canonicalising v_max per operand; scores are
-// never signalling NaNs, so issue v_max3 directly (2 elements per instruction).
-// hipcc does not pad hazards for an asm statement: an MFMA result read by this VALU needs
-// the XDL->VALU wait states first -- mfma_ready() below provides them.
-__device__ __forceinline__ float max3(float a, float b, float c) {
-  float d;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-  return d;
-}
-
-// Wait states between the last MFMA writing `a`/`b` and an inline-asm VALU reading them
-// (8-pass XDL -> VALU: 12 states; 16 given).  The "+v" operands pin the order: the MFMAs
-// complete-issue before it, every reader comes after.  Without it v_max3 read stale
-// accumulator values on some waves (non-deterministic row maxima, 1-ulp output jitter).
-__device__ __forceinline__ void mfma_ready(f32x16& a, f32x16& b) {
-  asm volatile("s_nop 15" : "+v"(a), "+v"(b));
-}
+// Row max of MFMA results: builtin fmaxf, which hipcc lowers to v_max3_f32 AND pads with
+// the XDL->VALU wait states (an inline-asm v_max3 reading the accumulators directly is not
+// padded by the compiler and read stale values on some waves -- non-deterministic maxima).
+__device__ __forceinline__ float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 // value of lane ^ 32 (the other half-wave) without an LDS round trip
 __device__ __forceinline__ float xor32(float x) {
@@ -294,21 +281,36 @@ __device__ __forceinline__ void store_rows(uint16_t* dst, const f32x16* acc, flo
   }
 }
 
-// Stages the (bias / scale) values of a 64-key tile: thread t < 64 holds key kv0 + t.
-__device__ __forceinline__ float load_bias(const AttnParams& p, int64_t b, int key, float inv_scale) {
-  return key < p.sk ? p.kbias[b * p.kbias_sb + key] * inv_scale : 0.f;
+// Issues the load of a tile's raw bias value (thread t < 64 holds key kv0 + t).  The value is
+// consumed (scaled, stored to LDS) only at the next tile's staging, like the K/V registers:
+// using it right away would make wave 0 wait out the global-load latency every tile.
+__device__ __forceinline__ float load_bias(const AttnParams& p, int64_t b, int key) {
+  return key < p.sk ? p.kbias[b * p.kbias_sb + key] : 0.f;
 }
 
-// Accumulator init for a transposed score tile (key rows in registers): bias of the
-// register's key, 4 consecutive keys per float4 (acc_row(4g..4g+3) = 8g + 4hh + 0..3).
-__device__ __forceinline__ void init_from_keys(f32x16& a, const float* sB, int hh, float add) {
+// Adds the staged bias of each register's key to a transposed score tile (key rows in
+// registers), 4 consecutive keys per float4 (acc_row(4g..4g+3) = 8g + 4hh + 0..3).  Applied
+// after the score MFMAs and only on tiles that carry a bias: the MFMA chains keep their
+// zero / row-constant initial accumulators (a runtime choice of initial accumulator would
+// cost 32 register moves per tile on every tile).
+__device__ __forceinline__ void add_from_keys(f32x16& a, const float* sB, int hh) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const float4 v = *reinterpret_cast<const float4*>(&sB[8 * g + 4 * hh]);
-    a[4 * g + 0] = v.x + add;
-    a[4 * g + 1] = v.y + add;
-    a[4 * g + 2] = v.z + add;
-    a[4 * g + 3] = v.w + add;
+    a[4 * g + 0] += v.x;
+    a[4 * g + 1] += v.y;
+    a[4 * g + 2] += v.z;
+    a[4 * g + 3] += v.w;
+  }
+}
+
+// Publishes whether the tile being stored carries any nonzero bias: wave 0 holds the 64
+// staged values (thread t = key kv0 + t), one ballot, one LDS word; read after the barrier.
+// An all-zero bias (e.g. an all-ones padding mask) then costs only the 256-byte staging.
+__device__ __forceinline__ void publish_bias_flag(float bstage, int* sFlag) {
+  if (threadIdx.x < 64) {
+    const bool any = __any(bstage != 0.f);
+    if (threadIdx.x == 0) *sFlag = any ? 1 : 0;
   }
 }
 
@@ -345,6 +347,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   __shared__ __attribute__((aligned(16))) uint16_t sV[BN * DS];
   __shared__ __attribute__((aligned(16))) uint16_t sQ[QLDS ? BM * DS : 8];
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
+  __shared__ int sFlag;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
@@ -406,39 +409,39 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   if (kv_begin < kv_end) {
     stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
     stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
-    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x, inv_scale);
+    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
   }
   const int wave_last_q = q0 + 31;
   for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
     __syncthreads();
     stK.store(sK);
     stV.store(sV);
-    if (BIAS && threadIdx.x < BN) sB[threadIdx.x] = bstage;
+    if (BIAS) {
+      if (threadIdx.x < BN) sB[threadIdx.x] = bstage * inv_scale;
+      publish_bias_flag(bstage, &sFlag);
+    }
     __syncthreads();
+    const bool tile_bias = BIAS && sFlag != 0;
     if (kv0 + BN < kv_end) {
       stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
       stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
-      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x, inv_scale);
+      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
     }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
     if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
     const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
                           (win <= 0 || kv0 > wave_last_q + diag - win);
-    f32x16 s0, s1;
-    if (BIAS) {
-      init_from_keys(s0, sB, hh, 0.f);
-      init_from_keys(s1, sB + 32, hh, 0.f);
-    } else {
-      s0 = f32x16{0};
-      s1 = f32x16{0};
-    }
+    f32x16 s0 = f32x16{0}, s1 = f32x16{0};
 #pragma unroll
     for (int t = 0; t < D / 16; ++t) {
       const typename MF<T>::e8 qt = QLDS ? ld8<T>(sQ + ro.o[t] + wave * 32 * DS) : qf[t];
       s0 = MF<T>::mma(ld8<T>(sK + ro.o[t]), qt, s0);
       s1 = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * DS), qt, s1);
     }
-    mfma_ready(s0, s1);
+    if (tile_bias) {
+      add_from_keys(s0, sB, hh);
+      add_from_keys(s1, sB + 32, hh);
+    }
     if (!interior) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
@@ -581,7 +584,11 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   for (int i = 0; i < DO / 32; ++i) dv[i] = dk[i] = f32x16{0};
   const float sl2 = p.scale * kLog2e;
   const float inv_sl2 = 1.f / sl2;
-  const float kbias = BIAS ? load_bias(p, b, krow, 1.f / p.scale) : 0.f;
+  // the lane's key bias: loaded now, first consumed after the first tile's staging wait
+  // (an immediate use would stall every block on the load latency)
+  const float kbias_raw = BIAS ? load_bias(p, b, krow) : 0.f;
+  float kbias = 0.f;
+  bool blk_bias = false;  // this wave's 32 keys carry a bias
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
   const uint32_t npairs = static_cast<uint32_t>((sk + 1) >> 1);
   const uint32_t kpair = static_cast<uint32_t>(krow >> 1);
@@ -621,6 +628,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       sDl[threadIdx.x] = -d_stage;
     }
     __syncthreads();
+    if (BIAS) {
+      kbias = kbias_raw * (1.f / p.scale);
+      blk_bias = __any(kbias != 0.f);
+    }
     if (qt + BQ < q_end) {
       stQ.load(Q + static_cast<int64_t>(qt + BQ) * p.q_ss, sq - qt - BQ);
       stO.load(dO + static_cast<int64_t>(qt + BQ) * P.do_ss, sq - qt - BQ);
@@ -643,7 +654,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       for (int g = 0; g < 4; ++g) {
         const float4 lv = *reinterpret_cast<const float4*>(&sL[32 * sub + 8 * g + 4 * hh]);
         const float4 dv4 = *reinterpret_cast<const float4*>(&sDl[32 * sub + 8 * g + 4 * hh]);
-        s[4 * g + 0] = lv.x + kbias; s[4 * g + 1] = lv.y + kbias; s[4 * g + 2] = lv.z + kbias; s[4 * g + 3] = lv.w + kbias;
+        s[4 * g + 0] = lv.x; s[4 * g + 1] = lv.y; s[4 * g + 2] = lv.z; s[4 * g + 3] = lv.w;
         if (DROP) {
           ndl[4 * g + 0] = dv4.x; ndl[4 * g + 1] = dv4.y; ndl[4 * g + 2] = dv4.z; ndl[4 * g + 3] = dv4.w;
           dp[4 * g + 0] = dp[4 * g + 1] = dp[4 * g + 2] = dp[4 * g + 3] = 0.f;
@@ -655,6 +666,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       for (int t = 0; t < D / 16; ++t) {
         s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * DS), kf[t], s);
         dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * DS), vf[t], dp);
+      }
+      if (blk_bias) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s[j] += kbias;
       }
       auto finish = [&](float pv, int reg, int qq) {
         if (DROP) {
@@ -710,6 +725,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   __shared__ __attribute__((aligned(16))) uint16_t sK[BN * DS];
   __shared__ __attribute__((aligned(16))) uint16_t sV[BN * DS];
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
+  __shared__ int sFlag;
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -772,19 +788,23 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   if (kv_begin < kv_end) {
     stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
     stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
-    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x, inv_scale);
+    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
   }
   const int wave_last_q = q0 + 31;
   for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
     __syncthreads();
     stK.store(sK);
     stV.store(sV);
-    if (BIAS && threadIdx.x < BN) sB[threadIdx.x] = bstage;
+    if (BIAS) {
+      if (threadIdx.x < BN) sB[threadIdx.x] = bstage * inv_scale;
+      publish_bias_flag(bstage, &sFlag);
+    }
     __syncthreads();
+    const bool tile_bias = BIAS && sFlag != 0;
     if (kv0 + BN < kv_end) {
       stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
       stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
-      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x, inv_scale);
+      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
     }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
     if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
@@ -797,19 +817,17 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (BIAS) {
-        init_from_keys(s[u], sB + 32 * u, hh, s_init);
-      } else {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) s[u][j] = s_init;
+      for (int j = 0; j < 16; ++j) {
+        s[u][j] = s_init;
+        dp[u][j] = DROP ? 0.f : -dl;
       }
-#pragma unroll
-      for (int j = 0; j < 16; ++j) dp[u][j] = DROP ? 0.f : -dl;
 #pragma unroll
       for (int t = 0; t < D / 16; ++t) {
         s[u] = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * u * DS), qf[t], s[u]);
         dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[t] + 32 * u * DS), df[t], dp[u]);
       }
+      if (tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       if (DROP) {
         // dp <- Z o dP (raw), then dS = P o (Z o dP - delta)
         drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, thr16, p.drop_rs, true);

@@ -398,7 +398,8 @@ void check_bshd(const at::Tensor& t, const char* n) {
 }
 
 smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool causal,
-                             int64_t window, const c10::optional<at::Tensor>& kbias, double dropout_p, int64_t seed,
+                             int64_t window, const c10::optional<at::Tensor>& kbias,
+                             double dropout_p, int64_t seed,
                              int64_t offset) {
   check_bshd(q, "q");
   check_bshd(k, "k");
@@ -448,7 +449,8 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
 }
 
 std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale, bool causal,
-                                      int64_t window, c10::optional<at::Tensor> kbias, double dropout_p, int64_t seed,
+                                      int64_t window, c10::optional<at::Tensor> kbias,
+                                      double dropout_p, int64_t seed,
                                       int64_t offset) {
   auto p = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   auto o = at::empty({p.b, p.sq, p.h, p.d}, q.options());
@@ -463,7 +465,8 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
 // Writes into the provided dq/dk/dv (may be views of one packed gradient buffer).
 void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
                         at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window,
-                        c10::optional<at::Tensor> kbias, double dropout_p, int64_t seed, int64_t offset) {
+                        c10::optional<at::Tensor> kbias, double dropout_p,
+                        int64_t seed, int64_t offset) {
   smpk::AttnBwdParams P{};
   P.f = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   check_bshd(dout, "dout");
@@ -525,10 +528,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xent_bwd", &xent_bwd, py::arg("logits"), py::arg("target"), py::arg("lse"), py::arg("grad_rows"),
         py::arg("vocab_start"), py::arg("ignore_index"), py::arg("vocab") = -1);
   m.def("attention_fwd", &attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"),
-        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(), py::arg("dropout_p") = 0.0,
-        py::arg("seed") = 0, py::arg("offset") = 0);
+        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
   m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
-        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(), py::arg("dropout_p") = 0.0,
-        py::arg("seed") = 0, py::arg("offset") = 0);
+        py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
 }

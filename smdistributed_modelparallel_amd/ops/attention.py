@@ -22,21 +22,43 @@ _FLASH_OK = None
 FLASH_HEAD_DIMS = (64, 96, 128, 256)
 
 
+class KeyBias:
+    """Additive per-key bias [b|1, sk] (float32).  The kernels test each 64-key tile for a
+    nonzero entry as they stage it (one ballot) and skip the bias work on all-zero tiles, so
+    an all-ones padding mask costs nothing but the 256-byte staging per tile."""
+
+    __slots__ = ("bias",)
+
+    def __init__(self, bias):
+        self.bias = bias.float().contiguous()
+
+
 def key_padding_bias(mask, sq, sk, mask_value=-1e4):
     """A [b|1, 1, sq, sk] bool/uint8 mask (True = masked) that only depends on the key
-    (the usual padding mask, expanded over queries) -> additive float32 bias [b|1, sk];
-    None when the mask varies over queries (the kernel then cannot take it)."""
+    (the usual padding mask, expanded over queries) -> KeyBias (additive mask_value on
+    masked keys); None when the mask varies over queries (the kernel then cannot take it).
+    Cached on the mask tensor: every layer of a forward pass shares one conversion."""
     if mask is None:
         return None
+    cached = getattr(mask, "_smp_kbias", None)
+    if cached is not None and cached[0] == (sk, mask_value):
+        return cached[1]
     if mask.dim() != 4 or mask.shape[1] != 1 or mask.shape[-1] != sk:
         return None
     if mask.shape[2] != 1 and mask.stride(2) != 0:
-        if not mask.is_cuda or not bool((mask == mask[:, :, :1]).all()):  # pragma: no cover - rare
+        if not bool((mask == mask[:, :, :1]).all()):  # one host sync for non-expanded masks
             return None
     row = mask[:, 0, 0, :]
     if row.dtype not in (torch.bool, torch.uint8):
-        return row.float().contiguous()  # already additive
-    return torch.zeros(row.shape, dtype=torch.float32, device=row.device).masked_fill_(row.bool(), mask_value)
+        kb = KeyBias(row)  # already additive
+    else:
+        kb = KeyBias(torch.zeros(row.shape, dtype=torch.float32, device=row.device).masked_fill_(row.bool(),
+                                                                                              mask_value))
+    try:
+        mask._smp_kbias = ((sk, mask_value), kb)
+    except (AttributeError, RuntimeError):  # pragma: no cover
+        pass
+    return kb
 
 
 def flash_supported(q, dropout_p=0.0, mask=None, kbias=None):
@@ -95,21 +117,25 @@ def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu")
 
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, scale, causal, window, kbias, dropout_p):
+    def forward(ctx, q, k, v, scale, causal, window, kb, dropout_p):
         seed, off = dropout_seed_offset(q.device) if dropout_p > 0.0 else (0, 0)
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, kbias, dropout_p, seed, off)
-        ctx.save_for_backward(q, k, v, o, lse, kbias)
+        bias = kb.bias if kb is not None else None
+        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        ctx.save_for_backward(q, k, v, o, lse)
+        ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
         ctx.drop = (dropout_p, seed, off)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse, kbias = ctx.saved_tensors
+        q, k, v, o, lse = ctx.saved_tensors
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         p, seed, off = ctx.drop
+        kb = ctx.kb
+        bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
-                                 kbias, p, seed, off)
+                                 bias, p, seed, off)
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -118,22 +144,26 @@ class _FlashAttentionPacked(torch.autograd.Function):
     the backward writes dQ/dK/dV into one packed gradient (no scatter/zero-fill copies)."""
 
     @staticmethod
-    def forward(ctx, qkv, scale, causal, window, kbias, dropout_p):
+    def forward(ctx, qkv, scale, causal, window, kb, dropout_p):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, kbias, dropout_p, seed, off)
-        ctx.save_for_backward(qkv, o, lse, kbias)
+        bias = kb.bias if kb is not None else None
+        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
         ctx.drop = (dropout_p, seed, off)
         return o
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse, kbias = ctx.saved_tensors
+        qkv, o, lse = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
         p, seed, off = ctx.drop
+        kb = ctx.kb
+        bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
-                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, kbias, p, seed, off)
+                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off)
         return dqkv, None, None, None, None, None
 
 

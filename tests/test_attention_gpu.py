@@ -106,10 +106,12 @@ def test_flash_key_padding_bias(d, causal):
     lengths = torch.tensor([160, 97, 33], device="cuda")
     pad = torch.arange(s, device="cuda").view(1, -1) >= lengths.view(-1, 1)  # True = masked
     mask = pad.view(b, 1, 1, s).expand(b, 1, s, s)
-    kbias = key_padding_bias(mask, s, s, -1e4)
+    kb = key_padding_bias(mask, s, s, -1e4)
+    kbias = kb.bias
     assert kbias.shape == (b, s) and kbias.dtype == torch.float32
+    assert key_padding_bias(mask, s, s, -1e4) is kb  # cached on the mask
     scale = 1.0 / math.sqrt(d)
-    o = _FlashAttention.apply(q, k, v, scale, causal, 0, kbias, 0.0)
+    o = _FlashAttention.apply(q, k, v, scale, causal, 0, kb, 0.0)
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     orf = _ref(qr, kr, vr, scale, causal, kbias=kbias)
     assert (o.float() - orf).abs().max().item() < 2e-2
@@ -120,7 +122,7 @@ def test_flash_key_padding_bias(d, causal):
 
 
 def test_flash_bias_and_dropout_together():
-    from smdistributed_modelparallel_amd.ops.attention import _FlashAttention, flash_dropout_keep_mask
+    from smdistributed_modelparallel_amd.ops.attention import KeyBias, _FlashAttention, flash_dropout_keep_mask
 
     torch.manual_seed(5)
     b, s, h, d, p = 2, 256, 2, 64, 0.1
@@ -129,7 +131,7 @@ def test_flash_bias_and_dropout_together():
     kbias[1, 200:] = -1e4
     gen = torch.cuda.default_generators[torch.cuda.current_device()]
     seed, off = gen.initial_seed(), gen.get_offset()
-    o = _FlashAttention.apply(q, k, v, 0.125, True, 0, kbias, p)
+    o = _FlashAttention.apply(q, k, v, 0.125, True, 0, KeyBias(kbias), p)
     keep = flash_dropout_keep_mask(b, h, s, s, p, seed & ((1 << 63) - 1), off, device="cuda")
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     orf = _ref(qr, kr, vr, 0.125, True, kbias=kbias, keep=keep, p=p)

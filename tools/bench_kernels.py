@@ -26,14 +26,15 @@ def timeit(fn, iters=20, warm=5):
     return s.elapsed_time(e) / iters
 
 
-def bench_attention(b, s, h, d, causal=True, dropout=0.0, sdpa=True):
-    from smdistributed_modelparallel_amd.ops.attention import _FlashAttentionPacked
+def bench_attention(b, s, h, d, causal=True, dropout=0.0, sdpa=True, zero_bias=False):
+    from smdistributed_modelparallel_amd.ops.attention import KeyBias, _FlashAttentionPacked
 
     qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     scale = 1.0 / math.sqrt(d)
     flops = 4 * b * h * s * s * d * (0.5 if causal else 1.0)
     out = {}
-    fwd = lambda: _FlashAttentionPacked.apply(qkv, scale, causal, 0, None, dropout)  # noqa: E731
+    kb = KeyBias(torch.zeros(b, s, device="cuda")) if zero_bias else None  # all-ones padding mask
+    fwd = lambda: _FlashAttentionPacked.apply(qkv, scale, causal, 0, kb, dropout)  # noqa: E731
     out["ours_fwd_ms"] = timeit(fwd)
     o = fwd()
     g = torch.randn_like(o)
@@ -114,6 +115,7 @@ if __name__ == "__main__":
     only_attn = "--attention" in sys.argv
     results = {"attention_gpt2xl_b32_s2048": bench_attention(32, 2048, 25, 64, sdpa=False),
                "attention_gpt2xl_b32_s2048_dropout0.1": bench_attention(32, 2048, 25, 64, dropout=0.1, sdpa=False),
+               "attention_gpt2xl_b32_s2048_onesmask": bench_attention(32, 2048, 25, 64, sdpa=False, zero_bias=True),
                "attention_gpt2xl_b8_s2048": bench_attention(8, 2048, 25, 64),
                "attention_neox_b4_s2048_h16_d96": bench_attention(4, 2048, 16, 96, sdpa=False),
                "attention_b4_s4096_h32_d128": bench_attention(4, 4096, 32, 128),
