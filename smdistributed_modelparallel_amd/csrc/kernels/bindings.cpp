@@ -117,8 +117,50 @@ void cast_copy_(at::Tensor src, at::Tensor dst, double scale) {
 }
 
 // ------------------------------------------------------------------- layernorm
+smpk::DropoutArgs dropout_args(double p, int64_t seed, int64_t offset) {
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1)");
+  smpk::DropoutArgs d;
+  if (p > 0.0) {
+    uint32_t thr = static_cast<uint32_t>(p * 65536.0 + 0.5);
+    d.thr = thr < 1 ? 1 : (thr > 65535 ? 65535 : thr);
+    d.rs = static_cast<float>(1.0 / (1.0 - p));
+    d.seed = static_cast<uint64_t>(seed);
+    d.offset = static_cast<uint64_t>(offset);
+  }
+  return d;
+}
+
+bool aligned16(const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
+
+// y = residual + dropout(x)
+at::Tensor dropout_add(at::Tensor x, c10::optional<at::Tensor> residual, double p, int64_t seed, int64_t offset) {
+  check_gpu(x, "x");
+  TORCH_CHECK(aligned16(x), "dropout_add: x must be 16-byte aligned");
+  if (residual.has_value()) {
+    check_gpu(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type() && aligned16(*residual),
+                "dropout_add: residual mismatch");
+  }
+  auto y = at::empty_like(x);
+  check(smpk::dropout_add(dt_code(x), x.data_ptr(), opt_ptr(residual), y.data_ptr(), x.numel(),
+                          dropout_args(p, seed, offset), stream()),
+        "dropout_add");
+  return y;
+}
+
+at::Tensor dropout_bwd(at::Tensor dy, double p, int64_t seed, int64_t offset) {
+  check_gpu(dy, "dy");
+  TORCH_CHECK(aligned16(dy), "dropout_bwd: dy must be 16-byte aligned");
+  auto dx = at::empty_like(dy);
+  check(smpk::dropout_bwd(dt_code(dy), dy.data_ptr(), dx.data_ptr(), dy.numel(), dropout_args(p, seed, offset),
+                          stream()),
+        "dropout_bwd");
+  return dx;
+}
+
 std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> residual,
-                                      c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, double eps) {
+                                      c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, double eps,
+                                      double dropout_p, int64_t seed, int64_t offset) {
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / cols;
@@ -137,7 +179,7 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> re
   if (b.has_value()) TORCH_CHECK(b->numel() == cols && b->is_contiguous() && dt_code(*b) == wdt, "bias mismatch");
   check(smpk::layernorm_fwd(dt_code(x), x.data_ptr(), opt_ptr(residual), residual.has_value() ? xo.data_ptr() : nullptr,
                             wdt, opt_ptr(w), opt_ptr(b), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                            rows, cols, eps, stream()),
+                            rows, cols, eps, stream(), dropout_args(residual.has_value() ? dropout_p : 0.0, seed, offset)),
         "layernorm_fwd");
   if (residual.has_value()) return {y, mean, rstd, xo};
   return {y, mean, rstd};
@@ -508,7 +550,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nonfinite_", &nonfinite_);
   m.def("axpby_", &axpby_);
   m.def("cast_copy_", &cast_copy_);
-  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("residual"), py::arg("w"), py::arg("b"),
+        py::arg("eps"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+  m.def("dropout_add", &dropout_add, py::arg("x"), py::arg("residual"), py::arg("p"), py::arg("seed"),
+        py::arg("offset"));
+  m.def("dropout_bwd", &dropout_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"));
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("need_wgrad"), py::arg("need_bgrad"), py::arg("dres"), py::arg("dw_out") = py::none(),
         py::arg("db_out") = py::none());

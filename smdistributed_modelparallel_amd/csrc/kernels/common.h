@@ -55,6 +55,45 @@ __device__ __forceinline__ void store16(T* p, const Vec16<T>& r) {
   *reinterpret_cast<uint4*>(p) = r.raw;
 }
 
+// ------------------------------------------------------------ element-wise dropout hash
+// lowbias32 mixer; a 32-bit hash serves an element PAIR (16-bit uniform each), indexed by
+// the flat element index, so any kernel that knows an element's index can regenerate the
+// decision (forward fused into LayerNorm / residual add, backward fused into its consumer).
+__device__ __forceinline__ uint32_t dmix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ uint32_t dropout_key(const DropoutArgs& d) {
+  const uint32_t s0 = static_cast<uint32_t>(d.seed), s1 = static_cast<uint32_t>(d.seed >> 32);
+  const uint32_t o0 = static_cast<uint32_t>(d.offset), o1 = static_cast<uint32_t>(d.offset >> 32);
+  return dmix32(s0 ^ dmix32(s1 + 0x27d4eb2fu) ^ dmix32(o0 ^ dmix32(o1 + 0x165667b1u)));
+}
+
+// keep factors (0 or rs) of the 8 consecutive elements e0..e0+7 (e0 even)
+__device__ __forceinline__ void dropout_factors8(uint32_t key, int64_t e0, const DropoutArgs& d, float (&f)[8]) {
+  const uint32_t thr16 = d.thr << 16;
+  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(e0) >> 33) * 0x9e3779b1u;
+  const uint32_t pr = static_cast<uint32_t>(static_cast<uint64_t>(e0) >> 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t h = dmix32(key ^ hi ^ (pr + j));
+    f[2 * j] = (h << 16) >= thr16 ? d.rs : 0.f;
+    f[2 * j + 1] = h >= thr16 ? d.rs : 0.f;
+  }
+}
+
+__device__ __forceinline__ float dropout_factor1(uint32_t key, int64_t e, const DropoutArgs& d) {
+  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(e) >> 33) * 0x9e3779b1u;
+  const uint32_t h = dmix32(key ^ hi ^ static_cast<uint32_t>(static_cast<uint64_t>(e) >> 1));
+  const uint32_t u = (e & 1) ? (h >> 16) : (h & 0xffffu);
+  return u >= d.thr ? d.rs : 0.f;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

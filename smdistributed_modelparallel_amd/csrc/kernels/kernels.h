@@ -38,8 +38,22 @@ int cast_copy(int dt_src, const void* src, int dt_dst, void* dst, int64_t n, flo
 
 // ------------------------------------------------------------------ norms (layernorm.hip)
 // y = (x - mean) * rstd * w + b ; optional residual add: x = x + r written to x_out first.
+// Element-wise dropout decided by a counter hash of (seed, offset, element index): no mask
+// tensor is stored, the backward regenerates the decisions.  thr = 0 disables dropout.
+struct DropoutArgs {
+  uint32_t thr = 0;  // element dropped iff its 16-bit uniform < thr
+  float rs = 1.f;    // 1 / (1 - p)
+  uint64_t seed = 0, offset = 0;
+};
+// y = residual + dropout(x)  (residual may be null); x, residual, y same dtype, contiguous
+int dropout_add(int dt, const void* x, const void* residual, void* y, int64_t n, const DropoutArgs& d, hipStream_t s);
+// dx = dy * keep * rs  (the backward of dropout)
+int dropout_bwd(int dt, const void* dy, void* dx, int64_t n, const DropoutArgs& d, hipStream_t s);
+
+// residual != null: x_out = residual + dropout(x) is written and normalised (pre-LN block)
 int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
-                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);
+                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s,
+                  const DropoutArgs& drop = DropoutArgs());
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
                   const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
                   int part_rows, const void* dres, hipStream_t s);

@@ -45,12 +45,13 @@ __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const
                                                   T* __restrict__ x_out, const W* __restrict__ w,
                                                   const W* __restrict__ b, T* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                  int64_t rows, int cols, float eps) {
+                                                  int64_t rows, int cols, float eps, DropoutArgs drop) {
   constexpr int N = Vec16<T>::N;
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= rows) return;
   const T* xr = x + row * cols;
+  const uint32_t dkey = drop.thr ? dropout_key(drop) : 0u;
   float v[VPT][N];
   float sum = 0.f;
 #pragma unroll
@@ -60,9 +61,22 @@ __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const
       Vec16<T> a = load16(xr + c);
       if (res != nullptr) {
         Vec16<T> r = load16(res + row * cols + c);
+        float f[N];
+        if (drop.thr) {  // x_out = residual + dropout(x)
+          static_assert(N == 8 || N == 4, "dropout factors come in groups of 8");
+          if constexpr (N == 8) {
+            dropout_factors8(dkey, row * cols + c, drop, f);
+          } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) f[j] = dropout_factor1(dkey, row * cols + c + j, drop);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) f[j] = 1.f;
+        }
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-          v[k][j] = to_f32(a.v[j]) + to_f32(r.v[j]);
+          v[k][j] = fmaf(to_f32(a.v[j]), f[j], to_f32(r.v[j]));
           a.v[j] = from_f32<T>(v[k][j]);
         }
         store16(x_out + row * cols + c, a);
@@ -128,15 +142,17 @@ __global__ void __launch_bounds__(256) ln_fwd_stream(const T* __restrict__ x, co
                                                      T* __restrict__ x_out, const W* __restrict__ w,
                                                      const W* __restrict__ b, T* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     int64_t rows, int cols, float eps) {
+                                                     int64_t rows, int cols, float eps, DropoutArgs drop) {
   __shared__ float smem[16];
   const int64_t row = blockIdx.x;
   const T* xr = x + row * cols;
+  const uint32_t dkey = drop.thr ? dropout_key(drop) : 0u;
   float sum = 0.f;
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
     float a = to_f32(xr[c]);
     if (res != nullptr) {
-      T s = from_f32<T>(a + to_f32(res[row * cols + c]));
+      const float f = drop.thr ? dropout_factor1(dkey, row * cols + c, drop) : 1.f;
+      T s = from_f32<T>(fmaf(a, f, to_f32(res[row * cols + c])));
       x_out[row * cols + c] = s;
       a = to_f32(s);
     }
@@ -455,7 +471,8 @@ bool vec_ok(const void* p) {
 }  // namespace
 
 int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
-                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s) {
+                  void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s,
+                  const DropoutArgs& drop) {
   if (rows <= 0) return 0;
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
@@ -472,15 +489,15 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
       T* yy = static_cast<T*>(y);
       const int c = static_cast<int>(cols);
       if (aligned && vpt <= 1) {
-        ln_fwd_reg<T, W, 1><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+        ln_fwd_reg<T, W, 1><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
       } else if (aligned && vpt <= 2) {
-        ln_fwd_reg<T, W, 2><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+        ln_fwd_reg<T, W, 2><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
       } else if (aligned && vpt <= 4) {
-        ln_fwd_reg<T, W, 4><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+        ln_fwd_reg<T, W, 4><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
       } else if (aligned && vpt <= 8) {
-        ln_fwd_reg<T, W, 8><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+        ln_fwd_reg<T, W, 8><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
       } else {
-        ln_fwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps);
+        ln_fwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
       }
     });
   });

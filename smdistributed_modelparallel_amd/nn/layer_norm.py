@@ -47,9 +47,9 @@ class FusedLayerNorm(nn.Module):
                 self.weight.fill_(1.0)
                 self.bias.zero_()
 
-    def forward_add(self, x, residual):
-        """(LN(x + residual), x + residual) in one kernel."""
-        return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
+    def forward_add(self, x, residual, dropout_p=0.0):
+        """(LN(dropout(x) + residual), dropout(x) + residual) in one kernel."""
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout_p)
 
     def forward_passthrough(self, x):
         """(LN(x), x) where x's two gradient paths (LN input, residual branch) are summed

@@ -35,6 +35,7 @@ from ..backend.exceptions import SMPInvalidArgumentError
 from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
+from ..ops.dropout import dropout_add as _dropout_add
 from ..ops.gelu import bias_gelu
 from ..ops import lm_head as lm_head_op
 from ..ops.linear import linear
@@ -165,14 +166,43 @@ class DistributedModule(nn.Module):
 
 
 class _Dropout(nn.Module):
+    """Mask-free dropout (ops/dropout.py); ``add`` fuses the residual add."""
+
     def __init__(self, p):
         super().__init__()
         self.p = p
 
+    def active_p(self):
+        return self.p if (self.training and self.p > 0.0) else 0.0
+
     def forward(self, x):
         if self.p == 0.0 or not self.training:
             return x
-        return F.dropout(x, self.p, True)
+        return _dropout_add(x, None, self.p, True)
+
+    def add(self, x, residual):
+        """residual + dropout(x) in one pass."""
+        return _dropout_add(x, residual, self.p, self.training)
+
+
+def _all_ones(attention_mask):
+    """An all-ones padding mask masks nothing: drop it (attention then runs the unmasked
+    kernels).  Decided once per mask tensor (one host sync, cached on the tensor), and only
+    outside pipelines, where a sync per microbatch would stall the schedule.
+    SMP_SKIP_ALL_ONES_MASK_CHECK=1 disables the check."""
+    if os.environ.get("SMP_SKIP_ALL_ONES_MASK_CHECK", "0") == "1" or not torch.is_tensor(attention_mask):
+        return False
+    if state.initialized and state.core.pp_size() > 1:
+        return False
+    cached = getattr(attention_mask, "_smp_all_ones", None)
+    if cached is not None and cached[0] == attention_mask._version:
+        return cached[1]
+    val = bool((attention_mask != 0).all())
+    try:
+        attention_mask._smp_all_ones = (attention_mask._version, val)
+    except (AttributeError, RuntimeError):  # pragma: no cover
+        pass
+    return val
 
 
 def _runs_here(module):
@@ -394,7 +424,7 @@ class DistributedAttentionLayer(DistributedModule):
             hidden = _enter_tp(hidden, self._mem, self.hidden_size)
             mask = _gather_mask(mask)
         a = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
-        out = self.dropout(self.core(a, mask, cross_states, cross_mask)) + hidden
+        out = self.dropout.add(self.core(a, mask, cross_states, cross_mask), hidden)
         if self.post_layernorm:
             out = self.layernorm(out)
         if self._tp > 1 and self.output_layer and not _prescaled():
@@ -504,7 +534,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
         if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = _enter_tp(hidden, self._mem, self.hidden_size)
         m = self.pre_layernorm_module(hidden) if self.pre_layernorm else hidden
-        out = self.dropout(self.core(m)) + hidden
+        out = self.dropout.add(self.core(m), hidden)
         if self.post_layernorm:
             out = self.layernorm(out)
         if self._tp > 1 and self.output_layer and not _prescaled():
@@ -558,15 +588,15 @@ class DistributedTransformerLayer(DistributedModule):
                 a, hidden = at.pre_layernorm_module.forward_passthrough(hidden)
             else:
                 a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
-            attn = at.dropout(at.core(a, mask))
+            attn = at.core(a, mask)
             if at.post_layernorm:
-                hidden = at.layernorm(attn + hidden)
+                hidden = at.layernorm(at.dropout.add(attn, hidden))
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
             elif out.pre_layernorm and hasattr(out.pre_layernorm_module, "forward_add"):
-                # fused: residual add + LayerNorm in one HIP kernel
-                m, hidden = out.pre_layernorm_module.forward_add(attn, hidden)
+                # fused: attention-branch dropout + residual add + LayerNorm in one HIP kernel
+                m, hidden = out.pre_layernorm_module.forward_add(attn, hidden, at.dropout.active_p())
             else:
-                hidden = attn + hidden
+                hidden = at.dropout.add(attn, hidden)
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
             if self.add_cross_attention:
                 ca = self.cross_attention
@@ -575,7 +605,7 @@ class DistributedTransformerLayer(DistributedModule):
                 if ca.post_layernorm:
                     hidden = ca.layernorm(hidden)
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
-            hidden = out.dropout(out.core(m)) + hidden
+            hidden = out.dropout.add(out.core(m), hidden)
             if out.post_layernorm:
                 hidden = out.layernorm(hidden)
         if self._tp > 1 and self.output_layer and not _prescaled():
@@ -702,7 +732,7 @@ class DistributedTransformerLMHead(DistributedModule):
         # TOGETHER with the causal mask (the flash kernel takes both; the reference's fused
         # causal softmax dropped it with a warning, `transformer.py:1684-1696`).
         mask = None
-        if attention_mask is not None:
+        if attention_mask is not None and not _all_ones(attention_mask):
             mask = (attention_mask.view(B, -1) == 0).view(B, 1, 1, -1).expand(B, 1, s, s)
 
         prescaled = _prescaled() and self._tp > 1

@@ -17,6 +17,7 @@ import torch
 
 from . import softmax as _sm
 from ._ext import ext
+from .dropout import dropout_seed_offset  # noqa: F401  (re-exported)
 
 _FLASH_OK = None
 FLASH_HEAD_DIMS = (64, 96, 128, 256)
@@ -74,19 +75,6 @@ def flash_supported(q, dropout_p=0.0, mask=None, kbias=None):
     if _FLASH_OK is None:
         _FLASH_OK = hasattr(ext(), "attention_fwd")
     return _FLASH_OK
-
-
-def dropout_seed_offset(device, increment=4):
-    """(seed, offset) for the in-kernel dropout hash, drawn from the device generator
-    state (so torch.manual_seed, the TP-consistent RNG fork and activation-checkpoint RNG
-    replay all apply) and advanced like a philox consumer; no device synchronisation."""
-    if device.type == "cuda":
-        idx = device.index if device.index is not None else torch.cuda.current_device()
-        gen = torch.cuda.default_generators[idx]
-        seed, off = gen.initial_seed(), gen.get_offset()
-        gen.set_offset(off + increment)
-        return int(seed) & ((1 << 63) - 1), int(off)
-    return int(torch.randint(0, 1 << 62, (1,)).item()), 0
 
 
 def _mix32(x):

@@ -8,6 +8,7 @@ input / weight dtypes.
 import torch
 
 from ._ext import ext
+from .dropout import dropout_seed_offset
 from .linear import _fusable
 
 
@@ -72,16 +73,19 @@ class _FusedLayerNormPassthrough(torch.autograd.Function):
 
 
 class _FusedAddLayerNorm(torch.autograd.Function):
-    """s = x + r ; y = LN(s).  Returns (y, s). Backward fuses ds into dx."""
+    """s = dropout(x) + r ; y = LN(s).  Returns (y, s).  Backward fuses ds into the LN
+    backward; the x branch then gets dropout's backward (mask regenerated from the hash)."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps):
+    def forward(ctx, x, residual, weight, bias, eps, dropout_p):
         x2, r2 = x.contiguous(), residual.contiguous()
-        y, mean, rstd, s = ext().layernorm_fwd(x2, r2, weight, bias, eps)
+        seed, off = dropout_seed_offset(x.device) if dropout_p > 0.0 else (0, 0)
+        y, mean, rstd, s = ext().layernorm_fwd(x2, r2, weight, bias, eps, dropout_p, seed, off)
         ctx.save_for_backward(s, weight, mean, rstd)
         ctx.bias = bias
         ctx.has_w = weight is not None
         ctx.has_b = bias is not None
+        ctx.drop = (dropout_p, seed, off)
         return y.view(x.shape), s.view(x.shape)
 
     @staticmethod
@@ -91,7 +95,9 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         need_b = ctx.has_b and ctx.needs_input_grad[3]
         dres = ds.contiguous() if ds is not None else None
         dx, dw, db = _ln_bwd(dy.contiguous(), s, w, ctx.bias, mean, rstd, need_w, need_b, dres)
-        return dx, dx, dw, db, None
+        p, seed, off = ctx.drop
+        dxin = ext().dropout_bwd(dx, p, seed, off) if p > 0.0 else dx
+        return dxin, dx, dw, db, None, None
 
 
 def layer_norm(x, weight, bias, eps=1e-5):
@@ -107,9 +113,11 @@ def layer_norm_passthrough(x, weight, bias, eps=1e-5):
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps), x
 
 
-def add_layer_norm(x, residual, weight, bias, eps=1e-5):
-    """Returns (LN(x + residual), x + residual)."""
+def add_layer_norm(x, residual, weight, bias, eps=1e-5, dropout_p=0.0):
+    """Returns (LN(dropout(x) + residual), dropout(x) + residual)."""
     if x.is_cuda:
-        return _FusedAddLayerNorm.apply(x, residual, weight, bias, eps)
+        return _FusedAddLayerNorm.apply(x, residual, weight, bias, eps, float(dropout_p))
+    if dropout_p > 0.0:
+        x = torch.nn.functional.dropout(x, dropout_p, True)
     s = x + residual
     return torch.nn.functional.layer_norm(s, (s.shape[-1],), weight, bias, eps), s
