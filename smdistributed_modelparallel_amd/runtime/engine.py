@@ -31,9 +31,20 @@ How it is built here (our design, not the reference's):
   locally queued result, a scheduling action) it sends the event's TP-invariant key to
   its TP peers, which execute exactly that sequence (reference `DeterministicServerQueue`,
   `server_queue.py:224-626`, forced when TP > 1).  Message ids are (pp_rank, counter),
-  so the same logical message has the same key on every TP peer.
+  the counter restarting every step, so the same logical message has the same key on
+  every TP peer AND in every step.
+* **Record and replay.**  For the first ``SMP_REPLAY_RECORD_STEPS`` (5) steps of a step
+  function every decider records its event sequence and the step time.  Then the global
+  leader picks the fastest recorded step, every decider hands that step's sequence to its
+  TP peers, and from then on all ranks of the model-parallel group replay it: no decision
+  messages, no dynamic choices (reference `server_queue.py:224-626`, record window 5 steps
+  `:245`, best step `:575-626`).  All stages replay the SAME recorded step, so the replayed
+  orders are one feasible global execution.  ``static_mode`` turns this on without TP.
+  With the IPC transport a tensor is pulled the moment its control message is dispatched,
+  so the reference's pre-registered receptions (`:488`) have nothing left to pre-post.
 """
 import os
+import time
 from collections import deque
 import itertools
 
@@ -98,9 +109,14 @@ class _MbState:
 
 
 class PipelineEngine:
+    RECORD_STEPS = int(os.environ.get("SMP_REPLAY_RECORD_STEPS", "5"))
+
     def __init__(self, state):
         self.state = state
         self._ids = itertools.count()
+        self._recorded = {}  # step fn id -> [(seconds, [event keys])]   (deciders only)
+        self._replay = {}  # step fn id -> frozen event keys
+        self._recording = None
         self.reset_step()
 
     # ------------------------------------------------------------- plumbing
@@ -181,6 +197,7 @@ class PipelineEngine:
     # ------------------------------------------------------------ pipelined
     def _run_pipelined(self, step_fn, mb_inputs):
         self.reset_step()
+        self._ids = itertools.count()  # step-relative ids: keys repeat step to step (replay)
         cfg = self.state.cfg
         n = cfg.microbatches
         self.num_mb = n
@@ -204,14 +221,61 @@ class PipelineEngine:
         self.reset_step()
         return outs
 
+    # ------------------------------------------------------- record / replay
+    def replay_enabled(self):
+        """Record-and-replay runs for pipelines whose order must be deterministic (TP > 1)
+        or when static_mode asks for it; SMP_REPLAY=0 keeps the dynamic (recording-free)
+        scheduler."""
+        core = self.core
+        if os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") == "1" or os.environ.get("SMP_REPLAY", "1") == "0":
+            return False
+        return core.pp_size() > 1 and (core.tp_size() > 1 or bool(self.state.cfg.static_mode))
+
+    def after_step(self, step_fn, seconds):
+        """Called on every rank after every pipelined step (symmetric collectives)."""
+        if not self.replay_enabled():
+            return
+        sid = step_fn.id
+        if sid in self._replay:
+            return
+        core, comm = self.core, self.state.comm
+        from ..backend.collectives import CommGroup
+
+        rec = self._recorded.setdefault(sid, [])
+        rec.append((seconds, self._recording or []))
+        self._recording = None
+        if len(rec) < self.RECORD_STEPS:
+            return
+        # the global leader picks the fastest recorded step; every stage replays that SAME step
+        ranker = core.ranker
+        best = None
+        if core.pp_rank() == 0 and core.tp_rank() == 0:
+            best = min(range(len(rec)), key=lambda i: rec[i][0])
+        if core.mp_size() > 1:
+            best = comm.bcast(best, ranker.translate(0, 0, core.rdp_rank()), CommGroup.MP_GROUP)
+        keys = rec[best][1] if core.tp_rank() == 0 else None
+        if core.tp_size() > 1:
+            keys = comm.bcast(keys, ranker.translate(core.pp_rank(), 0, core.rdp_rank()), CommGroup.TP_GROUP)
+        self._replay[sid] = list(keys)
+        self._recorded.pop(sid, None)
+        logger.info(f"pipeline schedule frozen for step function {sid}: recorded step {best} "
+                    f"({len(keys)} events) is replayed from now on")
+
     def _serve(self, leader):
         core = self.core
-        self._det = core.tp_size() > 1 and os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") != "1"
+        replay = self._replay.get(self.step_fn.id) if self.replay_enabled() else None
+        self._det = (core.tp_size() > 1 and os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") != "1") or \
+            self.replay_enabled()
+        if replay is not None:
+            self._tp_peers = []
+            return self._serve_follower(leader, replay=replay)
         if self._det:
             me = core.rank()
             self._tp_peers = [r for r in core.get_tp_group() if r != me]
             if core.tp_rank() != 0:
                 return self._serve_follower(leader)
+            if self.replay_enabled():
+                self._recording = []
         timeout = 0.05
         while not self._stop:
             progressed = False
@@ -264,6 +328,8 @@ class PipelineEngine:
 
     def _announce(self, key):
         if self._det:
+            if self._recording is not None:
+                self._recording.append(key)
             # tagged with the step: a decider may start step t+1 while a TP peer (in
             # another pipeline) is still finishing step t
             msg = ("dec", self.state.step_count, key)
@@ -276,13 +342,17 @@ class PipelineEngine:
             self._announce(self._event_key(src, stubbed))
         self._dispatch(src, stubbed, tensors)
 
-    def _serve_follower(self, leader):
-        """TP peer of a deciding rank: execute events strictly in the decided order."""
+    def _serve_follower(self, leader, replay=None):
+        """TP peer of a deciding rank (or any rank replaying a frozen schedule): execute
+        events strictly in the decided order."""
         pending = {}
         step = self.state.step_count
-        stash = getattr(self, "_dec_stash", deque())
-        decisions = deque(k for st, k in stash if st == step)
-        self._dec_stash = deque((st, k) for st, k in stash if st != step)
+        if replay is not None:
+            decisions = deque(replay)
+        else:
+            stash = getattr(self, "_dec_stash", deque())
+            decisions = deque(k for st, k in stash if st == step)
+            self._dec_stash = deque((st, k) for st, k in stash if st != step)
         timeout = 0.05
         while not self._stop:
             m = self.state.transport.poll(0.0 if decisions else timeout)

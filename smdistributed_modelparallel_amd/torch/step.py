@@ -7,6 +7,7 @@ results), and the optional per-step memory metrics file (``SMP_WRITE_STEP_MEMORY
 """
 import functools
 import os
+import time
 
 import torch
 
@@ -83,6 +84,7 @@ class StepFunction:
             state.current_offloader.reset()
         num_mb = state.cfg.microbatches
         state.in_step_func = True
+        t0 = time.perf_counter()
         try:
             with state.model._step():
                 if core.pp_rank() == 0:
@@ -93,6 +95,8 @@ class StepFunction:
         finally:
             state.in_step_func = False
             core.timeline_end_step()
+        if core.pp_size() > 1 and state.model.partitioned:
+            state.engine.after_step(self, time.perf_counter() - t0)
         state.step_count += 1
         self.memory_metrics.record(state.step_count)
         if outputs is None:

@@ -8,11 +8,11 @@ import pytest
 from tests.dist_utils import run_workers
 
 
-def _run(world, pp, tp, mbs, pipe="interleaved", auto=0, steps=2, extra=None, timeout=200):
+def _run(world, pp, tp, mbs, pipe="interleaved", auto=0, steps=2, extra=None, timeout=200, env=None):
     args = [pp, tp, mbs, pipe, auto, steps]
     if extra:
         args.append(json.dumps(extra))
-    outs = run_workers("pp_gpt", world, args, timeout=timeout)
+    outs = run_workers("pp_gpt", world, args, timeout=timeout, env_extra=env)
     assert all("OK" in o for o in outs)
 
 
@@ -151,3 +151,17 @@ def test_dp2_delayed_parameter_initialization():
 def test_dp2_fp16_fp32_grad_accumulation():
     outs = run_workers("fp32_accum", 2, [], timeout=200)
     assert all("OK" in o for o in outs)
+
+
+@pytest.mark.parametrize("pipe", ["interleaved", "simple"])
+def test_pp2_tp2_record_and_replay_under_jitter(pipe):
+    """Record 2 steps, freeze the fastest order, replay it (no decision messages) for the
+    remaining steps while message timing is jittered differently on every rank; results
+    still match the unpartitioned model (reference DeterministicServerQueue)."""
+    _run(4, 2, 2, 4, pipe=pipe, steps=5, extra={"jitter": True, "expect_replay": True},
+         env={"SMP_REPLAY_RECORD_STEPS": "2"})
+
+
+def test_pp2_static_mode_replay_without_tp():
+    _run(2, 2, 1, 3, steps=4, extra={"cfg": {"static_mode": True}, "expect_replay": True},
+         env={"SMP_REPLAY_RECORD_STEPS": "2"})

@@ -157,6 +157,10 @@ def main():
         if d > worst:
             worst, worst_name = d, n
     assert worst < 2e-4, (worst, worst_name if worst > 0 else None)
+    if extra.get("expect_replay"):
+        eng = smp.state.engine
+        assert eng._replay, "schedule was never frozen"
+        print(f"rank {smp.rank()} replaying {sum(len(v) for v in eng._replay.values())} recorded events", flush=True)
     if extra.get("cfg", {}).get("offload_activations") and smp.state.current_offloader is not None:
         st = smp.state.current_offloader.stats
         # every rank that runs checkpointed layers must have offloaded and reloaded them
