@@ -190,7 +190,8 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> re
 std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> w, at::Tensor mean,
                                       at::Tensor rstd, bool need_wgrad, bool need_bgrad,
                                       c10::optional<at::Tensor> dres, c10::optional<at::Tensor> dw_out,
-                                      c10::optional<at::Tensor> db_out) {
+                                      c10::optional<at::Tensor> db_out, c10::optional<at::Tensor> ext_sums,
+                                      double ext_n) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
@@ -216,7 +217,8 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
   check(smpk::layernorm_bwd(dt_code(x), dy.data_ptr(), x.data_ptr(), wdt, opt_ptr(w), mean.data_ptr<float>(),
                             rstd.data_ptr<float>(), dx.data_ptr(), dwp.defined() ? dwp.data_ptr<float>() : nullptr,
                             dbp.defined() ? dbp.data_ptr<float>() : nullptr, rows, cols, parts, opt_ptr(dres),
-                            stream()),
+                            stream(), ext_sums.has_value() ? ext_sums->data_ptr<float>() : nullptr,
+                            static_cast<float>(ext_n)),
         "layernorm_bwd");
   if (dwp.defined()) {
     auto wo = w.has_value() ? w->options() : x.options();
@@ -237,6 +239,48 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
           "layernorm_bwd_reduce");
   }
   return {dx, dw, db};
+}
+
+// dst (view) <- src (view), same shape, <= 4 dims after the caller's collapsing, any strides
+void strided_copy_(at::Tensor dst, at::Tensor src) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda() && dst.device() == src.device(), "strided_copy_: GPU tensors required");
+  TORCH_CHECK(dst.sizes() == src.sizes() && dst.scalar_type() == src.scalar_type(), "strided_copy_: shape/dtype mismatch");
+  TORCH_CHECK(dst.dim() <= 4, "strided_copy_: at most 4 dims (collapse first)");
+  int64_t sz[4] = {1, 1, 1, 1}, ss[4] = {0, 0, 0, 0}, ds[4] = {0, 0, 0, 0};
+  const int off = 4 - static_cast<int>(dst.dim());
+  for (int i = 0; i < dst.dim(); ++i) {
+    sz[off + i] = dst.size(i);
+    ss[off + i] = src.stride(i);
+    ds[off + i] = dst.stride(i);
+  }
+  check(smpk::strided_copy4(static_cast<int>(dst.element_size()), src.data_ptr(), dst.data_ptr(), sz, ss, ds, stream()),
+        "strided_copy4");
+}
+
+at::Tensor layernorm_local_stats(at::Tensor x) {
+  check_gpu(x, "x");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  auto out = at::empty({rows, 3}, x.options().dtype(at::kFloat));
+  check(smpk::layernorm_local_stats(dt_code(x), x.data_ptr(), out.data_ptr<float>(), rows, cols, stream()),
+        "layernorm_local_stats");
+  return out;
+}
+
+at::Tensor layernorm_bwd_local_sums(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> w, at::Tensor mean,
+                                    at::Tensor rstd) {
+  check_gpu(dy, "dy");
+  check_gpu(x, "x");
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd_local_sums: stats mismatch");
+  auto out = at::empty({rows, 2}, x.options().dtype(at::kFloat));
+  int wdt = w.has_value() ? dt_code(*w) : dt_code(x);
+  check(smpk::layernorm_bwd_local_sums(dt_code(x), dy.data_ptr(), x.data_ptr(), wdt, opt_ptr(w),
+                                       mean.data_ptr<float>(), rstd.data_ptr<float>(), out.data_ptr<float>(), rows,
+                                       cols, stream()),
+        "layernorm_bwd_local_sums");
+  return out;
 }
 
 at::Tensor layernorm_apply_stats(at::Tensor x, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
@@ -557,7 +601,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bwd", &dropout_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"));
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("need_wgrad"), py::arg("need_bgrad"), py::arg("dres"), py::arg("dw_out") = py::none(),
-        py::arg("db_out") = py::none());
+        py::arg("db_out") = py::none(), py::arg("ext_sums") = py::none(), py::arg("ext_n") = 0.0);
+  m.def("layernorm_local_stats", &layernorm_local_stats);
+  m.def("strided_copy_", &strided_copy_);
+  m.def("layernorm_bwd_local_sums", &layernorm_bwd_local_sums);
   m.def("layernorm_apply_stats", &layernorm_apply_stats);
   m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("bias"), py::arg("exact") = false);
   m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("exact") = false);

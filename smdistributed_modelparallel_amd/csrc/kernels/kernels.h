@@ -56,7 +56,8 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
                   const DropoutArgs& drop = DropoutArgs());
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
                   const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
-                  int part_rows, const void* dres, hipStream_t s);
+                  int part_rows, const void* dres, hipStream_t s,
+                  const float* ext_sums = nullptr, float ext_n = 0.f);
 // dgamma/dbeta from the per-block partials; work = [kLnReduceSlices][2][cols] fp32 scratch.
 constexpr int kLnReduceSlices = 32;
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
@@ -64,7 +65,18 @@ int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, vo
 // Distributed-LN pieces (hidden sharded across TP): apply with global stats, local sums.
 int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const void* b, const float* mean,
                           const float* var, void* y, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s);
-int layernorm_local_sums(int dt, const void* x, const float* mean, hipStream_t s);
+// Distributed LayerNorm over a TP-sharded hidden dim (K6-K8; reference
+// smp/torch/nn/layer_norm.py:24-102):
+//  * layernorm_local_stats: per row of the local shard (n*m, M2, n*m*m) with m the local
+//    mean and M2 = sum (x - m)^2 -- summed over the TP group they give the exact global
+//    mean and variance (Chan's parallel combination, no E[x^2] - E[x]^2 cancellation);
+//  * layernorm_apply_stats (K6): y from the global mean / var;
+//  * layernorm_bwd_local_sums (K7): per row (sum dy*w, sum dy*w*xhat) over the local shard;
+//  * layernorm_bwd with ext_sums (K8): dx from the TP-summed row sums over ext_n columns,
+//    plus this shard's dgamma / dbeta partials.
+int layernorm_local_stats(int dt, const void* x, float* stats3, int64_t rows, int64_t cols, hipStream_t s);
+int layernorm_bwd_local_sums(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
+                             const float* rstd, float* sums2, int64_t rows, int64_t cols, hipStream_t s);
 int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned);
 
 // ------------------------------------------------------------- elementwise (gelu.hip)

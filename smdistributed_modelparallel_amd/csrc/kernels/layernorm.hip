@@ -182,7 +182,8 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
                                                   const W* __restrict__ w, const float* __restrict__ mean_in,
                                                   const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                   float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                  int64_t rows, int cols, const T* __restrict__ dres) {
+                                                  int64_t rows, int cols, const T* __restrict__ dres,
+                                                  const float* __restrict__ ext, float ext_n) {
   constexpr int N = Vec16<T>::N;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -223,8 +224,13 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
         }
       }
     }
-    s1 = wave_sum(s1) / cols;
-    s2 = wave_sum(s2) / cols;
+    if (ext != nullptr) {  // distributed LN: row sums over the whole TP-sharded row
+      s1 = ext[2 * row] / ext_n;
+      s2 = ext[2 * row + 1] / ext_n;
+    } else {
+      s1 = wave_sum(s1) / cols;
+      s2 = wave_sum(s2) / cols;
+    }
 #pragma unroll
     for (int k = 0; k < VPT; ++k) {
       const int c = (k * 64 + lane) * N;
@@ -377,7 +383,8 @@ __global__ void __launch_bounds__(256) ln_bwd_stream(const T* __restrict__ dy, c
                                                      const W* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                      float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                     int64_t rows, int cols, const T* __restrict__ dres) {
+                                                     int64_t rows, int cols, const T* __restrict__ dres,
+                                                     const float* __restrict__ ext, float ext_n) {
   // one block per row; dw/db partial per row (parts == rows) -- only used for odd shapes
   __shared__ float smem[16];
   const int64_t row = blockIdx.x;
@@ -394,6 +401,10 @@ __global__ void __launch_bounds__(256) ln_bwd_stream(const T* __restrict__ dy, c
   }
   s1 = block_sum(s1, smem) / cols;
   s2 = block_sum(s2, smem) / cols;
+  if (ext != nullptr) {
+    s1 = ext[2 * row] / ext_n;
+    s2 = ext[2 * row + 1] / ext_n;
+  }
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
     const float dyv = to_f32(dy[row * cols + c]);
     const float xh = (to_f32(x[row * cols + c]) - mean) * rstd;
@@ -515,7 +526,7 @@ static inline int ln_bwd_parts(int64_t rows, int64_t cols, bool reg_path) {
 
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean, const float* rstd,
                   void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols, int part_rows,
-                  const void* dres, hipStream_t s) {
+                  const void* dres, hipStream_t s, const float* ext_sums, float ext_n) {
   if (rows <= 0) return 0;
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
@@ -535,21 +546,22 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
       const size_t lds = static_cast<size_t>(2 * kRowsPerBlock) * cols * sizeof(float);
       const int64_t nvec = cols / N;
       const int64_t rpb = (rows + parts - 1) / parts;
-      if (reg && nvec <= 256 && nvec >= 128) {
+      const bool blk_ok = ext_sums == nullptr;  // the block-per-rows form has no external-sum mode
+      if (blk_ok && reg && nvec <= 256 && nvec >= 128) {
         ln_bwd_blk<T, W, 1><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
-      } else if (reg && nvec <= 512 && nvec > 256) {
+      } else if (blk_ok && reg && nvec <= 512 && nvec > 256) {
         ln_bwd_blk<T, W, 2><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
       } else if (reg && vpt <= 1) {
-        ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+        ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else if (reg && vpt <= 2) {
-        ln_bwd_reg<T, W, 2><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+        ln_bwd_reg<T, W, 2><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else if (reg && vpt <= 4) {
-        ln_bwd_reg<T, W, 4><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+        ln_bwd_reg<T, W, 4><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else if (reg) {
-        ln_bwd_reg<T, W, 8><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr);
+        ln_bwd_reg<T, W, 8><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else {
         ln_bwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part,
-                                                                   rows, c, dr);
+                                                                   rows, c, dr, ext_sums, ext_n);
       }
     });
   });
@@ -583,7 +595,81 @@ int layernorm_apply_stats(int dt, const void* x, int wdt, const void* w, const v
   return static_cast<int>(hipGetLastError());
 }
 
-int layernorm_local_sums(int, const void*, const float*, hipStream_t) { return -1; }
+namespace {
+
+// one wave per row, strided over the local shard (any width); two passes over x (local mean,
+// then M2 about it) -- exact, and the values stay in L2 between the passes
+template <typename T>
+__global__ void __launch_bounds__(256) ln_local_stats_kernel(const T* __restrict__ x, float* __restrict__ out,
+                                                             int64_t rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* xr = x + row * cols;
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += to_f32(xr[c]);
+  s = wave_sum(s);
+  const float m = s / cols;
+  float m2 = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float d = to_f32(xr[c]) - m;
+    m2 += d * d;
+  }
+  m2 = wave_sum(m2);
+  if (lane == 0) {
+    out[3 * row] = s;
+    out[3 * row + 1] = m2;
+    out[3 * row + 2] = s * m;
+  }
+}
+
+template <typename T, typename W>
+__global__ void __launch_bounds__(256) ln_bwd_local_sums_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                const W* __restrict__ w,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd,
+                                                                float* __restrict__ out, int64_t rows, int cols) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float mu = mean[row], rs = rstd[row];
+  float a = 0.f, b = 0.f;
+  for (int c = lane; c < cols; c += 64) {
+    const float g = to_f32(dy[row * cols + c]) * (w ? to_f32(w[c]) : 1.f);
+    a += g;
+    b += g * (to_f32(x[row * cols + c]) - mu) * rs;
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    out[2 * row] = a;
+    out[2 * row + 1] = b;
+  }
+}
+
+}  // namespace
+
+int layernorm_local_stats(int dt, const void* x, float* stats3, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    ln_local_stats_kernel<T><<<static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock), 256, 0, s>>>(
+        static_cast<const T*>(x), stats3, rows, static_cast<int>(cols));
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int layernorm_bwd_local_sums(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
+                             const float* rstd, float* sums2, int64_t rows, int64_t cols, hipStream_t s) {
+  if (rows <= 0) return 0;
+  SMPK_DISPATCH(dt, T, {
+    SMPK_DISPATCH(wdt, W, {
+      ln_bwd_local_sums_kernel<T, W><<<static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock), 256, 0, s>>>(
+          static_cast<const T*>(dy), static_cast<const T*>(x), static_cast<const W*>(w), mean, rstd, sums2, rows,
+          static_cast<int>(cols));
+    });
+  });
+  return static_cast<int>(hipGetLastError());
+}
 
 // exported helper so bindings can size partial buffers
 int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned) {

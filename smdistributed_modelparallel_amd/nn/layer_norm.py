@@ -105,6 +105,49 @@ class _DistLNStats(torch.autograd.Function):
         return gx, None, None
 
 
+class _DistLayerNormHIP(torch.autograd.Function):
+    """GPU form of the TP-sharded LayerNorm: native kernels K6-K8 (`csrc/kernels/layernorm.hip`)
+    around two [rows, k] fp32 all-reduces; inputs stay in their dtype (no fp32 upcast of the
+    activation), one all-reduce in each direction (reference `layer_norm.py:24-102` uses two
+    in the forward)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, full_dim, group):
+        from ..ops._ext import ext
+
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        st = ext().layernorm_local_stats(x2)  # (n*m, M2, n*m*m) per row of the local shard
+        if group is not None:
+            with throttler().throttle(st):
+                dist.all_reduce(st, group=group)
+        n = float(full_dim)
+        mean = st[:, 0] / n
+        var = ((st[:, 1] + st[:, 2]) / n - mean * mean).clamp_min_(0.0)  # Chan's combination
+        rstd = torch.empty_like(mean)
+        y = ext().layernorm_apply_stats(x2, weight, bias, mean.contiguous(), var.contiguous(), rstd, eps)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.shape, ctx.full_dim, ctx.group = shape, full_dim, group
+        ctx.has_w, ctx.has_b = weight is not None, bias is not None
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops._ext import ext
+
+        x2, w, mean, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(x2.shape).contiguous()
+        sums = ext().layernorm_bwd_local_sums(dy2, x2, w, mean, rstd)  # (sum g, sum g*xhat) local
+        if ctx.group is not None:
+            with throttler().throttle(sums):
+                dist.all_reduce(sums, group=ctx.group)
+        need_w = ctx.has_w and ctx.needs_input_grad[1]
+        need_b = ctx.has_b and ctx.needs_input_grad[2]
+        dx, dw, db = ext().layernorm_bwd(dy2, x2, w, mean, rstd, need_w, need_b, None, ext_sums=sums,
+                                         ext_n=float(ctx.full_dim))
+        return dx.view(ctx.shape), (dw if need_w else None), (db if need_b else None), None, None, None
+
+
 class DistributedLayerNorm(nn.Module):
     """LayerNorm whose normalised dim is split across the TP group (uneven splits ok)."""
 
@@ -138,6 +181,8 @@ class DistributedLayerNorm(nn.Module):
 
     def forward(self, x):
         group = tp_group() if tp_size() > 1 else None
+        if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32):
+            return _DistLayerNormHIP.apply(x, self.weight, self.bias, self.eps, self.full_dim, group)
         mean, var = _DistLNStats.apply(x, self.full_dim, group)
         y = (x.float() - mean) * torch.rsqrt(var + self.eps)
         if self.weight is not None:

@@ -349,7 +349,7 @@ class DistributedAttentionLayer(DistributedModule):
         all-reduce (bias included), [B, s, h]."""
         if self._mem:
             return self._core_memory(a, mask)
-        a = (bwd_allreduce_for_tp(a) if self._tp > 1 else a)
+        a = (bwd_allreduce_for_tp(a, inplace_grad=True) if self._tp > 1 else a)
         B, s, _ = a.shape
         lh, d = self.local_heads, self.attention_head_size
         if self.cross_attention:
@@ -370,7 +370,7 @@ class DistributedAttentionLayer(DistributedModule):
                     mask=mask, mask_value=getattr(self, "mask_value", -1e4),
                 )
                 out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
-                return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
+                return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
@@ -384,7 +384,7 @@ class DistributedAttentionLayer(DistributedModule):
         )
         ctx = ctx.reshape(B, s, lh * d)
         out = linear(ctx, self.dense_weight, self.dense_bias)
-        return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
+        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
 
     def _core_memory(self, a, mask):
         """optimize='memory': a is [B, s, h/tp] (hidden-sharded).  Partial QKV products
@@ -524,11 +524,11 @@ class DistributedTransformerOutputLayer(DistributedModule):
             x = _activation(x, self.activation, None, self._tanh_gelu)
             out = linear(x, self.dense2_weight, self.dense2_bias)
             return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
-        m = (bwd_allreduce_for_tp(m) if self._tp > 1 else m)
+        m = (bwd_allreduce_for_tp(m, inplace_grad=True) if self._tp > 1 else m)
         x = linear(m, self.dense1_weight)
         x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu)
         out = linear(x, self.dense2_weight, self.dense2_bias)
-        return (fwd_allreduce_for_tp(out) if self._tp > 1 else out)
+        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
 
     def forward(self, hidden):
         if self._tp > 1 and self.input_layer and not _prescaled():

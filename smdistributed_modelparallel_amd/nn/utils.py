@@ -20,6 +20,7 @@ import torch
 import torch.distributed as dist
 
 from ..torch.state_mod import state
+from ..ops.pack import strided_copy_
 from ..parallel.throttle import throttler
 
 
@@ -53,12 +54,16 @@ def get_merge_shapes(num_channels):
 
 
 # -------------------------------------------------------------- raw collectives
-def _pad_to(x, dim, n):
-    if x.size(dim) == n:
-        return x
-    pad_shape = list(x.shape)
-    pad_shape[dim] = n - x.size(dim)
-    return torch.cat([x, x.new_zeros(pad_shape)], dim=dim)
+# RCCL's all-gather / reduce-scatter / all-to-all move whole [rank, rows, ...] blocks; a
+# shard of dim `dim` is moved between its tensor layout and that block layout by ONE
+# strided HIP copy (ops/pack.py, K21) -- uneven shards are padded to the largest one, the
+# padding rows are never initialised (the receiver drops them).
+def _split3(x, dim):
+    """View x as [A, x.size(dim), B] (A = prod of leading dims, B = of trailing)."""
+    A = 1
+    for n in x.shape[:dim]:
+        A *= n
+    return x.reshape(A, x.size(dim), -1)
 
 
 def _allgather(x, dim, sizes=None):
@@ -71,13 +76,31 @@ def _allgather(x, dim, sizes=None):
     if sizes is None:
         sizes = [x.size(dim)] * ws
     mx = max(sizes)
-    xp = _pad_to(x, dim, mx).movedim(dim, 0).contiguous()
-    out = xp.new_empty((ws * mx,) + tuple(xp.shape[1:]))
-    with throttler().throttle(xp):
-        dist.all_gather_into_tensor(out, xp, group=group)
-    if any(s != mx for s in sizes):
-        out = torch.cat([p[:s] for p, s in zip(out.split(mx, dim=0), sizes)], dim=0)
-    return out.movedim(0, dim).contiguous() if dim != 0 else out
+    even = all(n == mx for n in sizes)
+    out_shape = list(x.shape)
+    out_shape[dim] = sum(sizes)
+    if dim == 0 and even:  # rank blocks are already the final layout
+        out = x.new_empty(out_shape)
+        with throttler().throttle(x):
+            dist.all_gather_into_tensor(out, x, group=group)
+        return out
+    x3 = _split3(x, dim)  # [A, n, B]
+    A, B = x3.shape[0], x3.shape[2]
+    send = x.new_empty((mx, A, B))
+    strided_copy_(send[: x3.shape[1]], x3.permute(1, 0, 2))
+    recv = x.new_empty((ws, mx, A, B))
+    with throttler().throttle(send):
+        dist.all_gather_into_tensor(recv.view(ws * mx, A, B), send, group=group)
+    out = x.new_empty(out_shape)
+    o3 = out.view(A, sum(sizes), B)
+    if even:
+        strided_copy_(o3.view(A, ws, mx, B).permute(1, 2, 0, 3), recv)
+    else:
+        off = 0
+        for r, n in enumerate(sizes):
+            strided_copy_(o3[:, off:off + n].permute(1, 0, 2), recv[r, :n])
+            off += n
+    return out
 
 
 def _reduce_scatter(x, dim, sizes=None):
@@ -90,20 +113,42 @@ def _reduce_scatter(x, dim, sizes=None):
         assert x.size(dim) % ws == 0, "reduce_scatter requires divisible size or explicit sizes"
         sizes = [x.size(dim) // ws] * ws
     mx = max(sizes)
-    parts = list(x.split(sizes, dim=dim))
-    padded = [_pad_to(p, dim, mx).movedim(dim, 0) for p in parts]
-    inp = torch.cat(padded, dim=0).contiguous()
-    out = inp.new_empty((mx,) + tuple(inp.shape[1:]))
+    even = all(n == mx for n in sizes)
+    me = tp_rank()
+    out_shape = list(x.shape)
+    out_shape[dim] = sizes[me]
+    if dim == 0 and even:
+        x = x.contiguous()
+        out = x.new_empty(out_shape)
+        with throttler().throttle(x):
+            dist.reduce_scatter_tensor(out, x, group=group)
+        return out
+    x3 = _split3(x, dim)
+    A, B = x3.shape[0], x3.shape[2]
+    inp = x.new_empty((ws, mx, A, B))
+    if even:
+        strided_copy_(inp, x3.view(A, ws, mx, B).permute(1, 2, 0, 3))
+    else:
+        off = 0
+        for r, n in enumerate(sizes):
+            strided_copy_(inp[r, :n], x3[:, off:off + n].permute(1, 0, 2))
+            off += n
+    red = x.new_empty((mx, A, B))
     with throttler().throttle(inp):
-        dist.reduce_scatter_tensor(out, inp, group=group)
-    out = out[: sizes[tp_rank()]]
-    return out.movedim(0, dim).contiguous()
+        dist.reduce_scatter_tensor(red, inp.view(ws * mx, A, B), group=group)
+    out = x.new_empty(out_shape)
+    strided_copy_(out.view(A, sizes[me], B).permute(1, 0, 2), red[: sizes[me]])
+    return out
 
 
-def _allreduce(x):
+def _allreduce(x, inplace=False):
+    """Sum over the TP group.  inplace=False leaves x untouched (a copy is reduced); the
+    autograd wrappers pass inplace=True where x is a dead temporary (a GEMM output or a
+    gradient nobody else reads), saving a full-size copy per call."""
     if tp_size() == 1:
         return x
-    x = x.contiguous()
+    if not inplace or not x.is_contiguous():
+        x = x.clone(memory_format=torch.contiguous_format)
     with throttler().throttle(x):
         dist.all_reduce(x, group=tp_group())
     return x
@@ -128,56 +173,84 @@ def _all_to_all(x, split_dim, merge_dim, split_sizes=None, merge_sizes=None):
         return x
     if split_sizes is None:
         split_sizes = [x.size(split_dim) // ws] * ws
-    pieces = [p.contiguous() for p in x.split(split_sizes, dim=split_dim)]
     me = tp_rank()
+    pieces = list(x.split(split_sizes, dim=split_dim))
     out_shapes = []
     for r in range(ws):
         s = list(pieces[me].shape)
-        if merge_sizes is not None:
-            s[merge_dim] = merge_sizes[r]
-        else:
-            s[merge_dim] = x.size(merge_dim)
+        s[merge_dim] = merge_sizes[r] if merge_sizes is not None else x.size(merge_dim)
         out_shapes.append(s)
-    outs = [x.new_empty(s) for s in out_shapes]
-    # each received piece r has this rank's split slice and rank r's merge extent
     group = tp_group()
+    out_shape = list(out_shapes[0])
+    out_shape[merge_dim] = sum(s[merge_dim] for s in out_shapes)
     if x.is_cuda:
+        # one flat send buffer (pieces packed back to back) and one flat receive buffer:
+        # a single RCCL all-to-all over xGMI with per-rank element counts
+        numels = [p.numel() for p in pieces]
+        send = x.new_empty(sum(numels))
+        off = 0
+        for p, n in zip(pieces, numels):
+            strided_copy_(send[off:off + n].view(p.shape), p)
+            off += n
+        rn = [int(torch.Size(s).numel()) for s in out_shapes]
+        recv = x.new_empty(sum(rn))
         with throttler().throttle(x):
-            dist.all_to_all(outs, pieces, group=group)  # RCCL all-to-all over xGMI
-    else:
-        # gloo has no all-to-all: pairwise exchange
-        ops = []
-        for r in range(ws):
-            if r == me:
-                outs[r].copy_(pieces[r])
-                continue
-            peer = dist.get_global_rank(group, r)
-            ops.append(dist.P2POp(dist.isend, pieces[r], peer, group))
-            ops.append(dist.P2POp(dist.irecv, outs[r], peer, group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+            dist.all_to_all_single(recv, send, output_split_sizes=rn, input_split_sizes=numels, group=group)
+        out = x.new_empty(out_shape)
+        off, moff = 0, 0
+        for s, n in zip(out_shapes, rn):
+            strided_copy_(out.narrow(merge_dim, moff, s[merge_dim]), recv[off:off + n].view(s))
+            off += n
+            moff += s[merge_dim]
+        return out
+    # gloo has no all-to-all: pairwise exchange
+    pieces = [p.contiguous() for p in pieces]
+    outs = [x.new_empty(s) for s in out_shapes]
+    ops = []
+    for r in range(ws):
+        if r == me:
+            outs[r].copy_(pieces[r])
+            continue
+        peer = dist.get_global_rank(group, r)
+        ops.append(dist.P2POp(dist.isend, pieces[r], peer, group))
+        ops.append(dist.P2POp(dist.irecv, outs[r], peer, group))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
     return torch.cat(outs, dim=merge_dim)
 
 
 # ------------------------------------------------------------ autograd wrappers
 class _FwdAllreduce(torch.autograd.Function):
+    """fwd all-reduce (in place on x when the caller marks it a dead temporary, e.g. the
+    row-parallel GEMM output -- no autograd node saves it); bwd identity."""
+
     @staticmethod
-    def forward(ctx, x):
-        return _allreduce(x.clone() if tp_size() > 1 else x)
+    def forward(ctx, x, inplace):
+        if inplace and tp_size() > 1 and x.is_contiguous():
+            # x is often a view returned by the GEMM Function (mark_dirty is forbidden there);
+            # its data is reduced in place behind autograd's back -- safe because no node
+            # saved x -- and a view of it is the output
+            _allreduce(x.detach(), inplace=True)
+            return x.view_as(x)
+        return _allreduce(x)
 
     @staticmethod
     def backward(ctx, g):
-        return g
+        return g, None
 
 
 class _BwdAllreduce(torch.autograd.Function):
+    """fwd identity; bwd all-reduce, in place when the caller guarantees the incoming
+    gradient is a fresh tensor (the dgrad of the column-parallel GEMM that consumes x)."""
+
     @staticmethod
-    def forward(ctx, x):
-        return x
+    def forward(ctx, x, inplace):
+        ctx.inplace = inplace
+        return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
-        return _allreduce(g.clone() if tp_size() > 1 else g)
+        return _allreduce(g, inplace=ctx.inplace), None
 
 
 class _Allgather(torch.autograd.Function):
@@ -243,12 +316,16 @@ class _ScatterAndMerge(torch.autograd.Function):
         return back, None, None, None, None
 
 
-def fwd_allreduce_for_tp(x):
-    return _FwdAllreduce.apply(x) if tp_size() > 1 else x
+def fwd_allreduce_for_tp(x, inplace=False):
+    """All-reduce in the forward (identity backward).  inplace=True: x is a dead temporary
+    (a row-parallel GEMM output) and is reduced in place -- no copy."""
+    return _FwdAllreduce.apply(x, inplace) if tp_size() > 1 else x
 
 
-def bwd_allreduce_for_tp(x):
-    return _BwdAllreduce.apply(x) if tp_size() > 1 else x
+def bwd_allreduce_for_tp(x, inplace_grad=False):
+    """Identity forward, all-reduce of the gradient.  inplace_grad=True: the consumer of the
+    output is a column-parallel GEMM whose dgrad is a fresh tensor -- reduced in place."""
+    return _BwdAllreduce.apply(x, inplace_grad) if tp_size() > 1 else x
 
 
 def allgather_for_tp(x, dim, sizes=None):
