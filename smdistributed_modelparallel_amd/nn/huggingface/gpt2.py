@@ -43,7 +43,7 @@ def config_to_kwargs(config):
         "attention_dropout_prob": config.attn_pdrop,
         "hidden_dropout_prob": config.resid_pdrop,
         "embedding_dropout_prob": config.embd_pdrop,
-        "activation": "gelu",  # gelu_new == tanh GeLU
+        "activation": _activation(config.activation_function),
         "layernorm_epsilon": config.layer_norm_epsilon,
         "initializer_range": config.initializer_range,
         "use_normal_initialization": True,
@@ -55,6 +55,19 @@ def config_to_kwargs(config):
         "add_lm_head": True,
         "tie_input_output_embedding": True,
     }
+
+
+def _activation(name):
+    """HF activation_function -> smp activation (reference `nn/huggingface/gpt2.py:46-58`):
+    the tanh GeLUs map to "gelu" (our bias-GeLU is the tanh form), relu to "relu"; anything
+    else (including the exact-erf "gelu") is refused as in the reference."""
+    if name in ("gelu_new", "gelu_pytorch_tanh", "gelu_fast"):
+        return "gelu"
+    if name == "relu":
+        return "relu"
+    from ...backend.exceptions import SMPUnsupportedError
+
+    raise SMPUnsupportedError(f"GPT-2 activation_function {name!r} is not supported by DistributedTransformer")
 
 
 def init_hook(config, *args, **kwargs):

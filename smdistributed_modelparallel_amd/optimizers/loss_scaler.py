@@ -86,8 +86,14 @@ def any_overflow(flat_grads, group=None):
     for g in flat_grads:
         f = multi_tensor.nonfinite_flag(g)
         flag = f if flag is None else torch.maximum(flag, f)
+    collective = group is not None and dist.is_initialized() and dist.get_world_size(group) > 1
     if flag is None:
-        return False
-    if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if not collective:
+            return False
+        # a rank without gradients still takes part in the group's decision
+        from ..torch.state_mod import state
+
+        flag = torch.zeros(1, dtype=torch.float32, device=state.device)
+    if collective:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     return bool(flag.item() > 0)

@@ -219,9 +219,14 @@ class DistributedOptimizer:
         return state.pgs.mp
 
     def _check_overflow(self):
+        """Skip-step decision shared by every rank whose gradients differ: the model-parallel
+        group, or the whole world when the gradients are sharded (optimizer-state sharding,
+        sharded data parallelism) -- otherwise one shard's inf would make only its rank skip
+        the step and halve its loss scale, and shards / scales would diverge."""
         grads = [self._grad_range(d) for d in self.domains]
-        return any_overflow(grads, self._model_parallel_group() if state.core.mp_size() > 1 or
-                            state.cfg.shard_optimizer_state else None)
+        sharded = state.cfg.shard_optimizer_state or state.sdp is not None
+        group = state.pgs.world if sharded else (self._model_parallel_group() if state.core.mp_size() > 1 else None)
+        return any_overflow(grads, group)
 
     def clip_master_grads(self, max_norm, norm_type=2):
         """Global L2 norm of the (unscaled) gradients across all ranks holding distinct
@@ -343,20 +348,58 @@ class DistributedOptimizer:
                 r.allgather_params()
 
     # ----------------------------------------------------------- state dicts
+    _STATE_KEYS = ("master", "m", "v")
+
+    def _param_pieces(self, d):
+        """(name, numel, lo, hi, dlo, dhi): elements [lo, hi) of parameter `name` live at
+        [dlo, dhi) of domain d (a bucket, or this rank's shard of it)."""
+        flat = state.model.flat_groups[d.key]
+        out = []
+        for p in d.params:
+            off, n = flat.offsets[p], p.numel()
+            a, b = max(off, d.start), min(off + n, d.end)
+            if a < b:
+                out.append((flat.name_of[p], n, a - off, b - off, a - d.start, b - d.start))
+        return out
+
     def local_optimizer_state_dict(self):
+        """Per-parameter optimizer state (reference format: a torch optimizer state_dict per
+        parameter, `optimizers/optimizer.py:150-200`): fp32 master / first / second moments
+        keyed by parameter NAME and element range, independent of the flat-buffer layout, so
+        a checkpoint loads after a change of bucket cap or parameter-group order.  The
+        generic (non-fused) path keeps the inner optimizer's domain-bound state, with the
+        layout recorded and verified on load."""
         if self._offload is not None:
             self._offload.wait()  # host copies of the last step are complete
-        return {
+        sd = {
+            "format": "smp_amd_per_param_v1",
             "kind": self.kind,
-            "domains": [
-                {k: (getattr(d, k).detach().cpu() if getattr(d, k) is not None else None)
-                 for k in ("master", "m", "v")} | {"key": d.key, "start": d.start, "end": d.end}
-                for d in self.domains
-            ],
             "step_count": list(self._step_count),
             "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.optimizer.param_groups],
-            "inner": self.optimizer.state_dict() if self.kind == "generic" else None,
         }
+        if self.kind == "generic" or state.sdp is not None:
+            # domain-bound: the generic path's inner optimizer state, and sharded data
+            # parallelism (whose files are per shard rank and need the same layout anyway)
+            sd["domains"] = [
+                {k: (getattr(d, k).detach().cpu() if getattr(d, k) is not None else None) for k in self._STATE_KEYS}
+                | {"key": d.key, "start": d.start, "end": d.end}
+                | ({"names": [(n, lo, hi) for n, _, lo, hi, _, _ in self._param_pieces(d)]} if state.sdp is None else {})
+                for d in self.domains
+            ]
+            sd["inner"] = self.optimizer.state_dict() if self.kind == "generic" else None
+            return sd
+        params = {}
+        for d in self.domains:
+            for name, numel, lo, hi, dlo, dhi in self._param_pieces(d):
+                e = params.setdefault(name, {"numel": numel, "pieces": []})
+                piece = {"lo": lo, "hi": hi}
+                for k in self._STATE_KEYS:
+                    t = getattr(d, k)
+                    if t is not None:
+                        piece[k] = t[dlo:dhi].detach().to("cpu", copy=True)
+                e["pieces"].append(piece)
+        sd["params"] = params
+        return sd
 
     def local_fp16_state_dict(self):
         return {"loss_scaler": self.loss_scaler.state_dict(), "fp16": self.fp16, "bf16": self.bf16}
@@ -369,14 +412,59 @@ class DistributedOptimizer:
     def state_dict(self):
         return self.local_state_dict()
 
-    def load_local_optimizer_state_dict(self, sd):
-        if len(sd["domains"]) != len(self.domains):
-            raise SMPInvalidArgumentError("optimizer state does not match the current partition/sharding layout")
-        for d, s in zip(self.domains, sd["domains"]):
-            for k in ("master", "m", "v"):
+    def _load_per_param(self, saved):
+        """Copy every saved (name, element range) piece into the domains that hold it now."""
+        for d in self.domains:
+            for name, numel, lo, hi, dlo, dhi in self._param_pieces(d):
+                e = saved.get(name)
+                if e is None:
+                    raise SMPInvalidArgumentError(f"optimizer checkpoint has no state for parameter {name}")
+                if e["numel"] != numel:
+                    raise SMPInvalidArgumentError(
+                        f"optimizer checkpoint: parameter {name} has {e['numel']} elements, the model {numel}")
+                covered = 0
+                for pc in e["pieces"]:
+                    a, b = max(lo, pc["lo"]), min(hi, pc["hi"])
+                    if a >= b:
+                        continue
+                    covered += b - a
+                    for k in self._STATE_KEYS:
+                        t = getattr(d, k)
+                        if t is not None and k in pc:
+                            t[dlo + (a - lo):dlo + (b - lo)].copy_(pc[k][a - pc["lo"]:b - pc["lo"]].to(t.device))
+                if covered < hi - lo:
+                    raise SMPInvalidArgumentError(
+                        f"optimizer checkpoint covers {covered} of elements [{lo}, {hi}) of {name} on this rank "
+                        "(the optimizer-state sharding layout changed; save and load with the same layout)")
+
+    def _load_domains(self, sd):
+        """Generic / legacy domain-bound state: the layout must match exactly."""
+        doms = sd["domains"]
+        if len(doms) != len(self.domains):
+            raise SMPInvalidArgumentError(
+                f"optimizer state has {len(doms)} domains, the current layout {len(self.domains)} "
+                "(partition / sharding / bucket layout changed)")
+        for d, s in zip(self.domains, doms):
+            if (s.get("key"), s.get("start"), s.get("end")) != (d.key, d.start, d.end):
+                raise SMPInvalidArgumentError(
+                    f"optimizer state domain {(s.get('key'), s.get('start'), s.get('end'))} does not match the "
+                    f"current layout {(d.key, d.start, d.end)}")
+            if "names" in s and state.sdp is None:
+                cur = [(n, lo, hi) for n, _, lo, hi, _, _ in self._param_pieces(d)]
+                if [tuple(x) for x in s["names"]] != cur:
+                    raise SMPInvalidArgumentError(f"optimizer state domain {d.key}[{d.start}:{d.end}] holds "
+                                                  "different parameters than the current layout")
+            for k in self._STATE_KEYS:
                 t = getattr(d, k)
                 if t is not None and s.get(k) is not None:
                     t.copy_(s[k].to(t.device))
+
+    def load_local_optimizer_state_dict(self, sd):
+        if "params" in sd:
+            self._load_per_param(sd["params"])
+        else:
+            self._load_domains(sd)
+        for d in self.domains:
             lowp = self.fp16 or self.bf16
             if lowp:
                 src = d.master.to(self._param_range(d).device, non_blocking=False)

@@ -12,7 +12,10 @@ File layout and semantics follow the reference (`smp/torch/checkpoint.py:124-535
 
 Loading validates the number of parts (v1/v2/v3 names), verifies ``smp_config.pt``
 (pp/tp/sharding must match to load optimizer state) and defers model/optimizer loads
-until those objects exist.  Files are always read with ``weights_only=True``.
+until those objects exist.  Files are read with ``weights_only=True`` (``user_content`` too,
+unless the caller passes ``trust_user_content=True``).  Optimizer state is stored per
+parameter NAME and element range (optimizers/optimizer.py), so a checkpoint survives
+changes of the gradient bucket cap or of the parameter-group order.
 """
 import glob
 import os
@@ -199,7 +202,10 @@ def verify_smp_config(saved, partial=True, load_optimizer=True):
 
 
 def resume_from_checkpoint(path, tag=None, partial=True, strict=True, load_optimizer=True,
-                           load_sharded_optimizer_state=True, translate_function=None):
+                           load_sharded_optimizer_state=True, translate_function=None, trust_user_content=False):
+    """... (reference `checkpoint.py:381-484`).  ``user_content`` is loaded with
+    ``weights_only=True`` (tensors, containers, numbers, strings); pass
+    ``trust_user_content=True`` to unpickle arbitrary objects from a checkpoint you trust."""
     core = _c()
     if tag is None:
         if not partial:
@@ -256,5 +262,12 @@ def resume_from_checkpoint(path, tag=None, partial=True, strict=True, load_optim
 
     uc = os.path.join(ckpt, "user_content.pt") if partial else os.path.join(path, f"user_content_{tag}")
     if os.path.isfile(uc):
-        return torch.load(uc, weights_only=False, map_location="cpu")
+        try:
+            return torch.load(uc, weights_only=not trust_user_content, map_location="cpu")
+        except Exception as e:  # noqa: BLE001 - surface the safe-loader refusal clearly
+            if trust_user_content:
+                raise
+            raise CheckpointingError(
+                f"user_content at {uc} holds objects the safe loader refuses ({e}); if you trust this "
+                "checkpoint, call resume_from_checkpoint(..., trust_user_content=True)") from e
     return None

@@ -56,3 +56,25 @@ def test_sharded_dp_checkpoint(tmp_path):
     assert {"model_0.pt", "model_1.pt", "optimizer_0.pt", "optimizer_1.pt"} <= set(
         os.listdir(os.path.join(ckpt, "t_partial")))
     _phase("load", 2, ckpt, 1, 1, True, extra)
+
+
+@pytest.mark.parametrize("pp", [1, 2])
+def test_partial_resume_after_bucket_cap_change(tmp_path, pp):
+    """Optimizer state is keyed by parameter name and element range: a checkpoint written
+    with many small gradient buckets resumes bit-for-bit into a one-bucket layout."""
+    ckpt = str(tmp_path)
+    extra = {"dm_kwargs_save": {"bucket_cap_mb": 0.01}, "dm_kwargs_load": {"bucket_cap_mb": 50}}
+    _phase("save", 2, ckpt, pp, 1, True, extra)
+    _phase("load", 2, ckpt, pp, 1, True, extra)
+
+
+def test_partial_resume_after_bucket_cap_change_sharded_optimizer(tmp_path):
+    """With optimizer-state sharding each rank keeps a slice of every bucket; a changed
+    bucket cap moves the slice boundaries, so the load must refuse (not silently misplace
+    moments) -- the reference requires the same sharding layout too (checkpoint.py:506-524)."""
+    ckpt = str(tmp_path)
+    extra = {"cfg": {"shard_optimizer_state": True}, "dm_kwargs_save": {"bucket_cap_mb": 0.01},
+             "dm_kwargs_load": {"bucket_cap_mb": 50}}
+    _phase("save", 2, ckpt, 1, 1, True, extra)
+    with pytest.raises(AssertionError, match="sharding layout changed"):
+        _phase("load", 2, ckpt, 1, 1, True, extra)

@@ -165,3 +165,8 @@ def test_pp2_tp2_record_and_replay_under_jitter(pipe):
 def test_pp2_static_mode_replay_without_tp():
     _run(2, 2, 1, 3, steps=4, extra={"cfg": {"static_mode": True}, "expect_replay": True},
          env={"SMP_REPLAY_RECORD_STEPS": "2"})
+
+
+def test_sharded_dp_fp16_overflow_skips_on_every_rank():
+    outs = run_workers("sdp_overflow", 2, [], timeout=200)
+    assert all("OK" in o for o in outs)

@@ -85,7 +85,7 @@ for _ in range(4):
     opt.zero_grad(); losses.append(float(train(m, ids).reduce_mean())); opt.step()
 sd = opt.local_optimizer_state_dict()
 torch.save({"losses": losses, "params": {n: p.detach().float().cpu() for n, p in m.named_parameters()},
-            "m0": sd["domains"][0]["m"]}, sys.argv[2])
+            "m0": torch.cat([pc["m"] for e in sd["params"].values() for pc in e["pieces"]])}, sys.argv[2])
 print("RUN_OK", losses)
 """
 

@@ -38,7 +38,8 @@ def main():
     if pp > 1:
         for i, layer in enumerate(net.transformer.seq_layers):
             smp.set_partition(layer, (i * pp) // len(net.transformer.seq_layers))
-    model = smp.DistributedModel(net)
+    dm_kwargs = extra.get("dm_kwargs_" + phase, {})
+    model = smp.DistributedModel(net, **dm_kwargs)
     opt = smp.DistributedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=0.01))
 
     @smp.step
