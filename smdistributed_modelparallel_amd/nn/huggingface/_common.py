@@ -103,6 +103,32 @@ def masked_from_hf(mask):
     return mask < 0
 
 
+def block_mask_from_hf(mask):
+    """The per-block mask of an HF decoder (``create_causal_mask``: None, or 4-D causal AND
+    key-padding) for a layer that applies causality itself: reduced to the key-padding row
+    [B, 1, 1, sk] when it is exactly causal | padding (so attention stays on the flash
+    kernel's key-bias path), None when nothing is padded, else the full bool mask.  The
+    decision is cached on the mask tensor, which HF shares across all blocks of a step."""
+    if mask is None or mask.dim() != 4 or mask.shape[-2] == 1:
+        return masked_from_hf(mask)
+    cached = getattr(mask, "_smp_block_mask", None)
+    if cached is not None:
+        return cached[0]
+    masked = masked_from_hf(mask)
+    sq, sk = masked.shape[-2], masked.shape[-1]
+    keypad = masked[:, :, -1:, :]
+    causal = torch.ones(sq, sk, dtype=torch.bool, device=masked.device).triu_(1 + sk - sq)
+    if torch.equal((keypad | causal).expand_as(masked), masked):
+        out = keypad if bool(keypad.any()) else None
+    else:
+        out = masked
+    try:
+        mask._smp_block_mask = (out,)
+    except (AttributeError, RuntimeError):  # pragma: no cover
+        pass
+    return out
+
+
 def causal_lm_output(out, labels_given):
     from transformers.modeling_outputs import CausalLMOutputWithCrossAttentions
 

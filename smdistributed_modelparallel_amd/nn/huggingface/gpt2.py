@@ -5,7 +5,7 @@ state-dict translators.  Re-derived for transformers 5.x: Conv1D weights are sto
 [in, out] in HF (transposed here), c_attn is already the fused [q|k|v] projection, the LM
 head is tied to wte, pre-LayerNorm with a final ln_f.
 """
-from ._common import KeyMap, add_tied, lm_forward_hook, lm_return_hook
+from ._common import KeyMap, add_tied, block_mask_from_hf, lm_forward_hook, lm_return_hook, masked_from_hf
 
 _L = r"transformer\.h\.(\d+)\."
 _S = "transformer.seq_layers.{}."
@@ -91,3 +91,104 @@ def smp_to_hf(sd):
     out.update(rest)
     add_tied(out, "transformer.wte.weight", "lm_head.weight")
     return out
+
+
+# ----------------------------------------------------------------- GPT2Block -> layer
+# Reference `smp/torch/nn/huggingface/gpt2.py:144-290` ("huggingface-gpt-2-layer" in
+# `predefined_hooks.py:109-116`): each HF ``GPT2Block`` of a ``GPT2Model`` (one that is not
+# wrapped whole as an LM head) becomes a pre-LayerNorm causal ``DistributedTransformerLayer``.
+# The rules carry no layer prefix so they translate a block's own state dict
+# (``_match_weights``) as well as a whole model's (``transformer.h.{i}.`` prefixes);
+# the cross-attention rules come first because ``attn.``/``attention.`` also end their keys.
+LAYER_RULES = KeyMap([
+    (r"crossattention\.q_attn\.weight", "cross_attention.qkv_weight", "t"),
+    (r"crossattention\.q_attn\.bias", "cross_attention.qkv_bias", "copy"),
+    (r"crossattention\.c_attn\.weight", "cross_attention.kv_weight", "t"),
+    (r"crossattention\.c_attn\.bias", "cross_attention.kv_bias", "copy"),
+    (r"crossattention\.c_proj\.weight", "cross_attention.dense_weight", "t"),
+    (r"crossattention\.c_proj\.bias", "cross_attention.dense_bias", "copy"),
+    (r"ln_cross_attn\.weight", "cross_attention.pre_layernorm_module.weight", "copy"),
+    (r"ln_cross_attn\.bias", "cross_attention.pre_layernorm_module.bias", "copy"),
+    (r"ln_1\.weight", "attention.pre_layernorm_module.weight", "copy"),
+    (r"ln_1\.bias", "attention.pre_layernorm_module.bias", "copy"),
+    (r"attn\.c_attn\.weight", "attention.qkv_weight", "t"),
+    (r"attn\.c_attn\.bias", "attention.qkv_bias", "copy"),
+    (r"attn\.c_proj\.weight", "attention.dense_weight", "t"),
+    (r"attn\.c_proj\.bias", "attention.dense_bias", "copy"),
+    (r"ln_2\.weight", "output.pre_layernorm_module.weight", "copy"),
+    (r"ln_2\.bias", "output.pre_layernorm_module.bias", "copy"),
+    (r"mlp\.c_fc\.weight", "output.dense1_weight", "t"),
+    (r"mlp\.c_fc\.bias", "output.dense1_bias", "copy"),
+    (r"mlp\.c_proj\.weight", "output.dense2_weight", "t"),
+    (r"mlp\.c_proj\.bias", "output.dense2_bias", "copy"),
+])
+
+
+def layer_config_to_kwargs(config, layer_idx=None):
+    h = config.n_embd
+    return {
+        "num_attention_heads": config.n_head,
+        "attention_head_size": h // config.n_head,
+        "hidden_size": h,
+        "intermediate_size": config.n_inner if config.n_inner is not None else 4 * h,
+        "attention_dropout_prob": config.attn_pdrop,
+        "hidden_dropout_prob": config.resid_pdrop,
+        "activation": _activation(config.activation_function),
+        "layernorm_epsilon": config.layer_norm_epsilon,
+        "add_cross_attention": bool(getattr(config, "add_cross_attention", False)),
+        "initializer_range": config.initializer_range,
+        "use_normal_initialization": True,
+        "pre_layernorm": True,
+        "post_layernorm": False,
+        "causal_mask_size": config.n_positions,
+        "scale_attn_by_layer_idx": bool(getattr(config, "scale_attn_by_inverse_layer_idx", False)),
+        "layer_idx": layer_idx or 0,
+    }
+
+
+def layer_init_hook(config, layer_idx=None, *args, **kwargs):
+    return (), layer_config_to_kwargs(config, layer_idx)
+
+
+def layer_forward_hook(hidden_states, past_key_values=None, attention_mask=None, encoder_hidden_states=None,
+                       encoder_attention_mask=None, use_cache=False, **kwargs):
+    """HF ``GPT2Block.forward`` signature -> the layer's input tuple.  ``position_ids`` and
+    other pass-through kwargs are ignored (GPT-2 positions live in the embedding); an
+    incremental-decoding cache is refused (the layer keeps no KV cache), as the reference
+    refuses ``use_cache``."""
+    if kwargs.get("output_attentions"):
+        raise NotImplementedError("output_attentions is not supported by the distributed GPT-2 layer")
+    if past_key_values is not None and past_key_values.get_seq_length() > 0:
+        raise NotImplementedError("past_key_values (incremental decoding) is not supported by the distributed GPT-2 layer")
+    mask = block_mask_from_hf(attention_mask)
+    if encoder_hidden_states is not None:
+        return ((hidden_states, mask, encoder_hidden_states, masked_from_hf(encoder_attention_mask)),), {}
+    return ((hidden_states, mask),), {}
+
+
+def layer_return_hook(out):
+    return out[0]
+
+
+def layer_hf_to_smp(sd):
+    out = {}
+    out.update(LAYER_RULES.hf_to_smp(sd, out))
+    return out
+
+
+def layer_smp_to_hf(sd):
+    out = {}
+    out.update(LAYER_RULES.smp_to_hf(sd, out))
+    add_tied(out, "transformer.wte.weight", "lm_head.weight")  # whole-model dicts: the tied head
+    return out
+
+
+class _LayerFamily:
+    init_hook = staticmethod(layer_init_hook)
+    forward_hook = staticmethod(layer_forward_hook)
+    return_hook = staticmethod(layer_return_hook)
+    hf_to_smp = staticmethod(layer_hf_to_smp)
+    smp_to_hf = staticmethod(layer_smp_to_hf)
+
+
+LAYER = _LayerFamily

@@ -1,8 +1,9 @@
 """Predefined tensor-parallel mappings for HF transformers models.
 
 Reference: `smp/torch/nn/predefined_hooks.py:5-168` -- GPT2LMHeadModel / GPTJForCausalLM /
-GPTNeoForCausalLM / GPTNeoXForCausalLM -> DistributedTransformerLMHead, BertEncoder /
-RobertaEncoder -> DistributedTransformer, each with init / forward / return hooks and
+GPTNeoForCausalLM / GPTNeoXForCausalLM -> DistributedTransformerLMHead, GPT2Block ->
+DistributedTransformerLayer ("huggingface-gpt-2-layer"), BertEncoder / RobertaEncoder ->
+DistributedTransformer, each with init / forward / return hooks and
 HF<->smp state-dict translators.  Re-targeted to transformers 5.x module and parameter
 names.  A model marked with ``smp.tensor_parallelism()`` (or created under
 ``smp.model_creation(tensor_parallelism=True)``) is replaced by the distributed module at
@@ -22,6 +23,12 @@ def _families():
         from transformers import GPT2LMHeadModel
 
         out.append((GPT2LMHeadModel, "lm", gpt2))
+    except Exception:  # pragma: no cover
+        pass
+    try:
+        from transformers.models.gpt2.modeling_gpt2 import GPT2Block
+
+        out.append((GPT2Block, "layer", gpt2.LAYER))
     except Exception:  # pragma: no cover
         pass
     try:
@@ -58,10 +65,12 @@ def _families():
 
 
 def register_predefined_hooks(registry):
-    from ..transformer import DistributedTransformer, DistributedTransformerLMHead
+    from ..transformer import DistributedTransformer, DistributedTransformerLayer, DistributedTransformerLMHead
 
+    kinds = {"lm": DistributedTransformerLMHead, "encoder": DistributedTransformer,
+             "layer": DistributedTransformerLayer}
     for cls, kind, mod in _families():
-        dist_cls = DistributedTransformerLMHead if kind == "lm" else DistributedTransformer
+        dist_cls = kinds[kind]
         registry.register(cls, dist_cls, init_hook=mod.init_hook, forward_hook=mod.forward_hook,
                           return_hook=mod.return_hook, translate_functions=(mod.smp_to_hf, mod.hf_to_smp))
     logger.debug("registered HF predefined tensor-parallel hooks")

@@ -13,8 +13,10 @@ predefined set covers the GPT/BERT families).
 """
 from ._common import KeyMap, masked_from_hf, pack_qkv, unpack_qkv
 
-_L = r"layers\.(\d+)\."
-_S = "layers.{}."
+# no layer prefix: the rules translate one layer's own state dict (``_match_weights``) as
+# well as a whole model's (``layers.{i}.`` prefixes are carried through)
+_L = ""
+_S = ""
 RULES = KeyMap([
     (_L + r"attention\.o_proj\.weight", _S + "attention.dense_weight", "copy"),
     (_L + r"attention\.o_proj\.bias", _S + "attention.dense_bias", "copy"),
@@ -81,10 +83,10 @@ def hf_to_smp(sd):
 
 def smp_to_hf(sd):
     out = {}
-    rest = unpack_qkv(sd, out, r"layers\.(\d+)\.attention\.qkv_weight", "layers.{}.attention.q_proj.weight",
-                      "layers.{}.attention.k_proj.weight", "layers.{}.attention.v_proj.weight")
-    rest = unpack_qkv(rest, out, r"layers\.(\d+)\.attention\.qkv_bias", "layers.{}.attention.q_proj.bias",
-                      "layers.{}.attention.k_proj.bias", "layers.{}.attention.v_proj.bias")
+    rest = unpack_qkv(sd, out, r"attention\.qkv_weight", "attention.q_proj.weight", "attention.k_proj.weight",
+                      "attention.v_proj.weight")
+    rest = unpack_qkv(rest, out, r"attention\.qkv_bias", "attention.q_proj.bias", "attention.k_proj.bias",
+                      "attention.v_proj.bias")
     rest = RULES.smp_to_hf(rest, out)
     out.update(rest)
     return out

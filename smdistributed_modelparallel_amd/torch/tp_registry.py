@@ -103,7 +103,7 @@ class TensorParallelismRegistry:
                 return rh(out) if rh is not None else out
 
             dist_mod.forward = wrapped
-        dist_mod.training = module.training
+        dist_mod.train(module.training)
         return dist_mod
 
 

@@ -124,6 +124,14 @@ def test_hf_gpt2_auto_tp2_matches_hf():
     assert all("OK" in o for o in outs)
 
 
+def test_hf_gpt2_blocks_tp2_match_hf():
+    """smp.set_tensor_parallelism on each GPT2Block: the blocks become TP=2
+    DistributedTransformerLayers (weights matched from HF), the rest stays HF; training
+    tracks the HF model and the state dict maps back to HF keys."""
+    outs = run_workers("hf_gpt2_tp", 2, ["layer"], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
+    assert all("OK" in o for o in outs)
+
+
 def test_gelu_selection_follows_reference():
     """activation="gelu": erf GeLU by default, tanh with fused_bias_gelu or SMP_USE_HF_GELU=1."""
     from smdistributed_modelparallel_amd.nn import DistributedTransformerOutputLayer
@@ -186,3 +194,100 @@ def test_vit_layer_parity():
             assert torch.equal(back[k], v), k
     finally:
         reg.unpatch()
+
+
+def _gpt2_block_model(cross=False):
+    import copy
+
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gpt2
+    from smdistributed_modelparallel_amd.torch.tp_registry import TensorParallelismRegistry
+
+    reg = TensorParallelismRegistry()
+    reg.register_builtins()
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_layer=3, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0,
+                     add_cross_attention=cross, scale_attn_by_inverse_layer_idx=True)
+    hf = GPT2LMHeadModel(cfg).eval()
+    smp_model = copy.deepcopy(hf)
+    for i, block in enumerate(list(smp_model.transformer.h)):
+        smp_model.transformer.h[i] = reg.distribute(block)
+    reg.unpatch()
+    return hf, smp_model, gpt2
+
+
+@pytest.mark.parametrize("padded", [False, True])
+def test_gpt2_block_layer_parity(padded):
+    """GPT2Block -> DistributedTransformerLayer ("huggingface-gpt-2-layer", reference
+    `smp/torch/nn/huggingface/gpt2.py:144-290`): every block of an HF GPT-2 replaced
+    through the predefined hooks reproduces the HF logits/loss, with a right-padded
+    attention mask too; the layer translators map a whole model's keys both ways."""
+    from smdistributed_modelparallel_amd.nn import DistributedTransformerLayer
+    from smdistributed_modelparallel_amd.nn.huggingface._common import block_mask_from_hf
+
+    hf, smp_model, gpt2 = _gpt2_block_model()
+    assert all(isinstance(b, DistributedTransformerLayer) for b in smp_model.transformer.h)
+    assert [b.layer_idx for b in smp_model.transformer.h] == [0, 1, 2]
+    hf_sd = hf.state_dict()
+    missing, unexpected = smp_model.load_state_dict(gpt2.layer_hf_to_smp(hf_sd), strict=True)
+    assert not missing and not unexpected
+    ids = torch.randint(0, 97, (2, 16))
+    am = torch.ones(2, 16, dtype=torch.long)
+    if padded:
+        am[1, 11:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=ids, attention_mask=am, labels=ids, use_cache=False)
+        out = smp_model(input_ids=ids, attention_mask=am, labels=ids, use_cache=False)
+    valid = am.bool()
+    assert torch.allclose(out.logits[valid], ref.logits[valid], atol=2e-4, rtol=1e-3), \
+        (out.logits[valid] - ref.logits[valid]).abs().max()
+    if not padded:
+        assert abs(out.loss.item() - ref.loss.item()) < 1e-4
+    back = gpt2.layer_smp_to_hf(smp_model.state_dict())
+    assert set(back) == set(hf_sd)
+    for k, v in hf_sd.items():
+        assert torch.equal(back[k], v), k
+    # HF's causal|padding 4-D mask reduces to the key-padding row (flash key-bias path)
+    m4 = torch.zeros(2, 1, 16, 16, dtype=torch.bool)
+    causal = torch.ones(16, 16, dtype=torch.bool).tril()
+    m4[:] = causal
+    m4[1, :, :, 11:] = False
+    red = block_mask_from_hf(m4)
+    assert red.shape == (2, 1, 1, 16) and red[1, 0, 0, 11:].all() and not red[0].any()
+    assert block_mask_from_hf(causal.expand(2, 1, 16, 16).clone()) is None
+    odd = m4.clone()
+    odd[0, 0, 5, 2] = False  # not causal|padding: kept whole
+    assert block_mask_from_hf(odd).shape == (2, 1, 16, 16)
+
+
+def test_gpt2_block_layer_cross_attention_parity():
+    from transformers import GPT2Config, GPT2Model
+
+    hf, smp_model, gpt2 = _gpt2_block_model(cross=True)
+    smp_model.load_state_dict(gpt2.layer_hf_to_smp(hf.state_dict()), strict=True)
+    ids = torch.randint(0, 97, (2, 12))
+    enc = torch.randn(2, 7, 64)
+    enc_mask = torch.ones(2, 7, dtype=torch.long)
+    enc_mask[0, 5:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=ids, encoder_hidden_states=enc, encoder_attention_mask=enc_mask, use_cache=False).logits
+        out = smp_model(input_ids=ids, encoder_hidden_states=enc, encoder_attention_mask=enc_mask,
+                        use_cache=False).logits
+    assert torch.allclose(out, ref, atol=2e-4, rtol=1e-3), (out - ref).abs().max()
+    assert GPT2Config and GPT2Model
+
+
+def test_gpt2_block_refuses_kv_cache_decoding():
+    hf, smp_model, gpt2 = _gpt2_block_model()
+    ids = torch.randint(0, 97, (1, 8))
+    with torch.no_grad():
+        out = smp_model(input_ids=ids, use_cache=True)  # an empty cache is harmless
+        with pytest.raises(NotImplementedError):
+            smp_model(input_ids=ids[:, -1:], past_key_values=out.past_key_values if out.past_key_values is not None
+                      and out.past_key_values.get_seq_length() > 0 else _filled_cache(hf, ids), use_cache=True)
+
+
+def _filled_cache(hf, ids):
+    with torch.no_grad():
+        return hf(input_ids=ids, use_cache=True).past_key_values

@@ -5,24 +5,34 @@ import torch
 from transformers import GPT2Config, GPT2LMHeadModel
 
 import smdistributed_modelparallel_amd.torch as smp
-from smdistributed_modelparallel_amd.nn import DistributedTransformerLMHead
+from smdistributed_modelparallel_amd.nn import DistributedTransformerLayer, DistributedTransformerLMHead
 from smdistributed_modelparallel_amd.nn.huggingface import gpt2
 
 
 def main():
     import sys
 
-    match = len(sys.argv) > 1 and sys.argv[1] == "match"
+    mode = sys.argv[1] if len(sys.argv) > 1 else ""
+    match = mode in ("match", "layer")
     cfg = GPT2Config(n_layer=2, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0,
                      resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)
     torch.manual_seed(0)
     ref = GPT2LMHeadModel(cfg)
     smp.init({"tensor_parallel_degree": 2, "ddp": True, "_match_weights": match})
     torch.manual_seed(0)
-    with smp.model_creation(tensor_parallelism=True):
-        net = GPT2LMHeadModel(cfg)  # same seed: the same initial weights as ref
-    model = smp.DistributedModel(net)
-    assert isinstance(model.get_module(), DistributedTransformerLMHead), type(model.get_module())
+    if mode == "layer":
+        # "huggingface-gpt-2-layer": only the GPT2Blocks are distributed (embeddings, ln_f
+        # and the tied head stay HF modules), their weights matched from the HF blocks
+        net = GPT2LMHeadModel(cfg)
+        for block in net.transformer.h:
+            smp.set_tensor_parallelism(block, True)
+        model = smp.DistributedModel(net)
+        assert all(isinstance(b, DistributedTransformerLayer) for b in model.get_module().transformer.h)
+    else:
+        with smp.model_creation(tensor_parallelism=True):
+            net = GPT2LMHeadModel(cfg)  # same seed: the same initial weights as ref
+        model = smp.DistributedModel(net)
+        assert isinstance(model.get_module(), DistributedTransformerLMHead), type(model.get_module())
     if not match:
         model.load_state_dict(ref.state_dict(), translate_function=gpt2.hf_to_smp)
     # (match: _match_weights already gave every TP rank its slices of the HF weights)
@@ -49,7 +59,7 @@ def main():
         assert abs(loss - rl[smp.rank()].item()) < 1e-4, (it, loss, rl[smp.rank()].item())
     # full state dict comes back in HF key space
     sd = model.state_dict(gather_to_rank0=False)
-    hf_sd = gpt2.smp_to_hf(sd)
+    hf_sd = gpt2.layer_smp_to_hf(sd) if mode == "layer" else gpt2.smp_to_hf(sd)
     worst = max((hf_sd[k].float() - v.detach().float()).abs().max().item() for k, v in ref.state_dict().items())
     assert worst < 2e-4, worst
     print(f"rank {smp.rank()} OK", flush=True)
