@@ -147,6 +147,14 @@ def _local_ip(master_addr):
         return "127.0.0.1"
 
 
+_INIT_GENERATION = [0]
+
+
+def _next_init_generation():
+    _INIT_GENERATION[0] += 1
+    return _INIT_GENERATION[0]
+
+
 class ModelParallelCore:
     def __init__(self):
         self.cfg = None
@@ -214,10 +222,13 @@ class ModelParallelCore:
         self.mailbox = rt.Mailbox(self._rank, self._size)
         host = _local_ip(os.environ.get("MASTER_ADDR", "127.0.0.1"))
         port = self.mailbox.listen("0.0.0.0" if host != "127.0.0.1" else "127.0.0.1")
-        store.set(f"smp/mailbox/{self._rank}", f"{host}:{port}")
+        # keys are per init generation: after smp.reset() + smp.init() a peer must never
+        # read the previous mailbox's address (every rank re-initialises the same times)
+        gen = _next_init_generation()
+        store.set(f"smp/mailbox/{gen}/{self._rank}", f"{host}:{port}")
         hosts, ports = [], []
         for r in range(self._size):
-            h, p = store.get(f"smp/mailbox/{r}").decode().rsplit(":", 1)
+            h, p = store.get(f"smp/mailbox/{gen}/{r}").decode().rsplit(":", 1)
             hosts.append(h)
             ports.append(int(p))
         self.mailbox.connect(hosts, ports, float(os.environ.get("SMP_CONNECT_TIMEOUT", "300")))

@@ -66,6 +66,37 @@ class MissingPathFromComputationToLossError(SMPRuntimeError):
     pass
 
 
+class MissingPathFromComputationToModuleOutputError(SMPRuntimeError):
+    """A remote module's output has no autograd path to the outputs of the module that
+    called it (reference `torch/exceptions.py:527-541`)."""
+
+    def __init__(self, parent_module_name, module_name):
+        super().__init__(parent_module_name, module_name)
+        self.parent_module_name = parent_module_name
+        self.module_name = module_name
+
+    def __str__(self):
+        return (f"during execution of {self.parent_module_name!r}: the output of module {self.module_name!r} has no "
+                "path to the outputs backward is called on; use it, detach it, or set "
+                "SMP_SKIP_GRAPH_VALIDATION=1 (the pipeline engine then runs the graph, the unused output gets no "
+                "gradient)")
+
+
+class MissingPathFromModuleInputToModuleOutputError(SMPRuntimeError):
+    """An input of a pipeline-executed module requires grad but does not reach the
+    module's outputs (reference `torch/exceptions.py:543-556`)."""
+
+    def __init__(self, module_name, idx):
+        super().__init__(module_name, idx)
+        self.module_name = module_name
+        self.idx = idx
+
+    def __str__(self):
+        return (f"during execution of {self.module_name!r}: input tensor #{self.idx} requires grad but has no path "
+                "to the module outputs; detach it, or set SMP_SKIP_GRAPH_VALIDATION=1 (the input then gets no "
+                "gradient)")
+
+
 class DistributedModelNotWrappedError(SMPRuntimeError):
     pass
 

@@ -3,7 +3,6 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include "grad_counter.h"
 #include "mailbox.h"
 #include "timeline.h"
 
@@ -96,18 +95,4 @@ PYBIND11_MODULE(_smprt, m) {
       .def("range_pop", &Timeline::range_pop)
       .def("now_us", &Timeline::now_us)
       .def("flush", &Timeline::flush);
-
-  py::class_<GradCounter>(m, "GradCounter")
-      .def(py::init<const std::vector<std::string>&, int>())
-      .def("increment_expected_num_grads", &GradCounter::increment_expected_num_grads)
-      .def("mark_grad_computed", &GradCounter::mark_grad_computed)
-      .def("mark_fwd_pass_done", &GradCounter::mark_fwd_pass_done)
-      .def("is_grad_ready", &GradCounter::is_grad_ready)
-      .def("all_forwards_done", &GradCounter::all_forwards_done)
-      .def("get_param_grad_count", &GradCounter::get_param_grad_count)
-      .def("get_seen_grad_count", &GradCounter::get_seen_grad_count)
-      .def("set_microbatch", &GradCounter::set_microbatch)
-      .def_property_readonly("microbatch", &GradCounter::microbatch)
-      .def("clear_minibatch_state", &GradCounter::clear_minibatch_state)
-      .def_property_readonly("num_params", &GradCounter::num_params);
 }

@@ -17,6 +17,7 @@
 #include <pybind11/stl.h>
 #include <torch/csrc/autograd/function.h>
 #include <torch/csrc/autograd/functions/accumulate_grad.h>
+#include <torch/csrc/autograd/variable.h>
 #include <torch/extension.h>
 
 #include <unordered_map>
@@ -144,7 +145,71 @@ class GradTracker {
   int fwd_done_count_ = 0;
 };
 
+// Graph validation (reference `patches/execution.py:57-72`): for every target tensor, does
+// the autograd graph of `roots` reach it?  A target with a grad_fn (a RemoteOutput result)
+// is matched by that node, a leaf target (an input leaf of a remote request) by its
+// AccumulateGrad node or by being a root itself.  `bridges[i]` continue the walk once
+// target i is hit: a RemoteOutput's graph goes on, through the remote stage, at the
+// tensors that were sent in that call.  The walk stops once every target is hit.
+std::vector<bool> graph_reaches(const std::vector<at::Tensor>& roots, const std::vector<at::Tensor>& targets,
+                                const std::vector<std::vector<at::Tensor>>& bridges) {
+  using torch::autograd::Node;
+  std::unordered_map<const Node*, std::vector<size_t>> by_node;
+  std::unordered_map<const c10::TensorImpl*, std::vector<size_t>> by_leaf;
+  std::vector<bool> hit(targets.size(), false);
+  size_t remaining = 0;
+  for (size_t i = 0; i < targets.size(); ++i) {
+    const auto& t = targets[i];
+    if (!t.defined() || !t.requires_grad()) continue;
+    ++remaining;
+    by_leaf[t.unsafeGetTensorImpl()].push_back(i);
+    if (const auto& fn = t.grad_fn()) {
+      by_node[fn.get()].push_back(i);
+    } else if (auto acc = torch::autograd::impl::try_get_grad_accumulator(t)) {
+      by_node[acc.get()].push_back(i);
+    }
+  }
+  std::unordered_set<const Node*> seen;
+  std::vector<Node*> stack;
+  std::vector<const at::Tensor*> pending;
+  auto mark = [&](const std::vector<size_t>& idx) {
+    for (size_t i : idx)
+      if (!hit[i]) {
+        hit[i] = true;
+        --remaining;
+        if (i < bridges.size())
+          for (const auto& b : bridges[i]) pending.push_back(&b);
+      }
+  };
+  auto push_root = [&](const at::Tensor& r) {
+    if (!r.defined() || !r.requires_grad()) return;
+    auto lt = by_leaf.find(r.unsafeGetTensorImpl());
+    if (lt != by_leaf.end()) mark(lt->second);
+    const auto& fn = r.grad_fn();
+    if (fn && seen.insert(fn.get()).second) stack.push_back(fn.get());
+  };
+  for (const auto& r : roots) push_root(r);
+  while (remaining > 0 && (!stack.empty() || !pending.empty())) {
+    while (!pending.empty()) {
+      const at::Tensor* t = pending.back();
+      pending.pop_back();
+      push_root(*t);
+    }
+    if (stack.empty()) continue;
+    Node* n = stack.back();
+    stack.pop_back();
+    auto it = by_node.find(n);
+    if (it != by_node.end()) mark(it->second);
+    for (const auto& e : n->next_edges()) {
+      if (e.function && seen.insert(e.function.get()).second) stack.push_back(e.function.get());
+    }
+  }
+  return hit;
+}
+
 void register_grad_tracker(py::module& m) {
+  m.def("graph_reaches", &graph_reaches, py::arg("roots"), py::arg("targets"),
+        py::arg("bridges") = std::vector<std::vector<at::Tensor>>());
   py::class_<GradTracker>(m, "GradTracker")
       .def(py::init<const std::vector<at::Tensor>&, int>(), py::arg("params"), py::arg("num_microbatches"))
       .def("reset", &GradTracker::reset)

@@ -7,14 +7,13 @@ Reference parity (`smp/torch/nn/utils.py:45-844`):
 * collectives with forward/backward pairs: all-reduce (f/g), all-gather <-> narrow,
   reduce-scatter <-> all-gather, all-to-all (scatter-and-merge), sequence shard/unshard;
   uneven splits are padded to the largest shard for RCCL and un-padded after;
-* ``parameter_creation_scope`` marks parameters created in distributed modules as
-  scaled-batch parameters and initialises them *as if unsharded* (fan-in/fan-out of the
-  full layer, or N(0, initializer_range)).
+* ``mark_scaled_batch`` / ``mark_tp`` tag parameters of distributed modules (scaled-batch
+  and their TP split layout) and ``init_weight_`` initialises a shard *as if unsharded*
+  (fan-in of the full layer, or N(0, initializer_range)).
 
 With tp_size == 1 every collective is an identity (no RCCL calls).
 """
 import math
-from contextlib import contextmanager
 
 import torch
 import torch.distributed as dist
@@ -373,25 +372,6 @@ def unshard_sequence(seq_length, *tensors, dim=1):
 
 
 # ---------------------------------------------------------- parameter creation
-class _ScopeState:
-    active = []
-
-
-@contextmanager
-def parameter_creation_scope(module, scaled_batch=True, dtype=None, use_normal=False, initializer_range=0.02,
-                             fan_in=None, fan_out=None):
-    """Parameters created inside are (optionally) scaled-batch and initialised as if
-    unsharded.  `fan_in` / `fan_out` override the fans seen by nn.init (full layer dims)."""
-    _ScopeState.active.append(
-        dict(module=module, scaled_batch=scaled_batch, dtype=dtype, use_normal=use_normal,
-             initializer_range=initializer_range, fan_in=fan_in, fan_out=fan_out)
-    )
-    try:
-        yield
-    finally:
-        _ScopeState.active.pop()
-
-
 def mark_scaled_batch(param, scaled=True):
     param._smp_scaled_batch = scaled
     param._smp_distributed = True
@@ -425,10 +405,3 @@ def init_weight_(w, full_in, full_out, initializer_range=0.02, use_normal=False)
             # kaiming_uniform(a=sqrt(5)) on the full layer == U(-1/sqrt(fan_in), 1/sqrt(fan_in))
             w.uniform_(-bound, bound)
     return w
-
-
-def init_bias_(b, full_in):
-    with torch.no_grad():
-        bound = 1.0 / math.sqrt(full_in) if full_in > 0 else 0.0
-        b.uniform_(-bound, bound)
-    return b

@@ -9,7 +9,7 @@ Reference behaviour (native ``smplib.Reducer`` + ``GradCounter``, N1f/N1g;
   (``average_grads_across_microbatches``);
 * a bucket is reduced as soon as every parameter in it has its *final* gradient -- for a
   single-stage model that is the last microbatch's backward; for pipeline stages the
-  native ``GradCounter`` decides;
+  native ``GradTracker`` (csrc/torchrt/grad_tracker.cpp) decides from the autograd graph;
 * ``backward_passes_per_step`` / ``require_backward_grad_sync`` gate the reduction;
 * DDP comm hooks can replace the all-reduce.
 

@@ -162,7 +162,7 @@ def checkpoint(module, *args, preserve_rng_state=True, **kwargs):
 
 def checkpoint_sequential(sequential_module, input, strategy="each", preserve_rng_state=True,
                           pack_args_as_tuple=False):
-    children = list(sequential_module.children())
+    children = list(sequential_module)  # keeps repeated modules (children() dedups)
     if strategy == "contiguous":
         groups = [children]
     elif strategy.startswith("group_"):

@@ -51,7 +51,12 @@ import itertools
 import torch
 from greenlet import greenlet
 
-from ..backend.exceptions import PipelineParallelBWDError, SMPRuntimeError
+from ..backend.exceptions import (
+    MissingPathFromComputationToModuleOutputError,
+    MissingPathFromModuleInputToModuleOutputError,
+    PipelineParallelBWDError,
+    SMPRuntimeError,
+)
 from ..backend.logger import get_logger
 from .pipeline import MbStatus, create_pipeline
 from .serialization import stubify, unstubify
@@ -90,13 +95,14 @@ class _Token:
 
 
 class _Worker:
-    __slots__ = ("g", "mb", "kind", "result", "exc", "wait_key")
+    __slots__ = ("g", "mb", "kind", "result", "exc", "wait_key", "routs")
 
     def __init__(self, g, mb, kind):
         self.g, self.mb, self.kind = g, mb, kind
         self.result = None
         self.exc = None
         self.wait_key = None
+        self.routs = []  # (RemoteOutput result, producing module) created by this worker
 
 
 class _MbState:
@@ -117,6 +123,7 @@ class PipelineEngine:
         self._recorded = {}  # step fn id -> [(seconds, [event keys])]   (deciders only)
         self._replay = {}  # step fn id -> frozen event keys
         self._recording = None
+        self._cur_worker = None
         self.reset_step()
 
     # ------------------------------------------------------------- plumbing
@@ -404,7 +411,11 @@ class PipelineEngine:
         self._resume(w, None)
 
     def _resume(self, worker, value):
-        ret = worker.g.switch(value)
+        prev, self._cur_worker = self._cur_worker, worker
+        try:
+            ret = worker.g.switch(value)
+        finally:
+            self._cur_worker = prev
         self._after_switch(worker, ret)
 
     def _after_switch(self, worker, ret):
@@ -515,7 +526,7 @@ class PipelineEngine:
     def remote_chain_call(self, seq, start, inp):
         mm = self.state.module_manager
         name = mm.get_module_name(seq)
-        child = list(seq.children())[start]
+        child = list(seq)[start]
         owner = self._pp_peer(mm.get_partition(child))
         return self._remote_call(owner, ("chain", name, start), ((inp,), {}))
 
@@ -525,6 +536,7 @@ class PipelineEngine:
         rid = self._new_id()
         grad_enabled = torch.is_grad_enabled()
         stubbed, tensors = stubify(payload)
+        sent = []
         if grad_enabled:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
@@ -532,9 +544,10 @@ class PipelineEngine:
                 st.model._track_segment(sent)
         st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled), tensors)
         out_stubbed, out_tensors, holder, out_key = self._suspend(("res", rid))
-        return self._materialize_outputs(out_stubbed, out_tensors, holder, out_key, mb, grad_enabled)
+        producer = target[1] if target[0] == "module" else f"{target[1]}[{target[2]}:]"
+        return self._materialize_outputs(out_stubbed, out_tensors, holder, out_key, mb, grad_enabled, producer, sent)
 
-    def _materialize_outputs(self, out_stubbed, tensors, holder, out_key, mb, grad_enabled):
+    def _materialize_outputs(self, out_stubbed, tensors, holder, out_key, mb, grad_enabled, producer=None, sent=()):
         _, stubs = _stubs_of(out_stubbed)
         rg_idx = [s.index for s in stubs if s.requires_grad] if grad_enabled else []
         if rg_idx:
@@ -547,6 +560,8 @@ class PipelineEngine:
             wrapped = RemoteOutput.apply(self, holder, out_key, mb, *ins)
             for i, w in zip(rg_idx, wrapped):
                 tensors[i] = w
+            if self._cur_worker is not None:
+                self._cur_worker.routs.append((wrapped[0], producer, sent))
         return unstubify(out_stubbed, tensors)
 
     def _exec_fwd(self, src, msg, tensors):
@@ -556,14 +571,15 @@ class PipelineEngine:
         torch.set_grad_enabled(grad_enabled)
         _, stubs = _stubs_of(stubbed)
         tensors = list(tensors)
+        leaves, leaf_idx = [], []
         if grad_enabled:
-            leaves = []
             for s in stubs:
                 if s.requires_grad:
                     t = tensors[s.index].detach()
                     t.requires_grad_(True)
                     tensors[s.index] = t
                     leaves.append(t)
+                    leaf_idx.append(s.index)
             if leaves:
                 self._mb(mb).leaves[rid] = (leaves, src)
         args, kwargs = unstubify(stubbed, tensors)
@@ -571,16 +587,57 @@ class PipelineEngine:
         if target[0] == "module":
             module = mm.get_module(target[1])
             out = st.model._call_local(module, args, kwargs)
+            if grad_enabled:
+                self.validate_frame(target[1], out, leaves, leaf_idx)
             self._send_result(reply_to, result_id, mb, out, rid, grad_enabled)
         else:
             seq = mm.get_module(target[1])
-            self.run_chain(seq, target[2], args[0], reply_to, result_id, mb, rid, grad_enabled)
+            h = self.run_chain(seq, target[2], args[0], reply_to, result_id, mb, rid, grad_enabled)
+            if grad_enabled:
+                self.validate_frame(f"{target[1]}[{target[2]}:]", h, leaves, leaf_idx)
+
+    def validate_frame(self, name, out, leaves=(), leaf_idx=()):
+        """Graph validation (reference `patches/execution.py:57-72`): every result of a
+        remote module obtained while executing this frame (a remote request, or the main
+        module on pp_rank 0) and every input that requires grad must have an autograd path
+        to the frame's outputs -- else ``MissingPathFromComputationToModuleOutputError`` /
+        ``MissingPathFromModuleInputToModuleOutputError``.  The reference must refuse such
+        graphs (its backward would wait forever for the missing requests); this engine can
+        run them -- an unused path simply receives no gradient, as without pipelining -- so
+        ``SMP_SKIP_GRAPH_VALIDATION=1`` turns the check off and executes them.  The walk is
+        native (``graph_reaches`` over torch::autograd::Node edges)."""
+        w = self._cur_worker
+        routs = w.routs if w is not None else []
+        if w is not None:
+            w.routs = []
+        if not (routs or leaves) or os.environ.get("SMP_SKIP_GRAPH_VALIDATION", "0").lower() in ("1", "true"):
+            return
+        from ..ops._ext import ext
+
+        _, tensors = stubify(out)
+        roots = [t for t in tensors if t.requires_grad]
+        if not roots:
+            return  # outputs without grad: nothing flows back, as in the reference (execution.py:131-135)
+        targets = [r[0] for r in routs] + list(leaves)
+        # a reached remote result continues the walk at the tensors sent in that call (the
+        # remote side validates its own inputs -> outputs path)
+        hit = ext().graph_reaches(roots, targets, [list(r[2]) for r in routs])
+        for (_, producer, _), ok in zip(routs, hit):
+            if not ok:
+                raise MissingPathFromComputationToModuleOutputError(name, producer)
+        for idx, ok in zip(leaf_idx, hit[len(routs):]):
+            if not ok:
+                raise MissingPathFromModuleInputToModuleOutputError(name, idx)
+
+    def begin_root_frame(self):
+        if self._cur_worker is not None:
+            self._cur_worker.routs = []
 
     def run_chain(self, seq, start, h, reply_to, result_id, mb, rid, grad_enabled):
         """Execute seq's children from `start` while they are local; hand the rest to the
         next stage directly (child-to-child)."""
         mm = self.state.module_manager
-        children = list(seq.children())
+        children = list(seq)  # iter(Sequential) keeps repeated modules; children() dedups them
         me = self.core.pp_rank()
         i = start
         j = i
@@ -589,7 +646,7 @@ class PipelineEngine:
         h = self.state.model._run_local_chain(seq, children, i, j, h)
         if j == len(children):
             self._send_result(reply_to, result_id, mb, h, rid, grad_enabled)
-            return
+            return h
         nxt = self._pp_peer(mm.get_partition(children[j]))
         rid2 = self._new_id()
         stubbed, tensors = stubify(((h,), {}))
@@ -602,6 +659,7 @@ class PipelineEngine:
             nxt, ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled),
             tensors,
         )
+        return h
 
     def _send_result(self, reply_to, result_id, mb, out, rid, grad_enabled):
         stubbed, tensors = stubify(out)

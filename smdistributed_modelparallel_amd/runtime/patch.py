@@ -74,7 +74,7 @@ def run_local_chain(seq, children, i, j, h):
 
 def _seq_forward(seq, inp):
     st = state
-    children = list(seq.children())
+    children = list(seq)  # iter(Sequential) keeps repeated modules; children() dedups them
     if st.core is None or st.core.pp_size() == 1 or not st.in_step_func or st.is_tracing:
         return run_local_chain(seq, children, 0, len(children), inp)
     mm = st.module_manager

@@ -439,7 +439,12 @@ class DistributedModel(nn.Module):
     def forward(self, *args, **kwargs):
         if state.core.pp_size() > 1 and not state.in_step_func and not state.is_tracing:
             raise StepFunctionCalledError("with pipeline parallelism the model can only be called inside smp.step")
-        return self.module(*args, **kwargs)
+        if state.core.pp_size() == 1 or state.is_tracing or not torch.is_grad_enabled():
+            return self.module(*args, **kwargs)
+        state.engine.begin_root_frame()
+        out = self.module(*args, **kwargs)
+        state.engine.validate_frame("main", out)
+        return out
 
     def backward(self, tensors, grad_tensors=None):
         if state.is_tracing:

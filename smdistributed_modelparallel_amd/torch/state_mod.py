@@ -68,11 +68,9 @@ class PTModelParallelState:
         self.engine = None
         self.rng_manager = None
         self.microbatch = 0
-        self.num_microbatches_in_step = 1
         self.is_tracing = False
         self.in_step_func = False
         self.step_count = 0
-        self.checkpoint_activations_config = None
         self.loaded_model_state = None
         self.loaded_optimizer_state = None
         self.param_initializers = {}
@@ -82,8 +80,6 @@ class PTModelParallelState:
         self.transport = None
         self.p2p_mode = "cpu"
         self.sdp = None
-        self.first_step_done = False
-        self.skip_graph_validation = os.environ.get("SMP_SKIP_GRAPH_VALIDATION", "0") == "1"
         self._lock = threading.RLock()
 
     # ----------------------------------------------------------------- device

@@ -368,26 +368,6 @@ def test_native_timeline(tmp_path):
     assert any("fwd mb1" in json.dumps(e) for e in events)
 
 
-def test_native_grad_counter():
-    rt = _rt()
-    gc = rt.GradCounter(["w", "b"], 2)
-    gc.set_microbatch(0)
-    gc.increment_expected_num_grads(0, ["w", "b"])
-    gc.increment_expected_num_grads(1, ["w"])
-    gc.mark_fwd_pass_done(0)
-    gc.mark_fwd_pass_done(1)
-    assert gc.all_forwards_done()
-    assert gc.get_param_grad_count("w") == 2
-    assert not gc.is_grad_ready("w")
-    gc.mark_grad_computed("w")
-    gc.mark_grad_computed("w")
-    assert gc.is_grad_ready("w")
-    gc.mark_grad_computed("b")
-    assert gc.is_grad_ready("b")
-    gc.clear_minibatch_state()
-    assert gc.get_seen_grad_count("w") == 0
-
-
 def test_config_legacy_dp_backends():
     from smdistributed_modelparallel_amd.backend.config import ModelParallelConfig
     from smdistributed_modelparallel_amd.backend.exceptions import SMPUnsupportedError
