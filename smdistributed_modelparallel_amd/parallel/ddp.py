@@ -48,6 +48,7 @@ class BucketReducer:
         self.next_launch = 0
         self._hooks = []
         self.launched_before_sync = 0  # buckets launched while backward was still running
+        self.active_size = None  # under model.join(): ranks still training (averaging divisor)
         self._in_sync = False
         self.group_rank = dist.get_rank(group) if (group is not None and dist.is_initialized()) else 0
         if overlap or flat.fp32_accumulation:
@@ -100,7 +101,7 @@ class BucketReducer:
         b.launched = True
         self.launched_before_sync += 0 if self._in_sync else 1
         buf = self.flat.grad[b.start : b.end]
-        scale = 1.0 / (self.divisor * self.group_size)
+        scale = 1.0 / (self.divisor * (self.active_size or self.group_size))
         if scale != 1.0:
             buf.mul_(scale)
         if self.group is None or self.group_size == 1:
@@ -147,6 +148,25 @@ class BucketReducer:
                 if hasattr(b.work, "wait"):
                     b.work.wait()
                 b.work = None
+
+    def shadow(self):
+        """Joined rank (model.join): issue this reducer's bucket collectives in bucket order
+        with zero contributions, matching the ranks that are still training."""
+        works = []
+        for b in self.flat.buckets:
+            if self.group is None or self.group_size == 1:
+                continue
+            zeros = torch.zeros(b.end - b.start, dtype=self.flat.grad.dtype, device=self.flat.grad.device)
+            if self.comm_hook is not None:
+                works.append(self.comm_hook(b, zeros, self.group))
+            elif self.shard:
+                n = b.numel // self.group_size
+                works.append(dist.reduce_scatter_tensor(zeros[:n].clone(), zeros, group=self.group, async_op=True))
+            else:
+                works.append(dist.all_reduce(zeros, group=self.group, async_op=True))
+        for w in works:
+            if w is not None and hasattr(w, "wait"):
+                w.wait()
 
     def shard_range(self, b):
         n = b.numel // self.group_size

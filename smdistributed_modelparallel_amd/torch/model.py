@@ -23,6 +23,7 @@ from ..backend.collectives import CommGroup
 from ..backend.exceptions import (
     SMPInvalidArgumentError,
     SMPRuntimeError,
+    SMPUnsupportedError,
     StepFunctionCalledError,
 )
 from ..backend.logger import get_logger
@@ -418,6 +419,9 @@ class DistributedModel(nn.Module):
             if getattr(self, "grad_tracker", None) is not None:
                 self.grad_tracker.reset(state.cfg.microbatches)
         self._step_had_backward = False
+        joining = self.partitioned and getattr(self, "_join", None) is not None
+        if joining:
+            self._join_begin_step(sync)
         yield
         if not self.partitioned:
             return
@@ -428,6 +432,11 @@ class DistributedModel(nn.Module):
                     r.synchronize()
                 if state.sdp is not None:
                     state.sdp.synchronize()
+        elif joining and sync:
+            # announced a synced step to the joined ranks but ran no backward: keep the
+            # collective sequence matched
+            for r in self.reducers.values():
+                r.shadow()
         for name, hook in list(self._post_step_hooks.items()):
             if name not in self._post_step_hooks_run:
                 self._post_step_hooks_run.add(name)
@@ -609,8 +618,65 @@ class DistributedModel(nn.Module):
                 r.comm_hook = compress
 
     @contextlib.contextmanager
-    def join(self, *args, **kwargs):
-        yield
+    def join(self, divide_by_initial_world_size=True, enable=True):
+        """Uneven inputs across data-parallel ranks (reference `model.py:1556-1566`, which
+        delegates to torch DDP's join).  A rank whose data ran out leaves the ``with`` block
+        and keeps shadowing the gradient reductions of the ranks still training -- with zero
+        contributions -- until every rank has left; then the model of the rank that trained
+        the most steps is broadcast to all.  ``divide_by_initial_world_size=False`` averages
+        each step over the ranks still training instead of the full DP group.  Supported for
+        pure data parallelism (the reference requires ddp=True)."""
+        cfg = state.cfg
+        if not cfg.ddp:
+            raise SMPUnsupportedError("join is only supported when using DDP. Please set ddp=True in SMP config")
+        core = state.core
+        if not enable or core.dp_size() == 1:
+            yield
+            return
+        if core.pp_size() > 1 or core.tp_size() > 1 or state.sdp is not None or cfg.shard_optimizer_state:
+            raise SMPUnsupportedError("model.join() supports pure data parallelism (no pipeline / tensor "
+                                      "parallelism, sharded data parallelism or optimizer-state sharding)")
+        self._join = {"divide_initial": bool(divide_by_initial_world_size), "steps": 0}
+        try:
+            yield
+        except BaseException:
+            self._join = None
+            raise
+        j, self._join = self._join, None
+        for r in self.reducers.values():
+            r.active_size = None
+        self._join_shadow(j)
+
+    def _join_flag(self, active, sync):
+        flag = torch.tensor([float(active), float(sync)], device=state.device)
+        dist.all_reduce(flag, group=state.pgs.dp)
+        return int(flag[0].item()), int(flag[1].item())
+
+    def _join_begin_step(self, sync):
+        n_active, _ = self._join_flag(1, sync)
+        self._join["steps"] += 1
+        for r in self.reducers.values():
+            r.active_size = None if self._join["divide_initial"] else n_active
+
+    def _join_shadow(self, j):
+        core = state.core
+        while True:
+            n_active, n_sync = self._join_flag(0, 0)
+            if n_active == 0:
+                break
+            if n_sync > 0:
+                for r in self.reducers.values():
+                    r.shadow()
+        # the rank that trained longest (ties: highest DP rank) holds the final model
+        key = torch.tensor([float(j["steps"] * core.dp_size() + core.dp_rank())], device=state.device)
+        dist.all_reduce(key, op=dist.ReduceOp.MAX, group=state.pgs.dp)
+        src = core.ranker.translate(core.pp_rank(), core.tp_rank(), int(key.item()) % core.dp_size())
+        with torch.no_grad():
+            for flat in self.flat_groups.values():
+                dist.broadcast(flat.data, src, group=state.pgs.dp)
+            for b in self.local_buffers():
+                if b is not None and b.numel() > 0:
+                    dist.broadcast(b, src, group=state.pgs.dp)
 
     @contextlib.contextmanager
     def no_sync(self):
@@ -673,6 +739,34 @@ class DistributedModel(nn.Module):
         self._partitions_assigned = True
 
     def cpu(self):
+        """Gather the whole model onto every rank's host (reference `model.py:1530-1534`):
+        every pipeline stage's parameters and buffers are filled from the full state dict
+        (each TP rank keeps its slice layout) and the module moves to CPU -- for export /
+        inference after training.  Parameters leave the flat gradient buffers, so training
+        does not continue on this model."""
+        if not self.partitioned:
+            self.module.cpu()
+            return self
+        from .checkpoint_utils import slice_for_param
+
+        full = self.state_dict(gather_to_rank0=False, cast_to_cpu=True)
+        core = state.core
+        tp_r, tp_n = core.tp_rank(), core.tp_size()
+        with torch.no_grad():
+            for mn, m in self.module.named_modules():
+                for pn, p in list(m._parameters.items()):
+                    n = f"{mn}.{pn}" if mn else pn
+                    if p is None or n not in full:
+                        continue
+                    t = full[n]
+                    if tp_n > 1:
+                        t = slice_for_param(t, p, tp_r, tp_n)
+                    p.data = t.to(p.dtype).clone()
+                for bn, b in list(m._buffers.items()):
+                    n = f"{mn}.{bn}" if mn else bn
+                    if b is not None and n in full:
+                        m._buffers[bn] = full[n].to(b.dtype).clone()
+        self.module.cpu()
         return self
 
     def cuda(self, *args, **kwargs):

@@ -170,3 +170,19 @@ def test_pp2_static_mode_replay_without_tp():
 def test_sharded_dp_fp16_overflow_skips_on_every_rank():
     outs = run_workers("sdp_overflow", 2, [], timeout=200)
     assert all("OK" in o for o in outs)
+
+
+@pytest.mark.parametrize("mode", ["join", "join_active"])
+def test_model_join_uneven_inputs(mode):
+    """model.join(): ranks with fewer batches shadow the gradient all-reduces with zeros
+    (reference `model.py:1556-1566` -> DDP join); the result equals a single process
+    averaging each step over the initial world size (or over the active ranks)."""
+    outs = run_workers("join_cpu", 3, [mode], timeout=120)
+    assert all("OK join" in o for o in outs)
+
+
+def test_model_cpu_gathers_all_stages():
+    """model.cpu() fills every stage's parameters from the full state dict on every rank
+    (reference `model.py:1530-1534`)."""
+    outs = run_workers("join_cpu", 2, ["cpu"], timeout=120)
+    assert all("OK cpu" in o for o in outs)
