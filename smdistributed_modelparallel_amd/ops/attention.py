@@ -185,9 +185,28 @@ def _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, fp3
         # slice's backward zero-fills a full-size gradient per chunk and adds them up
         qs, ks, vs = q.split(cb), k.split(cb), v.split(cb)
         ms = [mask] * len(qs) if mask is None or mask.shape[0] == 1 else mask.split(cb)
-        outs = [_materialised_chunk(qi, ki, vi, scale, causal, mi, dropout_p, window, training, fp32)
+        outs = [_chunk(qi, ki, vi, scale, causal, mi, dropout_p, window, training, fp32)
                 for qi, ki, vi, mi in zip(qs, ks, vs, ms)]
         return torch.cat(outs, 0)
+    return _chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32)
+
+
+def _checkpoint_attentions():
+    from ..torch.state_mod import state
+
+    return state.cfg is not None and bool(getattr(state.cfg, "checkpoint_attentions", False))
+
+
+def _chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32):
+    """``checkpoint_attentions`` (reference `nn/transformer.py:1487-1496`): the materialised
+    path keeps no [b, h, sq, sk] scores / probabilities for backward -- they are recomputed
+    (same dropout decisions: the RNG state is replayed).  The flash kernels need no such
+    option: they only ever keep the output and the per-row log-sum-exp."""
+    if _checkpoint_attentions() and torch.is_grad_enabled() and any(t.requires_grad for t in (q, k, v)):
+        from torch.utils.checkpoint import checkpoint
+
+        return checkpoint(_materialised_chunk, q, k, v, scale, causal, mask, dropout_p, window, training, fp32,
+                          use_reentrant=False, preserve_rng_state=True)
     return _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, training, fp32)
 
 

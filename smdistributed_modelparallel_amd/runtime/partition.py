@@ -15,6 +15,7 @@ every rank.
 Our formulation evaluates every segment count k explicitly (instead of the reference's
 dummy-node insertion) -- same objective, simpler to verify.
 """
+import os
 import time
 from collections import defaultdict
 
@@ -374,6 +375,8 @@ def auto_partition(model, step_fn, mb_inputs):
             raise PartitionError(f"auto-partitioning failed on rank 0: {info['__error__']}")
     for name, p in info.items():
         mm._module_partitions[mm.get_module(name)] = p
+    if state.cfg.partition_file and core.local_rank() == 0:
+        save_partition_file(state.cfg.partition_file, info, core.pp_size())
     if core.rank() == 0:
         counts = defaultdict(int)
         for p in info.values():
@@ -396,3 +399,34 @@ def enforce_shared_param_colocation(model):
                 logger.warning(f"moving {mm.get_module_name(u)} to partition {target}: it shares a parameter")
                 for c in u.modules():
                     mm._module_partitions[c] = target
+
+
+# ------------------------------------------------------------ partition files
+# ``partition_file`` / ``load_partition`` (reference `backend/config.yaml:305-314`,
+# `backend/state_mod.py:38-40`, used by its TensorFlow auto-partitioner `tensorflow/auto.py:
+# 181-232`): the auto-partition result is written to ``partition_file`` (one writer per node)
+# and a later run with ``load_partition: True`` reuses it instead of tracing again.  Stored as
+# JSON {module name: stage} (never a pickle), tagged with the pipeline degree.
+DEFAULT_PARTITION_FILE = "./partition.data"
+
+
+def save_partition_file(path, info, pp_size):
+    import json
+
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        json.dump({"format": "smp_amd_partition_v1", "pipeline_parallel_degree": pp_size, "partition": info}, f)
+    os.replace(tmp, path)
+
+
+def load_partition_file(path, pp_size):
+    import json
+
+    with open(path) as f:
+        data = json.load(f)
+    if data.get("format") != "smp_amd_partition_v1":
+        raise PartitionError(f"{path} is not a partition file written by this framework")
+    if data["pipeline_parallel_degree"] != pp_size:
+        raise PartitionError(f"{path} holds a partition for pipeline_parallel_degree "
+                             f"{data['pipeline_parallel_degree']}, this run uses {pp_size}")
+    return {k: int(v) for k, v in data["partition"].items()}

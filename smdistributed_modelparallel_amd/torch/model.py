@@ -126,6 +126,12 @@ class DistributedModel(nn.Module):
         else:
             self._deferred_load = None
 
+        if state.core.pp_size() > 1 and cfg.auto_partition and cfg.load_partition and not mm.partition_loaded:
+            from ..runtime.partition import DEFAULT_PARTITION_FILE, load_partition_file
+
+            path = cfg.partition_file or DEFAULT_PARTITION_FILE
+            mm.load_partition(load_partition_file(path, state.core.pp_size()))
+            logger.info(f"loaded the model partition from {path}; auto-partitioning skipped")
         if state.core.pp_size() == 1:
             for m in module.modules():
                 mm.assign_partition(m, 0)

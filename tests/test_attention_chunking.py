@@ -24,3 +24,38 @@ def test_chunked_matches_single_shot(monkeypatch):
         monkeypatch.setattr(A, "_MAX_SCORE_ELEMS", 1 << 26)
         for r, g in zip(ref, got):
             torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
+
+
+def test_checkpoint_attentions_saves_no_scores_and_matches(monkeypatch):
+    """checkpoint_attentions (reference nn/transformer.py:1487-1496): same outputs and
+    gradients -- dropout included, the RNG state is replayed -- and no [b, h, s, s] tensor
+    is kept for backward."""
+    import types
+
+    from smdistributed_modelparallel_amd.torch.state_mod import state
+
+    torch.manual_seed(0)
+    b, s, h, d = 2, 32, 2, 8
+    q, k, v = (torch.randn(b, s, h, d) for _ in range(3))
+
+    def run(ckpt):
+        monkeypatch.setattr(state, "cfg", types.SimpleNamespace(checkpoint_attentions=ckpt))
+        qq, kk, vv = (t.clone().requires_grad_(True) for t in (q, k, v))
+        saved = []
+
+        def pack(t):
+            saved.append(tuple(t.shape))
+            return t
+
+        torch.manual_seed(3)
+        with torch.autograd.graph.saved_tensors_hooks(pack, lambda t: t):
+            o = A.attention(qq, kk, vv, causal=True, dropout_p=0.2)
+        o.backward(torch.ones_like(o))
+        return (o.detach(), qq.grad, kk.grad, vv.grad), saved
+
+    ref, saved_ref = run(False)
+    got, saved_ck = run(True)
+    for r, g in zip(ref, got):
+        torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
+    assert any(sh[-2:] == (s, s) for sh in saved_ref)
+    assert not any(len(sh) == 4 and sh[-2:] == (s, s) for sh in saved_ck)

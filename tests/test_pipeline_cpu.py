@@ -186,3 +186,13 @@ def test_model_cpu_gathers_all_stages():
     (reference `model.py:1530-1534`)."""
     outs = run_workers("join_cpu", 2, ["cpu"], timeout=120)
     assert all("OK cpu" in o for o in outs)
+
+
+def test_partition_file_save_and_load(tmp_path):
+    """partition_file / load_partition (reference config.yaml:305-314): the auto-partition
+    is written as JSON and a later run reuses it without tracing."""
+    path = str(tmp_path / "partition.data")
+    outs = run_workers("partition_file", 2, ["save", path], timeout=120)
+    assert all("OK save" in o for o in outs)
+    outs = run_workers("partition_file", 2, ["load", path], timeout=120)
+    assert all("OK load" in o for o in outs)
