@@ -122,6 +122,7 @@ class PipelineEngine:
         self._ids = itertools.count()
         self._recorded = {}  # step fn id -> [(seconds, [event keys])]   (deciders only)
         self._replay = {}  # step fn id -> frozen event keys
+        self._replay_mbs = {}  # step fn id -> microbatch of each frozen event (None: n/a)
         self._recording = None
         self._cur_worker = None
         self.reset_step()
@@ -260,10 +261,12 @@ class PipelineEngine:
             best = min(range(len(rec)), key=lambda i: rec[i][0])
         if core.mp_size() > 1:
             best = comm.bcast(best, ranker.translate(0, 0, core.rdp_rank()), CommGroup.MP_GROUP)
-        keys = rec[best][1] if core.tp_rank() == 0 else None
+        pairs = rec[best][1] if core.tp_rank() == 0 else None
         if core.tp_size() > 1:
-            keys = comm.bcast(keys, ranker.translate(core.pp_rank(), 0, core.rdp_rank()), CommGroup.TP_GROUP)
-        self._replay[sid] = list(keys)
+            pairs = comm.bcast(pairs, ranker.translate(core.pp_rank(), 0, core.rdp_rank()), CommGroup.TP_GROUP)
+        keys = [k for k, _ in pairs]
+        self._replay[sid] = keys
+        self._replay_mbs[sid] = [m for _, m in pairs]
         self._recorded.pop(sid, None)
         logger.info(f"pipeline schedule frozen for step function {sid}: recorded step {best} "
                     f"({len(keys)} events) is replayed from now on")
@@ -275,7 +278,7 @@ class PipelineEngine:
             self.replay_enabled()
         if replay is not None:
             self._tp_peers = []
-            return self._serve_follower(leader, replay=replay)
+            return self._serve_follower(leader, replay=replay, replay_mbs=self._replay_mbs.get(self.step_fn.id))
         if self._det:
             me = core.rank()
             self._tp_peers = [r for r in core.get_tp_group() if r != me]
@@ -305,10 +308,11 @@ class PipelineEngine:
                     return
                 act = self.pipeline.next_action()
                 if act is not None:
-                    self._announce(("act",) + tuple(act))
+                    self._announce(("act",) + tuple(act), act[1])
                     self._do_action(act)
                     progressed = True
             if not progressed:
+                self._idle_prefetch()
                 m = self.state.transport.poll(timeout)
                 if m is not None:
                     self._dispatch_decided(m)
@@ -318,6 +322,7 @@ class PipelineEngine:
         if kind == "fwd":
             self._traced(mb, f"FWD mb{mb} (step fn)", self._start_microbatch, mb)
         else:
+            self._prefetch_activations(mb)
             self.pipeline.set_status(mb, MbStatus.BWD)
             self._traced(mb, f"BWD mb{mb} (loss)", self._resume, self.waiting.pop(("bwd_start", mb)), None)
 
@@ -333,10 +338,10 @@ class PipelineEngine:
             return (kind, stubbed[1])
         return (kind,)
 
-    def _announce(self, key):
+    def _announce(self, key, mb=None):
         if self._det:
             if self._recording is not None:
-                self._recording.append(key)
+                self._recording.append((key, mb))
             # tagged with the step: a decider may start step t+1 while a TP peer (in
             # another pipeline) is still finishing step t
             msg = ("dec", self.state.step_count, key)
@@ -346,13 +351,16 @@ class PipelineEngine:
     def _dispatch_decided(self, m):
         src, stubbed, tensors = m
         if stubbed[0] not in ("abort", "dec"):
-            self._announce(self._event_key(src, stubbed))
+            kind = stubbed[0]
+            mb = stubbed[2] if kind in ("fwd", "res", "bwd") else (stubbed[1] if kind == "mbdone" else None)
+            self._announce(self._event_key(src, stubbed), mb)
         self._dispatch(src, stubbed, tensors)
 
-    def _serve_follower(self, leader, replay=None):
+    def _serve_follower(self, leader, replay=None, replay_mbs=None):
         """TP peer of a deciding rank (or any rank replaying a frozen schedule): execute
         events strictly in the decided order."""
         pending = {}
+        pos = 0  # index of decisions[0] in the replayed schedule
         step = self.state.step_count
         if replay is not None:
             decisions = deque(replay)
@@ -375,8 +383,11 @@ class PipelineEngine:
                 else:
                     pending[self._event_key(src, stubbed)] = m
                 m = self.state.transport.poll(0.0)
+            if replay_mbs is not None:
+                self._lookahead_prefetch(replay, replay_mbs, pos)
             while decisions and not self._stop:
                 key = decisions[0]
+                pos += 1
                 if key[0] == "act":
                     decisions.popleft()
                     self._do_action(key[1:])
@@ -391,9 +402,42 @@ class PipelineEngine:
                     decisions.popleft()
                     self._dispatch(*pending.pop(key))
                 else:
+                    pos -= 1
                     break  # the decided message has not arrived yet
             if leader and self.pipeline.is_done() and not decisions:
                 self._stop = True
+
+    # ------------------------------------------------- activation prefetching
+    def _offloader(self):
+        st = self.state
+        return st.current_offloader if (st.cfg is not None and st.cfg.offload_activations) else None
+
+    def _prefetch_activations(self, mb):
+        off = self._offloader()
+        if off is not None:
+            off.prefetch_microbatch(mb)
+
+    def _lookahead_prefetch(self, keys, mbs, pos):
+        """Replayed schedule (reference `server_queue.py:492-548`): start loading the
+        offloaded activations of every backward among the next
+        ``task_level_activation_loading_horizon`` events, so host->device copies overlap
+        the tasks before them."""
+        off = self._offloader()
+        if off is None:
+            return
+        for i in range(pos, min(len(keys), pos + max(1, int(self.state.cfg.task_level_activation_loading_horizon)))):
+            k = keys[i]
+            if k[0] == "bwd" or (k[0] == "act" and k[1] == "bwd"):
+                off.prefetch_microbatch(mbs[i] if k[0] == "bwd" else k[2])
+
+    def _idle_prefetch(self):
+        """Dynamic schedule: nothing runnable -- use the idle link to load the activations
+        of the oldest microbatch whose backward has not reached this stage yet."""
+        off = self._offloader()
+        if off is not None:
+            mb = off.next_pending_microbatch()
+            if mb is not None:
+                off.prefetch_microbatch(mb)
 
     # ----------------------------------------------------------- coroutines
     def _spawn(self, fn, mb, kind, *args):
@@ -480,6 +524,7 @@ class PipelineEngine:
             _, key, mb, grads_stubbed, remote_token = stubbed
             # a backward request for mb: its forward is over everywhere (server.py:455)
             self.state.model._mark_fwd_pass_done(mb)
+            self._prefetch_activations(mb)
             grads = unstubify(grads_stubbed, tensors)
             self._process_bwd(src, key, mb, grads, remote_token)
         elif kind == "ack":

@@ -22,7 +22,7 @@ from ..torch.state_mod import state
 
 class _Handle:
     __slots__ = ("host", "gpu", "d2h_done", "h2d_done", "device", "shape", "dtype", "requires_grad", "sharded_out",
-                 "index")
+                 "index", "mb")
 
     def __init__(self):
         self.host = self.gpu = self.d2h_done = self.h2d_done = None
@@ -39,7 +39,7 @@ class ActivationOffloader:
             self.d2h = torch.cuda.Stream(device)
             self.h2d = torch.cuda.Stream(device)
         self.handles = []  # offload order of the current step
-        self.stats = {"offloaded_bytes": 0, "loaded_bytes": 0}
+        self.stats = {"offloaded_bytes": 0, "loaded_bytes": 0, "task_prefetches": 0}
 
     # ----------------------------------------------------------------- step
     def reset(self):
@@ -53,6 +53,7 @@ class ActivationOffloader:
         h = _Handle()
         h.device, h.shape, h.dtype, h.requires_grad = t.device, t.shape, t.dtype, t.requires_grad
         h.index = len(self.handles)
+        h.mb = state.microbatch
         self.handles.append(h)
         if self._tp_skip():
             h.sharded_out = True  # tp_rank 0 holds it; the load is a broadcast
@@ -98,6 +99,24 @@ class ActivationOffloader:
                 self._issue_load(x)
                 resident += 1
             i -= 1
+
+    def prefetch_microbatch(self, mb):
+        """Task-level prefetch (engine lookahead / idle time): issue the loads of microbatch
+        `mb`'s offloaded tensors, last offloaded first (backward order), while fewer than
+        ``activation_loading_horizon`` loaded tensors are resident."""
+        resident = sum(1 for x in self.handles if x.gpu is not None)
+        for x in reversed(self.handles):
+            if resident >= self.horizon:
+                return
+            if x.mb == mb and x.gpu is None and x.host is not None and not x.sharded_out:
+                self._issue_load(x)
+                self.stats["task_prefetches"] += 1
+                resident += 1
+
+    def next_pending_microbatch(self):
+        """Oldest microbatch with offloaded tensors not yet loaded (1F1B order)."""
+        mbs = [x.mb for x in self.handles if x.gpu is None and x.host is not None and not x.sharded_out]
+        return min(mbs) if mbs else None
 
     def load(self, h):
         if h.sharded_out or (self.shard_over_tp and state.core is not None and state.core.tp_size() > 1):

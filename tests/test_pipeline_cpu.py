@@ -167,6 +167,16 @@ def test_pp2_static_mode_replay_without_tp():
          env={"SMP_REPLAY_RECORD_STEPS": "2"})
 
 
+def test_pp2_offload_task_level_prefetch_under_replay():
+    """task_level_activation_loading_horizon (reference server_queue.py:492-548): with a
+    frozen schedule the engine loads offloaded activations for the backward tasks within
+    the look-ahead window before they run; results unchanged."""
+    _run(2, 2, 1, 3, steps=4, extra={"ckpt_layers": True, "expect_replay": True, "expect_task_prefetch": True,
+                                     "cfg": {"static_mode": True, "offload_activations": True,
+                                             "task_level_activation_loading_horizon": 3}},
+         env={"SMP_REPLAY_RECORD_STEPS": "2"})
+
+
 def test_sharded_dp_fp16_overflow_skips_on_every_rank():
     outs = run_workers("sdp_overflow", 2, [], timeout=200)
     assert all("OK" in o for o in outs)

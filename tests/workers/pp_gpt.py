@@ -165,6 +165,8 @@ def main():
         st = smp.state.current_offloader.stats
         # every rank that runs checkpointed layers must have offloaded and reloaded them
         assert st["offloaded_bytes"] > 0 and st["loaded_bytes"] == st["offloaded_bytes"], st
+        if extra.get("expect_task_prefetch"):
+            assert st["task_prefetches"] > 0, st
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
 
