@@ -32,6 +32,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..backend.exceptions import SMPInvalidArgumentError
+from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
@@ -60,6 +61,8 @@ from .utils import (
     tp_size,
     unshard_sequence,
 )
+
+logger = get_logger()
 
 _LAYER_KEYS = OrderedDict(
     [
@@ -344,9 +347,22 @@ class DistributedAttentionLayer(DistributedModule):
             s = s / float(self.layer_idx + 1)
         return s
 
+    def _note_causal_mask(self, mask):
+        """One-time notice (reference `nn/transformer.py:1684-1696` warns that its fused
+        causal softmax IGNORES the attention mask unless fused_softmax=False): here a
+        padding mask is always applied together with the causal mask -- on the flash
+        kernel's key-bias path -- whatever fused_softmax says."""
+        if mask is not None and self.causal_mask_size is not None and not _CAUSAL_MASK_NOTED[0]:
+            _CAUSAL_MASK_NOTED[0] = True
+            if tp_rank() == 0:
+                logger.info("causal attention with an attention mask: the mask is applied together with the causal "
+                            "mask (the reference's fused causal softmax ignored it unless fused_softmax=False)")
+
     def core(self, a, mask=None, cross_states=None, cross_mask=None):
         """a: [B, s, h] (already normalised). Returns the dense output after the TP
         all-reduce (bias included), [B, s, h]."""
+        if not self.cross_attention:
+            self._note_causal_mask(mask)
         if self._mem:
             return self._core_memory(a, mask)
         a = (bwd_allreduce_for_tp(a, inplace_grad=True) if self._tp > 1 else a)
@@ -613,6 +629,9 @@ class DistributedTransformerLayer(DistributedModule):
         elif self._tp > 1 and self._mem and getattr(self, "_full_batch_out", False):
             hidden = _leave_tp(hidden, True, self.hidden_size, full_batch=True)
         return (hidden,) + tuple(inputs[1:])
+
+
+_CAUSAL_MASK_NOTED = [False]
 
 
 # ================================================================ transformer

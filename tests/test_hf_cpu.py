@@ -291,3 +291,55 @@ def test_gpt2_block_refuses_kv_cache_decoding():
 def _filled_cache(hf, ids):
     with torch.no_grad():
         return hf(input_ids=ids, use_cache=True).past_key_values
+
+
+@pytest.mark.parametrize("fused_softmax", [True, False])
+def test_causal_layer_applies_padding_mask(fused_softmax):
+    """Causal self-attention + key-padding mask (reference nn/transformer.py:1684-1696: its
+    fused causal softmax ignored the mask unless fused_softmax=False): the mask is applied
+    in both cases -- equal to a float64 masked-softmax reference."""
+    from smdistributed_modelparallel_amd.nn import DistributedAttentionLayer
+
+    torch.manual_seed(0)
+    layer = DistributedAttentionLayer(num_attention_heads=2, attention_head_size=8, hidden_size=16,
+                                      attention_dropout_prob=0.0, hidden_dropout_prob=0.0, causal_mask_size=32,
+                                      pre_layernorm=False, post_layernorm=False, fused_softmax=fused_softmax).eval()
+    x = torch.randn(2, 10, 16)
+    mask = torch.zeros(2, 1, 1, 10, dtype=torch.bool)
+    mask[1, ..., 7:] = True
+    with torch.no_grad():
+        out = layer.core(x, mask)
+        qkv = torch.nn.functional.linear(x.double(), layer.qkv_weight.double(), layer.qkv_bias.double())
+        q, k, v = qkv.view(2, 10, 3, 2, 8).permute(2, 0, 3, 1, 4)
+        sc = q @ k.transpose(-1, -2) / 8 ** 0.5
+        causal = torch.ones(10, 10, dtype=torch.bool).triu(1)
+        sc = sc.masked_fill(causal | mask, float("-inf"))
+        ctx = (sc.softmax(-1) @ v).transpose(1, 2).reshape(2, 10, 16)
+        ref = torch.nn.functional.linear(ctx, layer.dense_weight.double(), layer.dense_bias.double())
+    valid = ~mask[:, 0, 0, :]
+    assert torch.allclose(out[valid].double(), ref[valid], atol=1e-5)
+
+
+def test_gpt2_position_ids_and_padding_honoured():
+    """Caller-provided position_ids (reference nn/transformer.py:372-409) and a padding
+    attention mask reach the distributed LM head: logits equal HF's for shifted positions."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gpt2
+
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_layer=2, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0)
+    hf = GPT2LMHeadModel(cfg).eval()
+    smp_model = DistributedTransformerLMHead(**gpt2.config_to_kwargs(cfg)).eval()
+    smp_model.load_state_dict(gpt2.hf_to_smp(hf.state_dict()), strict=False)
+    ids = torch.randint(0, 97, (2, 12))
+    pos = torch.arange(5, 17).unsqueeze(0).expand(2, -1)
+    am = torch.ones(2, 12, dtype=torch.long)
+    am[0, 9:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=ids, position_ids=pos, attention_mask=am, use_cache=False).logits
+        out = smp_model((ids, am, None, pos, None))
+        default = smp_model((ids, am, None, None, None))
+    valid = am.bool()
+    assert torch.allclose(out[valid], ref[valid], atol=2e-4, rtol=1e-3), (out[valid] - ref[valid]).abs().max()
+    assert not torch.allclose(default[valid], ref[valid], atol=1e-3)
