@@ -320,6 +320,46 @@ at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> 
   return dx;
 }
 
+// Weight gradient: c (+)= dy^T x with dy [tokens, n], x [tokens, k] (rows may be strided,
+// elements contiguous), c contiguous [n, k] (bf16/f16/f32 -- the bound .grad view or an fp32
+// main grad).  splits = 0: chosen for the device's CU count.
+void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t splits) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_: GPU tensors required");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_: 2-D operands required");
+  TORCH_CHECK(dy.size(0) == x.size(0), "wgrad_: token counts differ");
+  TORCH_CHECK(c.size(0) == dy.size(1) && c.size(1) == x.size(1) && c.is_contiguous(), "wgrad_: c must be [n, k]");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad_: operand rows must be contiguous");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "wgrad_: operand dtypes differ");
+  const int64_t tokens = dy.size(0), n = dy.size(1), k = x.size(1);
+  TORCH_CHECK(n % 8 == 0 && k % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0,
+              "wgrad_: n, k and row strides must be multiples of 8");
+  TORCH_CHECK(n < (1LL << 31) && k < (1LL << 31), "wgrad_: dims too large");
+  if (splits <= 0) {
+    const int cus = at::cuda::getCurrentDeviceProperties()->multiProcessorCount;
+    splits = smpk::wgrad_splits(tokens, static_cast<int>(n), static_cast<int>(k), cus);
+  }
+  // the kernel takes whole 64-token tiles; the remainder rows go through the library GEMM
+  const int64_t main_t = tokens / 64 * 64, tail = tokens - main_t;
+  if (main_t == 0) {
+    if (!accumulate) c.zero_();
+  } else {
+    auto ws = at::empty({splits * n * k}, dy.options().dtype(at::kFloat));
+    check(smpk::wgrad(dt_code(dy), dy.data_ptr(), x.data_ptr(), dt_code(c), c.data_ptr(), ws.data_ptr<float>(), main_t,
+                      static_cast<int>(n), static_cast<int>(k), dy.stride(0), x.stride(0), static_cast<int>(splits),
+                      accumulate ? 1 : 0, stream()),
+          "wgrad");
+  }
+  if (tail > 0) {
+    // < 64 rows: fp32 (no bf16 rounding of the partial product)
+    auto part = at::mm(dy.narrow(0, main_t, tail).to(at::kFloat).t(), x.narrow(0, main_t, tail).to(at::kFloat));
+    c.add_(part.to(c.scalar_type()));
+  }
+}
+
+int64_t wgrad_splits(int64_t tokens, int64_t n, int64_t k, int64_t cus) {
+  return smpk::wgrad_splits(tokens, static_cast<int>(n), static_cast<int>(k), static_cast<int>(cus));
+}
+
 // out=None: fresh [cols] tensor; out given: out += colsum(x) in place (bias .grad views).
 at::Tensor col_sum(at::Tensor x, c10::optional<at::Tensor> out_opt) {
   check_gpu(x, "x");
@@ -610,6 +650,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_gelu_bwd", &bias_gelu_bwd, py::arg("dy"), py::arg("x"), py::arg("bias"), py::arg("exact") = false);
   m.def("transpose_into", &transpose_into);
   m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
+  m.def("wgrad_", &wgrad_, py::arg("c"), py::arg("dy"), py::arg("x"), py::arg("accumulate") = true,
+        py::arg("splits") = 0);
+  m.def("wgrad_splits", &wgrad_splits);
   m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),
         py::arg("dbias_out") = py::none(), py::arg("exact") = false);

@@ -168,6 +168,14 @@ int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row
              void* dlogits, int64_t rows, int64_t vocab, int64_t vocab_start, int64_t ignore_index, hipStream_t s,
              int64_t ld = 0);
 
+// ------------------------------------------------------------ weight gradient (wgrad.hip)
+// C[n][k] (+)= sum_t A[t][n] B[t][k]  (A = dY [tokens, n], B = X [tokens, k], row-major with
+// row strides lda / ldb; C contiguous [n, k] of c_dt).  Split-K over tokens into the fp32
+// workspace ws [splits][n][k], then reduced into C.  n, k, lda, ldb multiples of 8.
+int wgrad_splits(int64_t tokens, int n, int k, int num_cus);
+int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
+          int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s);
+
 // ---------------------------------------------------------------- pack / unpack (pack.hip)
 // Generic strided 4-D copy: dst[i0,i1,i2,i3] = src[...] with element strides (for the
 // split/merge-axis all-to-all and allgatherv packing).

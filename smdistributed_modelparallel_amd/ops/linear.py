@@ -190,8 +190,29 @@ def _wgrad_pick(g, dy2, x2):
     return best
 
 
+# Hand-written split-K MFMA weight-gradient kernel (csrc/kernels/wgrad.hip): reads both
+# token-major operands as they are (LDS transpose reads, no transpose kernels) and accumulates
+# into the gradient with beta = 1.  Opt-in (SMP_WGRAD_KERNEL=1) until it beats hipBLASLt on
+# the bench shapes (tools/wgrad_bench.py).
+_WGRAD_KERNEL = os.environ.get("SMP_WGRAD_KERNEL", "0") == "1"
+_WGRAD_KERNEL_MIN_T = int(os.environ.get("SMP_WGRAD_KERNEL_MIN_TOKENS", "4096"))
+
+
+def _wgrad_native_ok(g, dy2, x2):
+    return (_WGRAD_KERNEL and g.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
+            and g.dtype in (torch.bfloat16, torch.float16, torch.float32) and g.is_contiguous()
+            and dy2.shape[0] >= _WGRAD_KERNEL_MIN_T and dy2.stride(1) == 1 and x2.stride(1) == 1
+            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+
+
 def _wgrad_accumulate(g, dy2, x2):
     """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape."""
+    if _wgrad_native_ok(g, dy2, x2):
+        from ._ext import ext
+
+        ext().wgrad_(g, dy2, x2, True)
+        return
     method = "nn"
     if _WGRAD_TUNE and g.is_cuda and dy2.shape[0] >= _WGRAD_MIN_T and dy2.is_contiguous() and x2.is_contiguous():
         key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype)
