@@ -82,6 +82,27 @@ void lamb_stage1(at::Tensor grad, at::Tensor master, at::Tensor m, at::Tensor v,
         "lamb_stage1");
 }
 
+// Whole-domain LAMB stage 2: per-segment norms then the trust-scaled update, two launches.
+void lamb_chunked(c10::optional<at::Tensor> param, at::Tensor master, at::Tensor update, at::Tensor chunks,
+                  int64_t nseg, double lr, bool use_trust) {
+  check_gpu(master, "master");
+  check_gpu(update, "update");
+  check_gpu(chunks, "chunks");
+  TORCH_CHECK(chunks.scalar_type() == at::kLong && chunks.dim() == 2 && chunks.size(1) == 3, "chunks: [n, 3] int64");
+  TORCH_CHECK(master.scalar_type() == at::kFloat && update.scalar_type() == at::kFloat, "master/update fp32");
+  TORCH_CHECK(update.numel() == master.numel(), "update size");
+  if (param.has_value()) TORCH_CHECK(param->numel() == master.numel() && param->is_contiguous(), "param size");
+  auto norms = at::zeros({nseg, 2}, master.options());
+  const int64_t n = chunks.size(0);
+  check(smpk::lamb_norms_chunked(master.data_ptr<float>(), update.data_ptr<float>(), chunks.data_ptr<int64_t>(), n,
+                                 norms.data_ptr<float>(), stream()),
+        "lamb_norms_chunked");
+  check(smpk::lamb_stage2_chunked(param.has_value() ? dt_code(*param) : 0, param.has_value() ? param->data_ptr() : nullptr,
+                                  master.data_ptr<float>(), update.data_ptr<float>(), chunks.data_ptr<int64_t>(), n,
+                                  norms.data_ptr<float>(), static_cast<float>(lr), use_trust ? 1 : 0, stream()),
+        "lamb_stage2_chunked");
+}
+
 void lamb_stage2(c10::optional<at::Tensor> param, at::Tensor master, at::Tensor update, double lr, at::Tensor pn,
                  at::Tensor un, bool use_trust) {
   check(smpk::lamb_stage2(param.has_value() ? dt_code(*param) : 0, param.has_value() ? param->data_ptr() : nullptr,
@@ -630,6 +651,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_adagrad", &fused_adagrad);
   m.def("lamb_stage1", &lamb_stage1);
   m.def("lamb_stage2", &lamb_stage2);
+  m.def("lamb_chunked_", &lamb_chunked);
   m.def("sumsq_", &sumsq_);
   m.def("nonfinite_", &nonfinite_);
   m.def("axpby_", &axpby_);

@@ -27,6 +27,14 @@ int lamb_stage1(int grad_dt, const void* grad, const float* master, float* exp_a
 // LAMB stage 2: p -= lr * trust * update, trust from per-range norms (device scalars).
 int lamb_stage2(int param_dt, void* param, float* master, const float* update, int64_t n, float lr,
                 const float* p_norm_sq, const float* u_norm_sq, int use_trust, hipStream_t s);
+// LAMB over a domain with per-parameter trust ratios in two launches: chunks [nchunks][3] =
+// (segment, start, end) element ranges (<= 64K elements, each inside one segment = one
+// parameter's piece); norms [nsegments][2] fp32 (zeroed by the caller) receive
+// (|p|^2, |update|^2) per segment; stage 2 applies p -= lr * trust(segment) * update.
+int lamb_norms_chunked(const float* master, const float* update, const int64_t* chunks, int64_t nchunks,
+                       float* norms, hipStream_t s);
+int lamb_stage2_chunked(int param_dt, void* param, float* master, const float* update, const int64_t* chunks,
+                        int64_t nchunks, const float* norms, float lr, int use_trust, hipStream_t s);
 // sum of squares of x (any dtype) * scale^2 accumulated into *out (fp32, atomic).
 int sumsq(int dt, const void* x, int64_t n, float scale, float* out, hipStream_t s);
 // *out = max(*out, 1 if any element non-finite).

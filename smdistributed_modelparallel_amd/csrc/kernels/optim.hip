@@ -239,7 +239,84 @@ __global__ void __launch_bounds__(kThreads) cast_kernel(const S* __restrict__ x,
   }
 }
 
+// ---- LAMB over a whole domain in two launches (no per-parameter host loop) ----------------
+// chunks [nchunks][3] = (segment, start, end): element ranges of <= kLambChunk elements, each
+// inside one parameter's piece; a block per chunk.
+template <typename P>
+__device__ __forceinline__ void lamb_chunk(const int64_t* chunks, int64_t& seg, int64_t& s, int64_t& e) {
+  const int64_t* c = chunks + 3 * static_cast<int64_t>(blockIdx.x);
+  seg = c[0];
+  s = c[1];
+  e = c[2];
+}
+
+__global__ void __launch_bounds__(kThreads) lamb_norms_kernel(const float* __restrict__ master,
+                                                              const float* __restrict__ upd,
+                                                              const int64_t* __restrict__ chunks,
+                                                              float* __restrict__ norms) {
+  __shared__ float smem[16];
+  int64_t seg, s, e;
+  lamb_chunk<float>(chunks, seg, s, e);
+  float a = 0.f, b = 0.f;
+  for (int64_t i = s + threadIdx.x; i < e; i += kThreads) {
+    const float p = master[i], u = upd[i];
+    a += p * p;
+    b += u * u;
+  }
+  a = block_sum(a, smem);
+  __syncthreads();
+  b = block_sum(b, smem);
+  if (threadIdx.x == 0) {
+    atomicAdd(norms + 2 * seg, a);
+    atomicAdd(norms + 2 * seg + 1, b);
+  }
+}
+
+template <typename P, bool HAS_P>
+__global__ void __launch_bounds__(kThreads) lamb2_chunked_kernel(P* __restrict__ param, float* __restrict__ master,
+                                                                 const float* __restrict__ upd,
+                                                                 const int64_t* __restrict__ chunks,
+                                                                 const float* __restrict__ norms, float lr,
+                                                                 int use_trust) {
+  int64_t seg, s, e;
+  lamb_chunk<P>(chunks, seg, s, e);
+  float trust = 1.f;
+  if (use_trust) {
+    const float a = sqrtf(norms[2 * seg]), b = sqrtf(norms[2 * seg + 1]);
+    trust = (a > 0.f && b > 0.f) ? a / b : 1.f;
+  }
+  const float st = lr * trust;
+  for (int64_t i = s + threadIdx.x; i < e; i += kThreads) {
+    const float p = master[i] - st * upd[i];
+    master[i] = p;
+    if (HAS_P) param[i] = from_f32<P>(p);
+  }
+}
+
 }  // namespace
+
+int lamb_norms_chunked(const float* master, const float* update, const int64_t* chunks, int64_t nchunks,
+                       float* norms, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  lamb_norms_kernel<<<static_cast<unsigned>(nchunks), kThreads, 0, s>>>(master, update, chunks, norms);
+  return static_cast<int>(hipGetLastError());
+}
+
+int lamb_stage2_chunked(int param_dt, void* param, float* master, const float* update, const int64_t* chunks,
+                        int64_t nchunks, const float* norms, float lr, int use_trust, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  if (param == nullptr) {
+    lamb2_chunked_kernel<float, false><<<grid, kThreads, 0, s>>>(nullptr, master, update, chunks, norms, lr,
+                                                                 use_trust);
+  } else {
+    SMPK_DISPATCH(param_dt, P, {
+      lamb2_chunked_kernel<P, true><<<grid, kThreads, 0, s>>>(static_cast<P*>(param), master, update, chunks, norms,
+                                                              lr, use_trust);
+    });
+  }
+  return static_cast<int>(hipGetLastError());
+}
 
 int fused_adam(int param_dt, void* param, int grad_dt, const void* grad, float* master, float* exp_avg,
                float* exp_avg_sq, int64_t n, float lr, float beta1, float beta2, float eps, float weight_decay,

@@ -85,6 +85,37 @@ def lamb_stage2_(param_lowp, master, update, lr, p_norm_sq, u_norm_sq, use_trust
         param_lowp.copy_(master)
 
 
+LAMB_CHUNK = 1 << 16
+
+
+def lamb_chunk_table(pieces, device):
+    """pieces: [(start, end)] element ranges (one per parameter piece, relative to the
+    domain) -> int64 [n, 3] (segment, start, end) table of <= LAMB_CHUNK-element chunks."""
+    rows = []
+    for seg, (s, e) in enumerate(pieces):
+        for c in range(s, e, LAMB_CHUNK):
+            rows.append((seg, c, min(c + LAMB_CHUNK, e)))
+    return torch.tensor(rows, dtype=torch.int64, device=device).view(-1, 3)
+
+
+def lamb_segmented_(param_lowp, master, update, chunks, nseg, lr, use_trust=True):
+    """LAMB stage 2 over a whole domain: each segment (parameter piece) gets its own trust
+    ratio |p| / |update|, all in two kernel launches (no per-parameter host loop)."""
+    if master.is_cuda:
+        ext().lamb_chunked_(param_lowp, master, update, chunks, nseg, lr, use_trust)
+        return
+    norms = torch.zeros(nseg, 2)
+    for seg, s, e in chunks.tolist():
+        norms[seg, 0] += master[s:e].pow(2).sum()
+        norms[seg, 1] += update[s:e].pow(2).sum()
+    a, b = norms[:, 0].sqrt(), norms[:, 1].sqrt()
+    trust = torch.where((a > 0) & (b > 0), a / b, torch.ones_like(a)) if use_trust else torch.ones_like(a)
+    for seg, s, e in chunks.tolist():
+        master[s:e].add_(update[s:e], alpha=-lr * float(trust[seg]))
+        if param_lowp is not None:
+            param_lowp[s:e].copy_(master[s:e])
+
+
 def sumsq(x, out=None, scale=1.0):
     """Accumulates sum(x^2) * scale^2 into `out` (fp32 1-element tensor) and returns it."""
     if out is None:

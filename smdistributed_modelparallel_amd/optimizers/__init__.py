@@ -98,17 +98,18 @@ class FusedNovoGrad(torch.optim.Optimizer):
                     continue
                 st = self.state[p]
                 grad = p.grad.float()
-                gn2 = float(mt.sumsq(grad.view(-1)).item())
+                # the per-tensor second moment stays on the device (no host sync per tensor)
+                gn2 = mt.sumsq(grad.view(-1))
                 if not st:
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32)
-                    st["exp_avg_sq"] = 0.0 if g["init_zero"] else gn2
+                    st["exp_avg_sq"] = torch.zeros_like(gn2) if g["init_zero"] else gn2.clone()
                 st["step"] += 1
-                st["exp_avg_sq"] = b2 * st["exp_avg_sq"] + (1 - b2) * gn2
-                denom = st["exp_avg_sq"] ** 0.5 + g["eps"]
-                upd = grad / denom
+                v = st["exp_avg_sq"]
+                v.mul_(b2).add_(gn2, alpha=1 - b2)
+                upd = grad / (v.sqrt() + g["eps"])
                 if g["weight_decay"] != 0:
-                    upd = upd + g["weight_decay"] * p.float()
+                    upd.add_(p.float(), alpha=g["weight_decay"])
                 m = st["exp_avg"]
                 m.mul_(b1).add_(upd, alpha=(1 - b1) if g["grad_averaging"] else 1.0)
                 bc1 = 1 - b1 ** st["step"] if g["bias_correction"] else 1.0

@@ -45,7 +45,7 @@ def _kind_of(opt):
 
 
 class _Domain:
-    __slots__ = ("key", "start", "end", "group_index", "master", "m", "v", "upd", "vparam", "params")
+    __slots__ = ("key", "start", "end", "group_index", "master", "m", "v", "upd", "vparam", "params", "_lamb_chunks")
 
     def __init__(self, key, start, end, group_index, params):
         self.key, self.start, self.end, self.group_index, self.params = key, start, end, group_index, params
@@ -316,18 +316,20 @@ class DistributedOptimizer:
             b1, b2 = g.get("betas", (0.9, 0.999))
             mt.lamb_stage1_(grad, d.master, d.m, d.v, d.upd, float(b1), float(b2), float(g.get("eps", 1e-6)), wd,
                             step, gscale, bias_correction=g.get("bias_correction", True))
-            # per-parameter trust ratios inside the domain
-            flat = state.model.flat_groups[d.key]
-            for p in d.params:
-                o = flat.offsets[p]
-                s, e = max(o, d.start), min(o + p.numel(), d.end)
-                if s >= e:
-                    continue
-                ms, upd = d.master[s - d.start:e - d.start], d.upd[s - d.start:e - d.start]
-                pn = mt.sumsq(ms)
-                un = mt.sumsq(upd)
-                pl = plow[s - d.start:e - d.start] if plow is not None else None
-                mt.lamb_stage2_(pl, ms, upd, lr, pn, un, use_trust=g.get("use_nvlamb", False) or wd != 0.0)
+            # per-parameter trust ratios inside the domain: one chunk table per domain (layout
+            # is fixed), two launches for all of its parameters
+            table = getattr(d, "_lamb_chunks", None)
+            if table is None:
+                flat = state.model.flat_groups[d.key]
+                pieces = []
+                for p in d.params:
+                    o = flat.offsets[p]
+                    s, e = max(o, d.start), min(o + p.numel(), d.end)
+                    if s < e:
+                        pieces.append((s - d.start, e - d.start))
+                table = d._lamb_chunks = (mt.lamb_chunk_table(pieces, d.master.device), len(pieces))
+            mt.lamb_segmented_(plow, d.master, d.upd, table[0], table[1], lr,
+                               use_trust=g.get("use_nvlamb", False) or wd != 0.0)
 
     def _generic_step(self, gscale, lowp):
         for d in self.domains:

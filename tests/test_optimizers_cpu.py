@@ -1,0 +1,21 @@
+"""Fused optimizers on CPU: DistributedOptimizer(FusedLAMB) updates every domain with
+per-parameter trust ratios in two segmented launches (reference apex FusedLAMB semantics),
+FusedNovoGrad keeps its per-tensor second moments on the device (no host sync)."""
+import torch
+
+from smdistributed_modelparallel_amd.ops import multi_tensor as mt
+from tests.dist_utils import run_workers
+
+
+def test_lamb_and_novograd_match_reference():
+    outs = run_workers("opt_cpu", 1, [], timeout=120)
+    assert "OK lamb" in outs[0] and "OK novograd" in outs[0]
+
+
+def test_lamb_chunk_table_covers_pieces(monkeypatch):
+    monkeypatch.setattr(mt, "LAMB_CHUNK", 5)
+    t = mt.lamb_chunk_table([(0, 12), (12, 13), (20, 31)], "cpu")
+    rows = [tuple(r) for r in t.tolist()]
+    assert rows[:3] == [(0, 0, 5), (0, 5, 10), (0, 10, 12)] and rows[3] == (1, 12, 13)
+    assert sum(e - s for _, s, e in rows) == 12 + 1 + 11
+    assert all(e - s <= 5 for _, s, e in rows)
