@@ -122,6 +122,11 @@ def model_load_state_dict(model, sd, strict=True, translate_function=None, same_
     sd = dict(sd)
     if translate_function is not None:
         sd = translate_function(sd)
+    from .checkpoint_compat import from_reference_state_dict, is_reference_state_dict
+
+    if is_reference_state_dict(sd):
+        # written by the reference library's smp.nn modules (separate query/key/value Linears)
+        sd = from_reference_state_dict(sd)
     is_partial = sd.pop("_smp_is_partial", False)
     info = sd.pop("_smp_load_info", None)
     params = dict(model.local_named_parameters())

@@ -78,3 +78,32 @@ def test_partial_resume_after_bucket_cap_change_sharded_optimizer(tmp_path):
     _phase("save", 2, ckpt, 1, 1, True, extra)
     with pytest.raises(AssertionError, match="sharding layout changed"):
         _phase("load", 2, ckpt, 1, 1, True, extra)
+
+
+def test_reference_layout_state_dict_round_trip():
+    """Checkpoints of the reference's smp.nn modules (separate query/key/value/dense Linears,
+    `smp/torch/nn/transformer.py:1251-1320`) convert to the fused layout and back, for
+    self- and cross-attention layers."""
+    import torch
+
+    from smdistributed_modelparallel_amd.nn import DistributedTransformerLMHead
+    from smdistributed_modelparallel_amd.torch.checkpoint_compat import (from_reference_state_dict,
+                                                                         is_reference_state_dict,
+                                                                         to_reference_state_dict)
+
+    torch.manual_seed(0)
+    m = DistributedTransformerLMHead(num_layers=2, num_attention_heads=2, attention_head_size=8, hidden_size=16,
+                                     intermediate_size=32, vocab_size=50, num_positions=16, pre_layernorm=True,
+                                     post_layernorm=False, add_cross_attention=True, add_lm_head=True)
+    ours = m.state_dict()
+    ref = to_reference_state_dict(ours)
+    assert is_reference_state_dict(ref) and not is_reference_state_dict(ours)
+    assert "transformer.seq_layers.0.attention.query.weight" in ref
+    assert "transformer.seq_layers.1.cross_attention.value.bias" in ref
+    assert "transformer.seq_layers.0.output.dense2.weight" in ref
+    assert "transformer.seq_layers.0.attention.pre_layernorm.weight" in ref
+    assert not any("qkv" in k or "_module" in k or "dense1_" in k for k in ref)
+    back = from_reference_state_dict(ref)
+    assert set(back) == set(ours)
+    for k, v in ours.items():
+        assert torch.equal(back[k], v), k
