@@ -41,6 +41,9 @@ def choose_mode(core, device, backend):
     mode = os.environ.get("SMP_P2P", "").lower()
     if mode in ("ipc", "rccl", "host"):
         return mode
+    if os.environ.get("SMP_DISABLE_D2D", "0") not in ("0", "", "false", "False"):
+        # reference: SMP_DISABLE_D2D routes pipeline tensors through the host path
+        return "host"
     same_node = all(core.is_in_same_instance(r) for r in core.get_pp_group())
     if same_node:
         return "ipc"
