@@ -471,3 +471,18 @@ def test_lamb_segmented_kernel_matches_cpu():
     for s, e in pieces:
         covered[s:e] = True
     torch.testing.assert_close(gp.float().cpu()[covered], ref_m[covered], rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("rows,cols", [(4097, 6400), (3001, 2056), (65, 40)])
+def test_gelu_flat_stream_matches_column_walker(C, rows, cols, monkeypatch):
+    """Forward bias-GeLU in memory order (default, SMP_GELU_FLAT) against the column walker:
+    same per-element math, bitwise-equal output."""
+    torch.manual_seed(11)
+    x = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(cols, device="cuda", dtype=torch.bfloat16)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("SMP_GELU_FLAT", mode)
+        monkeypatch.setenv("SMP_GELU_ROWS", "0")
+        out[mode] = (C.bias_gelu_fwd(x, b, False), C.bias_gelu_fwd(x, b, True))
+    assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
