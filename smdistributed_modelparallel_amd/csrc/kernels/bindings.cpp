@@ -181,11 +181,13 @@ at::Tensor dropout_bwd(at::Tensor dy, double p, int64_t seed, int64_t offset) {
 
 std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> residual,
                                       c10::optional<at::Tensor> w, c10::optional<at::Tensor> b, double eps,
-                                      double dropout_p, int64_t seed, int64_t offset) {
+                                      double dropout_p, int64_t seed, int64_t offset, bool mixed_output) {
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / cols;
-  auto y = at::empty_like(x);
+  // mixed_output: y in the affine parameters' dtype (MixedFusedLayerNorm)
+  TORCH_CHECK(!mixed_output || w.has_value(), "mixed-dtype LayerNorm needs a weight");
+  auto y = mixed_output ? at::empty(x.sizes(), x.options().dtype(w->scalar_type())) : at::empty_like(x);
   auto opts = x.options().dtype(at::kFloat);
   auto mean = at::empty({rows}, opts);
   auto rstd = at::empty({rows}, opts);
@@ -200,7 +202,8 @@ std::vector<at::Tensor> layernorm_fwd(at::Tensor x, c10::optional<at::Tensor> re
   if (b.has_value()) TORCH_CHECK(b->numel() == cols && b->is_contiguous() && dt_code(*b) == wdt, "bias mismatch");
   check(smpk::layernorm_fwd(dt_code(x), x.data_ptr(), opt_ptr(residual), residual.has_value() ? xo.data_ptr() : nullptr,
                             wdt, opt_ptr(w), opt_ptr(b), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                            rows, cols, eps, stream(), dropout_args(residual.has_value() ? dropout_p : 0.0, seed, offset)),
+                            rows, cols, eps, stream(), dropout_args(residual.has_value() ? dropout_p : 0.0, seed, offset),
+                            mixed_output ? wdt : -1),
         "layernorm_fwd");
   if (residual.has_value()) return {y, mean, rstd, xo};
   return {y, mean, rstd};
@@ -657,7 +660,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("axpby_", &axpby_);
   m.def("cast_copy_", &cast_copy_);
   m.def("layernorm_fwd", &layernorm_fwd, py::arg("x"), py::arg("residual"), py::arg("w"), py::arg("b"),
-        py::arg("eps"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+        py::arg("eps"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0,
+        py::arg("mixed_output") = false);
   m.def("dropout_add", &dropout_add, py::arg("x"), py::arg("residual"), py::arg("p"), py::arg("seed"),
         py::arg("offset"));
   m.def("dropout_bwd", &dropout_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"));

@@ -61,7 +61,9 @@ int dropout_bwd(int dt, const void* dy, void* dx, int64_t n, const DropoutArgs& 
 // residual != null: x_out = residual + dropout(x) is written and normalised (pre-LN block)
 int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
                   void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s,
-                  const DropoutArgs& drop = DropoutArgs());
+                  const DropoutArgs& drop = DropoutArgs(), int out_dt = -1);
+// out_dt: -1 = y in the input dtype; the parameter dtype = mixed-dtype LayerNorm (K10, apex
+// MixedFusedLayerNorm: output takes the affine parameters' dtype).
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
                   const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
                   int part_rows, const void* dres, hipStream_t s,

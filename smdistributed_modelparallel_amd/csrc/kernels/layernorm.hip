@@ -40,10 +40,25 @@ __device__ __forceinline__ void load_wn(const W* p, float (&o)[N]) {
   }
 }
 
-template <typename T, typename W, int VPT>
+// TO: output dtype -- T, or W for the mixed-dtype LayerNorm (apex MixedFusedLayerNorm, K10:
+// the output takes the parameters' dtype, computed from the fp32 statistics directly).
+template <typename TO, typename T, int N>
+__device__ __forceinline__ void store_out(TO* p, const float (&o)[N]) {
+  if constexpr (sizeof(TO) * N == 16) {
+    Vec16<TO> v;
+#pragma unroll
+    for (int j = 0; j < N; ++j) v.v[j] = from_f32<TO>(o[j]);
+    store16(p, v);
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) p[j] = from_f32<TO>(o[j]);
+  }
+}
+
+template <typename T, typename W, int VPT, typename TO = T>
 __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const T* __restrict__ res,
                                                   T* __restrict__ x_out, const W* __restrict__ w,
-                                                  const W* __restrict__ b, T* __restrict__ y,
+                                                  const W* __restrict__ b, TO* __restrict__ y,
                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                   int64_t rows, int cols, float eps, DropoutArgs drop) {
   constexpr int N = Vec16<T>::N;
@@ -128,19 +143,19 @@ __global__ void __launch_bounds__(256) ln_fwd_reg(const T* __restrict__ x, const
 #pragma unroll
         for (int j = 0; j < N; ++j) bb[j] = 0.f;
       }
-      Vec16<T> o;
+      float o[N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>((v[k][j] - mean) * rstd * g[j] + bb[j]);
-      store16(y + row * cols + c, o);
+      for (int j = 0; j < N; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + bb[j];
+      store_out<TO, T, N>(y + row * cols + c, o);
     }
   }
 }
 
 // Generic fallback: one block per row, streaming (any width, any alignment).
-template <typename T, typename W>
+template <typename T, typename W, typename TO = T>
 __global__ void __launch_bounds__(256) ln_fwd_stream(const T* __restrict__ x, const T* __restrict__ res,
                                                      T* __restrict__ x_out, const W* __restrict__ w,
-                                                     const W* __restrict__ b, T* __restrict__ y,
+                                                     const W* __restrict__ b, TO* __restrict__ y,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int64_t rows, int cols, float eps, DropoutArgs drop) {
   __shared__ float smem[16];
@@ -173,7 +188,7 @@ __global__ void __launch_bounds__(256) ln_fwd_stream(const T* __restrict__ x, co
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
     float g = w ? to_f32(w[c]) : 1.f;
     float bb = b ? to_f32(b[c]) : 0.f;
-    y[row * cols + c] = from_f32<T>((to_f32(src[c]) - mean) * rstd * g + bb);
+    y[row * cols + c] = from_f32<TO>((to_f32(src[c]) - mean) * rstd * g + bb);
   }
 }
 
@@ -481,35 +496,50 @@ bool vec_ok(const void* p) {
 
 }  // namespace
 
+namespace {
+template <typename T, typename W, typename TO>
+void launch_ln_fwd(const void* x, const void* residual, void* x_out, const void* w, const void* b, void* y,
+                   float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s,
+                   const DropoutArgs& drop) {
+  constexpr int N = Vec16<T>::N;
+  const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<TO>(y) && vec_ok<W>(w) && vec_ok<W>(b) &&
+                       (residual == nullptr || (vec_ok<T>(residual) && vec_ok<T>(x_out)));
+  const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
+  const int grid = static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock);
+  const T* xx = static_cast<const T*>(x);
+  const T* rr = static_cast<const T*>(residual);
+  T* xo = static_cast<T*>(x_out);
+  const W* ww = static_cast<const W*>(w);
+  const W* bb = static_cast<const W*>(b);
+  TO* yy = static_cast<TO*>(y);
+  const int c = static_cast<int>(cols);
+  if (aligned && vpt <= 1) {
+    ln_fwd_reg<T, W, 1, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && vpt <= 2) {
+    ln_fwd_reg<T, W, 2, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && vpt <= 4) {
+    ln_fwd_reg<T, W, 4, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && vpt <= 8) {
+    ln_fwd_reg<T, W, 8, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else {
+    ln_fwd_stream<T, W, TO><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps,
+                                                                   drop);
+  }
+}
+}  // namespace
+
 int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int wdt, const void* w, const void* b,
                   void* y, float* mean, float* rstd, int64_t rows, int64_t cols, float eps, hipStream_t s,
-                  const DropoutArgs& drop) {
+                  const DropoutArgs& drop, int out_dt) {
   if (rows <= 0) return 0;
+  if (out_dt >= 0 && out_dt != dt && out_dt != wdt) return -3;  // output: input or parameter dtype
+  const bool mixed = out_dt >= 0 && out_dt != dt;
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
-      constexpr int N = Vec16<T>::N;
-      const bool aligned = (cols % N == 0) && vec_ok<T>(x) && vec_ok<T>(y) && vec_ok<W>(w) && vec_ok<W>(b) &&
-                           (residual == nullptr || (vec_ok<T>(residual) && vec_ok<T>(x_out)));
-      const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
-      const int grid = static_cast<int>((rows + kRowsPerBlock - 1) / kRowsPerBlock);
-      const T* xx = static_cast<const T*>(x);
-      const T* rr = static_cast<const T*>(residual);
-      T* xo = static_cast<T*>(x_out);
-      const W* ww = static_cast<const W*>(w);
-      const W* bb = static_cast<const W*>(b);
-      T* yy = static_cast<T*>(y);
-      const int c = static_cast<int>(cols);
-      if (aligned && vpt <= 1) {
-        ln_fwd_reg<T, W, 1><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
-      } else if (aligned && vpt <= 2) {
-        ln_fwd_reg<T, W, 2><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
-      } else if (aligned && vpt <= 4) {
-        ln_fwd_reg<T, W, 4><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
-      } else if (aligned && vpt <= 8) {
-        ln_fwd_reg<T, W, 8><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
-      } else {
-        ln_fwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
-      }
+      if (mixed)
+        launch_ln_fwd<T, W, W>(x, residual, x_out, w, b, y, mean, rstd, rows, cols, eps, s, drop);
+      else
+        launch_ln_fwd<T, W, T>(x, residual, x_out, w, b, y, mean, rstd, rows, cols, eps, s, drop);
     });
   });
   return static_cast<int>(hipGetLastError());

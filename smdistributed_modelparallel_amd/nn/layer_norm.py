@@ -63,11 +63,17 @@ class FusedLayerNorm(nn.Module):
 
 
 class MixedFusedLayerNorm(FusedLayerNorm):
-    """fp32 input with low-precision affine params; output in the param dtype."""
+    """apex ``MixedFusedLayerNorm`` (reference `smp/torch/apex/normalization/
+    fused_layer_norm.py:198-218`, K10): input of any dtype, output in the parameters' dtype,
+    written directly by the LayerNorm kernel."""
 
     def forward(self, x):
-        y = super().forward(x)
-        return y.to(self.weight.dtype) if self.weight is not None else y
+        if self.weight is None or len(self.normalized_shape) != 1:
+            y = super().forward(x)
+            return y.to(self.weight.dtype) if self.weight is not None else y
+        from ..ops.layernorm import mixed_layer_norm
+
+        return mixed_layer_norm(x, self.weight, self.bias, self.eps)
 
 
 class _DistLNStats(torch.autograd.Function):

@@ -100,6 +100,35 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         return dxin, dx, dw, db, None, None
 
 
+class _MixedLayerNorm(torch.autograd.Function):
+    """apex MixedFusedLayerNorm (K10): output in the parameters' dtype, written by the kernel
+    from the fp32 statistics (no input-dtype rounding before the cast)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x2 = x.contiguous()
+        y, mean, rstd = ext().layernorm_fwd(x2, None, weight, bias, eps, 0.0, 0, 0, True)
+        ctx.save_for_backward(x2, weight, mean, rstd)
+        ctx.bias = bias
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        need_w, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        dx, dw, db = _ln_bwd(dy.to(x.dtype).contiguous(), x, w, ctx.bias, mean, rstd, need_w, need_b, None)
+        return dx.view(dy.shape), dw, db, None
+
+
+def mixed_layer_norm(x, weight, bias, eps=1e-5):
+    """LayerNorm whose output takes the affine parameters' dtype (input any dtype)."""
+    if x.is_cuda and weight is not None and bias is not None:
+        return _MixedLayerNorm.apply(x, weight, bias, eps)
+    y = torch.nn.functional.layer_norm(x.to(weight.dtype) if weight is not None else x, (x.shape[-1],), weight, bias,
+                                       eps)
+    return y.to(weight.dtype) if weight is not None else y
+
+
 def layer_norm(x, weight, bias, eps=1e-5):
     if x.is_cuda:
         return _FusedLayerNorm.apply(x, weight, bias, eps)

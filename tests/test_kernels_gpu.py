@@ -486,3 +486,31 @@ def test_gelu_flat_stream_matches_column_walker(C, rows, cols, monkeypatch):
         monkeypatch.setenv("SMP_GELU_ROWS", "0")
         out[mode] = (C.bias_gelu_fwd(x, b, False), C.bias_gelu_fwd(x, b, True))
     assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
+
+
+@pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.float32),
+                                     (torch.float16, torch.float32)])
+@pytest.mark.parametrize("cols", [1600, 1001])
+def test_mixed_fused_layer_norm(xdt, wdt, cols):
+    """MixedFusedLayerNorm (K10): output in the parameters' dtype straight from the kernel;
+    forward and backward against fp32 torch."""
+    from smdistributed_modelparallel_amd.nn.layer_norm import MixedFusedLayerNorm
+
+    torch.manual_seed(4)
+    ln = MixedFusedLayerNorm(cols).cuda().to(wdt)
+    with torch.no_grad():
+        ln.weight.normal_(1.0, 0.1)
+        ln.bias.normal_(0.0, 0.1)
+    x = torch.randn(257, cols, device="cuda", dtype=xdt, requires_grad=True)
+    y = ln(x)
+    assert y.dtype == wdt
+    xr = x.detach().float().requires_grad_()
+    wr, br = ln.weight.detach().float().requires_grad_(), ln.bias.detach().float().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (cols,), wr, br, ln.eps)
+    tol = 2e-2 if torch.bfloat16 in (xdt, wdt) else 5e-3
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(wdt))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=tol * 4, rtol=tol * 4)
+    torch.testing.assert_close(ln.weight.grad.float(), wr.grad, atol=tol * 20, rtol=tol * 4)
