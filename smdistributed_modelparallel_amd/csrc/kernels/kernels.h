@@ -185,7 +185,6 @@ int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row
 int wgrad_splits(int64_t tokens, int n, int k, int num_cus);
 int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
           int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s);
-
 // ---------------------------------------------------------------- pack / unpack (pack.hip)
 // Generic strided 4-D copy: dst[i0,i1,i2,i3] = src[...] with element strides (for the
 // split/merge-axis all-to-all and allgatherv packing).

@@ -28,11 +28,14 @@
 //  * workgroups are dealt to XCDs in contiguous runs of (split, n-tile) so that the
 //    workgroups sharing an A strip share one XCD's L2.
 //
-// Status (MI355X, GPT-2 XL shapes, tools/wgrad_bench.py, profiles/r2/wgrad_kernel.md): 640-775
-// TFLOP/s against hipBLASLt's 700-1020 -- one wave per SIMD with a one-tile-deep register
-// pipeline does not hide the operand latency (a 2-deep ring does not fit beside the 256
-// accumulator registers).  Opt-in (SMP_WGRAD_KERNEL=1) until a glds-fed multi-phase
-// pipeline (LDS-DMA, counted vmcnt across raw barriers) replaces the staging.
+// Status (MI355X, GPT-2 XL shapes, tools/wgrad_bench.py, profiles/r2/wgrad_kernel.md): the
+// register-staged version ran 630-775 TFLOP/s; the LDS-DMA version (wgrad_glds_kernel:
+// global_load_lds from inline asm so hipcc does not drain the prefetch before every ds_read,
+// two 64 KB stages, one barrier per tile, bijective XCD mapping) 750-900 TFLOP/s against
+// hipBLASLt's 700-1030.  ops/linear.py times both per shape on first use and keeps the faster
+// (in the GPT-2 XL step: the kernel wins the 1600 x 1600 weight gradient).  A stream-K
+// schedule (one persistent workgroup per CU) was slower: workgroups sharing a tile read
+// disjoint token ranges, so concurrent workgroups no longer share A / B strips in L2.
 #include "common.h"
 #include "kernels.h"
 
@@ -108,14 +111,15 @@ __device__ __forceinline__ typename WMF<T>::e8 ld_tr(const uint16_t* tile, int o
 // Workgroup -> (split, n tile, k tile), XCD-aware: the hardware deals workgroups to the 8
 // XCDs round-robin; logical tile L = (id % 8) * per + id / 8 gives XCD x a contiguous run.
 __device__ __forceinline__ void wg_map(int tiles_n, int tiles_k, int& s, int& tn, int& tk) {
+  // bijective for any grid size: XCD x owns logical tiles [start(x), start(x) + q (+1))
   const int total = gridDim.x;
   const int id = blockIdx.x;
-  int L = id;
-  if (total % 8 == 0) L = (id % 8) * (total / 8) + id / 8;
+  const int q = total / 8, rem = total % 8, xcd = id % 8;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + id / 8;
   tk = L % tiles_k;
-  const int r = L / tiles_k;
-  tn = r % tiles_n;
-  s = r / tiles_n;
+  const int rest = L / tiles_k;
+  tn = rest % tiles_n;
+  s = rest / tiles_n;
 }
 
 template <typename T>
@@ -221,6 +225,130 @@ __global__ __launch_bounds__(kT, 1) void wgrad_kernel(const uint16_t* __restrict
   }
 }
 
+// ---------------------------------------------------------------- LDS-DMA variant
+// Same tiling and MFMA work; operand tiles arrive by global_load_lds (16 B per lane, no VGPR
+// staging, no ds_write pass) into TWO 64 KB stage buffers: tile t+1 is in flight while tile
+// t is multiplied, one barrier per tile.  The LDS image is lane-linear per wave-instruction
+// (2 rows of 512 B), so the XOR swizzle moves to the SOURCE address: physical chunk pc of row
+// r is filled from logical chunk pc ^ g(r).
+//
+// The DMA is issued from inline asm: with the builtin, hipcc (ROCm 7.2) cannot tell the
+// buffer being filled from the one being read and drains vmcnt(0) before the first ds_read
+// of every tile -- the prefetch would never overlap the MFMAs.  The loop waits for its own
+// DMA explicitly (vmcnt(0) before the end-of-tile barrier).
+__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint16_t*)lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
+// one operand tile (TK rows x 256 cols) -> LDS; this wave issues rows 16 w + 2 i + (lane >> 5)
+__device__ __forceinline__ void stage_glds(uint16_t* lds, const uint16_t* src, int64_t ld, int vc, int wave,
+                                           int lane) {
+  const int pc = lane & 31, half = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 16 * wave + 2 * i + half;
+    const int g = ((r & 3) << 2) | ((r >> 2) & 3);
+    int c = pc ^ g;
+    c = c < vc ? c : vc - 1;
+    glds16(src + static_cast<int64_t>(r) * ld + c * 8, lds + (16 * wave + 2 * i) * RW);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kT, 1) void wgrad_glds_kernel(const uint16_t* __restrict__ A,
+                                                             const uint16_t* __restrict__ B, float* __restrict__ ws,
+                                                             int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
+                                                             int64_t t_split) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // 2 stages x (A, B) x 32 KB
+  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
+  int split, tn, tk;
+  wg_map(tiles_n, tiles_k, split, tn, tk);
+  const int n0 = tn * TM, k0 = tk * TN;
+  const int64_t t_begin = split * t_split;
+  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int hh = lane >> 5;
+  int aLo[4], aHi[4], bLo[4], bHi[4];
+  {
+    const int q = (lane & 15) >> 2, pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ca = wm * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
+      const int cb = wn * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
+      aLo[i] = swz(4 * hh + q, ca >> 3) + (ca & 7);
+      aHi[i] = swz(4 * hh + 8 + q, ca >> 3) + (ca & 7);
+      bLo[i] = swz(4 * hh + q, cb >> 3) + (cb & 7);
+      bHi[i] = swz(4 * hh + 8 + q, cb >> 3) + (cb & 7);
+    }
+  }
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0.f};
+  const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
+  const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
+  const int64_t ntiles = (t_end - t_begin) / TK;
+  const uint16_t* pa = A + t_begin * lda + n0;
+  const uint16_t* pb = B + t_begin * ldb + k0;
+  constexpr int STAGE = 2 * TK * RW;  // elements per stage (A then B)
+  if (ntiles > 0) {
+    stage_glds(smem, pa, lda, vcA, wave, lane);
+    stage_glds(smem + TK * RW, pb, ldb, vcB, wave, lane);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // publishes the first tile
+  for (int64_t t = 0; t < ntiles; ++t) {
+    uint16_t* cur = smem + (t & 1) * STAGE;
+    if (t + 1 < ntiles) {
+      uint16_t* nxt = smem + ((t + 1) & 1) * STAGE;
+      stage_glds(nxt, pa + (t + 1) * TK * lda, lda, vcA, wave, lane);
+      stage_glds(nxt + TK * RW, pb + (t + 1) * TK * ldb, ldb, vcB, wave, lane);
+    }
+    const uint16_t* sA = cur;
+    const uint16_t* sB = cur + TK * RW;
+#pragma unroll
+    for (int s = 0; s < TK / 16; ++s) {
+      typename WMF<T>::e8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
+        fb[i] = ld_tr<T>(sB, bLo[i] + s * 16 * RW, bHi[i] + s * 16 * RW);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
+    __syncthreads();  // ... everyone's, and every wave is done reading tile t
+  }
+  float* out = ws + static_cast<int64_t>(split) * N * K;
+  const int col_l = lane & 31;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + wn * 128 + 32 * j + col_l;
+    if (k >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nb = n0 + wm * 128 + 32 * i + 4 * hh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = nb + (r & 3) + 8 * (r >> 2);
+        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+inline bool wgrad_use_glds() {
+  const char* e = getenv("SMP_WGRAD_GLDS");
+  return e == nullptr || e[0] != '0';
+}
+
 // C (+)= sum over splits of ws, 4 elements per thread
 template <typename TO>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, TO* __restrict__ c,
@@ -275,7 +403,25 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   int64_t t_split = (tokens + splits - 1) / splits;
   t_split = (t_split + TK - 1) / TK * TK;
   const int grid = tiles * splits;
-  if (dt == BF16)
+  if (wgrad_use_glds()) {
+    constexpr size_t lds = 2 * 2 * TK * RW * sizeof(uint16_t);  // 128 KB
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<bf16>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<f16>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      attr_set = true;
+    }
+    if (dt == BF16)
+      wgrad_glds_kernel<bf16><<<grid, kT, lds, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
+                                                    tokens, n, k, lda, ldb, t_split);
+    else if (dt == F16)
+      wgrad_glds_kernel<f16><<<grid, kT, lds, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
+                                                   tokens, n, k, lda, ldb, t_split);
+    else
+      return -2;
+  } else if (dt == BF16)
     wgrad_kernel<bf16><<<grid, kT, 0, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
                                             tokens, n, k, lda, ldb, t_split);
   else if (dt == F16)

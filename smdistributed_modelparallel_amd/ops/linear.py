@@ -191,24 +191,60 @@ def _wgrad_pick(g, dy2, x2):
 
 
 # Hand-written split-K MFMA weight-gradient kernel (csrc/kernels/wgrad.hip): reads both
-# token-major operands as they are (LDS transpose reads, no transpose kernels) and accumulates
-# into the gradient with beta = 1.  Opt-in (SMP_WGRAD_KERNEL=1) until it beats hipBLASLt on
-# the bench shapes (tools/wgrad_bench.py).
-_WGRAD_KERNEL = os.environ.get("SMP_WGRAD_KERNEL", "0") == "1"
+# token-major operands as they are (LDS-DMA staging, LDS transpose reads, no transpose
+# kernels) and accumulates into the gradient with beta = 1.  It beats hipBLASLt on some
+# shapes and loses on others (profiles/r2/wgrad_kernel.md), so the first time a shape occurs
+# inside a step both are timed on the real operands (gradient restored after each trial) and
+# the faster one is kept for the process.  SMP_WGRAD_KERNEL=0 never uses the kernel,
+# =1 always does.
+_WGRAD_KERNEL = os.environ.get("SMP_WGRAD_KERNEL", "auto")
 _WGRAD_KERNEL_MIN_T = int(os.environ.get("SMP_WGRAD_KERNEL_MIN_TOKENS", "4096"))
+_WGRAD_KERNEL_CHOICE = {}
 
 
 def _wgrad_native_ok(g, dy2, x2):
-    return (_WGRAD_KERNEL and g.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16) and x2.dtype == dy2.dtype
-            and g.dtype in (torch.bfloat16, torch.float16, torch.float32) and g.is_contiguous()
-            and dy2.shape[0] >= _WGRAD_KERNEL_MIN_T and dy2.stride(1) == 1 and x2.stride(1) == 1
-            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(0) % 8 == 0 and x2.stride(0) % 8 == 0
-            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+    return (_WGRAD_KERNEL != "0" and g.is_cuda and dy2.dtype in (torch.bfloat16, torch.float16)
+            and x2.dtype == dy2.dtype and g.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and g.is_contiguous() and dy2.shape[0] >= _WGRAD_KERNEL_MIN_T and dy2.stride(1) == 1
+            and x2.stride(1) == 1 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(0) % 8 == 0
+            and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
+
+
+def _wgrad_kernel_wins(g, dy2, x2):
+    """Time the MFMA kernel against the library GEMM once per (T, N, K, dtypes)."""
+    if _WGRAD_KERNEL == "1" or g.dtype != dy2.dtype:  # (fp32 accumulators: no library equivalent)
+        return True
+    key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype, g.dtype)
+    hit = _WGRAD_KERNEL_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    from ._ext import ext
+
+    C = ext()
+    saved = g.clone()
+    times = {}
+    for name, fn in (("kernel", lambda: C.wgrad_(g, dy2, x2, True)), ("library", lambda: g.addmm_(dy2.t(), x2))):
+        fn()  # warm-up (library solution selection, allocator)
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(3):
+            fn()
+        end.record()
+        end.synchronize()
+        times[name] = start.elapsed_time(end)
+        g.copy_(saved)
+    del saved
+    win = times["kernel"] < times["library"]
+    _WGRAD_KERNEL_CHOICE[key] = win
+    if os.environ.get("SMP_WGRAD_LOG") == "1":
+        print(f"wgrad T={key[0]} N={key[1]} K={key[2]}: kernel {times['kernel'] / 3:.3f} ms, "
+              f"library {times['library'] / 3:.3f} ms -> {'kernel' if win else 'library'}", flush=True)
+    return win
 
 
 def _wgrad_accumulate(g, dy2, x2):
     """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape."""
-    if _wgrad_native_ok(g, dy2, x2):
+    if _wgrad_native_ok(g, dy2, x2) and _wgrad_kernel_wins(g, dy2, x2):
         from ._ext import ext
 
         ext().wgrad_(g, dy2, x2, True)

@@ -26,7 +26,7 @@ def test_wgrad_methods_match_fp32(method, shape):
 
 def test_wgrad_autotune_picks_and_preserves_gradient(monkeypatch):
     monkeypatch.setattr(L, "_WGRAD_TUNE", True)  # opt-in (SMP_WGRAD_AUTOTUNE=1)
-    monkeypatch.setattr(L, "_WGRAD_KERNEL", False)  # the hipBLASLt-side algorithm choice
+    monkeypatch.setattr(L, "_WGRAD_KERNEL", "0")  # the hipBLASLt-side algorithm choice
     T, N, K = 16384, 512, 256
     g0 = torch.Generator(device="cuda").manual_seed(1)
     dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
@@ -78,8 +78,10 @@ def test_wgrad_kernel_strided_rows_and_f16():
     torch.testing.assert_close(g, dy.float().t() @ x.float(), rtol=1e-4, atol=1e-2)
 
 
-def test_linear_uses_wgrad_kernel_for_bound_grads():
-    """ops.linear: a weight whose .grad is bound (flat buffer) accumulates through the kernel."""
+def test_linear_uses_wgrad_kernel_for_bound_grads(monkeypatch):
+    """ops.linear: a weight whose .grad is bound (flat buffer) accumulates through the kernel
+    (forced) and through the timed per-shape choice (auto): one accumulation either way."""
+    monkeypatch.setattr(L, "_WGRAD_KERNEL", "1")
     T, N, K = 8192, 512, 384
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     w.grad = torch.zeros_like(w)
@@ -90,4 +92,19 @@ def test_linear_uses_wgrad_kernel_for_bound_grads():
     y.backward(dy)
     ref = dy.float().t() @ x.detach().float()
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+
+
+def test_wgrad_auto_choice_accumulates_once(monkeypatch):
+    monkeypatch.setattr(L, "_WGRAD_KERNEL", "auto")
+    T, N, K = 8192, 1024, 512
+    g0 = torch.Generator(device="cuda").manual_seed(5)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    g = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    ref = g.float() + dy.float().t() @ x.float()
+    L._WGRAD_KERNEL_CHOICE.clear()
+    L._wgrad_accumulate(g, dy, x)
+    assert len(L._WGRAD_KERNEL_CHOICE) == 1
+    err = (g.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err

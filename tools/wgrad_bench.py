@@ -42,7 +42,7 @@ for n, k in ((4800, 1600), (1600, 1600), (6400, 1600), (1600, 6400), (50304, 160
     fl = 2.0 * T * n * k
     r = {"splits": C.wgrad_splits(T, n, k, cus)}
     r["hipblaslt_ms"] = timeit(lambda: g.addmm_(dy.t(), x))
-    r["kernel_ms"] = timeit(lambda: C.wgrad_(g, dy, x, True))
+    r["kernel_ms"] = timeit(lambda: C.wgrad_(g, dy, x, True))  # stream-K (default)
     for sp in (1, 2, 4):
         r[f"kernel_s{sp}_ms"] = timeit(lambda: C.wgrad_(g, dy, x, True, sp))
     r["hipblaslt_tflops"] = fl / r["hipblaslt_ms"] / 1e9
