@@ -110,27 +110,36 @@ __device__ __forceinline__ typename WMF<T>::e8 ld_tr(const uint16_t* tile, int o
 
 // Workgroup -> (split, n tile, k tile), XCD-aware: the hardware deals workgroups to the 8
 // XCDs round-robin; logical tile L = (id % 8) * per + id / 8 gives XCD x a contiguous run.
-__device__ __forceinline__ void wg_map(int tiles_n, int tiles_k, int& s, int& tn, int& tk) {
+// Within a split, L walks `group` n-tiles fastest and then the k-tiles, so the 32 workgroups
+// an XCD runs at once cover a compact group x (32 / group) block of output tiles and share
+// their A and B strips in that XCD's L2 (group 1: a row of k-tiles sharing one A strip).
+__device__ __forceinline__ void wg_map(int tiles_n, int tiles_k, int group, int& s, int& tn, int& tk) {
   // bijective for any grid size: XCD x owns logical tiles [start(x), start(x) + q (+1))
   const int total = gridDim.x;
   const int id = blockIdx.x;
   const int q = total / 8, rem = total % 8, xcd = id % 8;
   const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + id / 8;
-  tk = L % tiles_k;
-  const int rest = L / tiles_k;
-  tn = rest % tiles_n;
-  s = rest / tiles_n;
+  const int per = tiles_n * tiles_k;
+  s = L / per;
+  const int p = L - s * per;
+  const int gfull = group * tiles_k;
+  const int gid = p / gfull;
+  const int first = gid * group;
+  const int gs = tiles_n - first < group ? tiles_n - first : group;
+  const int r = p - gid * gfull;
+  tn = first + r % gs;
+  tk = r / gs;
 }
 
 template <typename T>
 __global__ __launch_bounds__(kT, 1) void wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                         float* __restrict__ ws, int64_t Tn, int N, int K,
-                                                        int64_t lda, int64_t ldb, int64_t t_split) {
+                                                        int64_t lda, int64_t ldb, int64_t t_split, int group) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[TK * RW];
   __shared__ __attribute__((aligned(16))) uint16_t sB[TK * RW];
   const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
   int split, tn, tk;
-  wg_map(tiles_n, tiles_k, split, tn, tk);
+  wg_map(tiles_n, tiles_k, group, split, tn, tk);
   const int n0 = tn * TM, k0 = tk * TN;
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
@@ -242,95 +251,121 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_b
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
 
-// one operand tile (TK rows x 256 cols) -> LDS; this wave issues rows 16 w + 2 i + (lane >> 5)
+// one operand tile (TKS rows x 256 cols) -> LDS by W waves; wave w issues rows
+// (TKS / W) w + 2 i + (lane >> 5), i < TKS / (2 W)
+template <int W, int TKS>
 __device__ __forceinline__ void stage_glds(uint16_t* lds, const uint16_t* src, int64_t ld, int vc, int wave,
                                            int lane) {
+  constexpr int RPW = TKS / W;
+  static_assert(RPW >= 2 && RPW % 2 == 0, "each wave stages whole row pairs");
   const int pc = lane & 31, half = lane >> 5;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = 16 * wave + 2 * i + half;
+  for (int i = 0; i < RPW / 2; ++i) {
+    const int r = RPW * wave + 2 * i + half;
     const int g = ((r & 3) << 2) | ((r >> 2) & 3);
     int c = pc ^ g;
     c = c < vc ? c : vc - 1;
-    glds16(src + static_cast<int64_t>(r) * ld + c * 8, lds + (16 * wave + 2 * i) * RW);
+    glds16(src + static_cast<int64_t>(r) * ld + c * 8, lds + (RPW * wave + 2 * i) * RW);
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(kT, 1) void wgrad_glds_kernel(const uint16_t* __restrict__ A,
+// s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// WN waves along the output columns (2 -> 4 waves of 128 x 128, 4 -> 8 waves of 128 x 64:
+// two waves per SIMD, each with half the accumulators).  NS-stage ring of TKS-token tiles:
+// the DMA of tile t + NS - 1 is issued right after the barrier that opens tile t, so a load
+// has NS - 1 tiles of MFMA work to land; one barrier per tile.
+template <typename T, int WN, int TKS, int NS>
+__global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B, float* __restrict__ ws,
                                                              int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
-                                                             int64_t t_split) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // 2 stages x (A, B) x 32 KB
+                                                             int64_t t_split, int group) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // NS stages x (A, B) x TKS rows
   const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
   int split, tn, tk;
-  wg_map(tiles_n, tiles_k, split, tn, tk);
+  wg_map(tiles_n, tiles_k, group, split, tn, tk);
   const int n0 = tn * TM, k0 = tk * TN;
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  constexpr int W = 2 * WN, NJ = 8 / WN, WCOLS = 32 * NJ;
+  constexpr int L = 2 * (TKS / W / 2);  // DMA instructions per wave per tile (A and B)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int hh = lane >> 5;
-  int aLo[4], aHi[4], bLo[4], bHi[4];
+  int aLo[4], aHi[4], bLo[NJ], bHi[NJ];
   {
     const int q = (lane & 15) >> 2, pp = lane & 3;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ca = wm * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
-      const int cb = wn * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
       aLo[i] = swz(4 * hh + q, ca >> 3) + (ca & 7);
       aHi[i] = swz(4 * hh + 8 + q, ca >> 3) + (ca & 7);
-      bLo[i] = swz(4 * hh + q, cb >> 3) + (cb & 7);
-      bHi[i] = swz(4 * hh + 8 + q, cb >> 3) + (cb & 7);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cb = wn * WCOLS + 32 * j + 16 * ((lane >> 4) & 1) + 4 * pp;
+      bLo[j] = swz(4 * hh + q, cb >> 3) + (cb & 7);
+      bHi[j] = swz(4 * hh + 8 + q, cb >> 3) + (cb & 7);
     }
   }
-  f32x16 acc[4][4];
+  f32x16 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{0.f};
   const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
   const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
-  const int64_t ntiles = (t_end - t_begin) / TK;
+  const int64_t ntiles = (t_end - t_begin) / TKS;
   const uint16_t* pa = A + t_begin * lda + n0;
   const uint16_t* pb = B + t_begin * ldb + k0;
-  constexpr int STAGE = 2 * TK * RW;  // elements per stage (A then B)
-  if (ntiles > 0) {
-    stage_glds(smem, pa, lda, vcA, wave, lane);
-    stage_glds(smem + TK * RW, pb, ldb, vcB, wave, lane);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // publishes the first tile
-  for (int64_t t = 0; t < ntiles; ++t) {
-    uint16_t* cur = smem + (t & 1) * STAGE;
-    if (t + 1 < ntiles) {
-      uint16_t* nxt = smem + ((t + 1) & 1) * STAGE;
-      stage_glds(nxt, pa + (t + 1) * TK * lda, lda, vcA, wave, lane);
-      stage_glds(nxt + TK * RW, pb + (t + 1) * TK * ldb, ldb, vcB, wave, lane);
+  constexpr int STAGE = 2 * TKS * RW;  // elements per stage (A then B)
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) {
+    if (p < ntiles) {
+      stage_glds<W, TKS>(smem + p * STAGE, pa + p * TKS * lda, lda, vcA, wave, lane);
+      stage_glds<W, TKS>(smem + p * STAGE + TKS * RW, pb + p * TKS * ldb, ldb, vcB, wave, lane);
     }
-    const uint16_t* sA = cur;
-    const uint16_t* sB = cur + TK * RW;
+  }
+  int cur_slot = 0, load_slot = NS - 1;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    if (t + NS - 2 < ntiles)
+      wait_vm<(NS - 2) * L>();  // this wave's DMA of tile t landed (later tiles may fly)
+    else
+      wait_vm<0>();
+    __syncthreads();  // ... everyone's, and every wave is done reading tile t - 1's slot
+    if (t + NS - 1 < ntiles) {
+      uint16_t* nxt = smem + load_slot * STAGE;
+      const int64_t tt = t + NS - 1;
+      stage_glds<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane);
+      stage_glds<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane);
+    }
+    load_slot = load_slot + 1 == NS ? 0 : load_slot + 1;
+    const uint16_t* sA = smem + cur_slot * STAGE;
+    const uint16_t* sB = sA + TKS * RW;
+    cur_slot = cur_slot + 1 == NS ? 0 : cur_slot + 1;
 #pragma unroll
-    for (int s = 0; s < TK / 16; ++s) {
-      typename WMF<T>::e8 fa[4], fb[4];
+    for (int s = 0; s < TKS / 16; ++s) {
+      typename WMF<T>::e8 fa[4], fb[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
-        fb[i] = ld_tr<T>(sB, bLo[i] + s * 16 * RW, bHi[i] + s * 16 * RW);
-      }
+      for (int i = 0; i < 4; ++i) fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = ld_tr<T>(sB, bLo[j] + s * 16 * RW, bHi[j] + s * 16 * RW);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1 landed
-    __syncthreads();  // ... everyone's, and every wave is done reading tile t
   }
   float* out = ws + static_cast<int64_t>(split) * N * K;
   const int col_l = lane & 31;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = k0 + wn * 128 + 32 * j + col_l;
+  for (int j = 0; j < NJ; ++j) {
+    const int k = k0 + wn * WCOLS + 32 * j + col_l;
     if (k >= K) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -341,6 +376,248 @@ __global__ __launch_bounds__(kT, 1) void wgrad_glds_kernel(const uint16_t* __res
         if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
       }
     }
+  }
+}
+
+// n-tiles per workgroup group in wg_map (SMP_WGRAD_GROUP, default 1: measured no better at 2-8)
+inline int wgrad_group() {
+  static const int v = [] {
+    const char* e = getenv("SMP_WGRAD_GROUP");
+    const int g = e != nullptr ? atoi(e) : 1;
+    return g >= 1 && g <= 32 ? g : 1;
+  }();
+  return v;
+}
+
+// ---------------------------------------------------------------- phased (ping-pong) variant
+// 8 waves (2 along N x 4 along K, 128 x 64 outputs each), 64-token K-tiles in two buffers.
+// A buffer holds four 16 KB QUARTERS, each the part of the tile one MFMA phase consumes:
+//   slot 0: A columns {0..63, 128..191}   (qm = 0 of both N wave rows)
+//   slot 1: B columns {64 w + 0..31}      (qn = 0 of the four K wave columns)
+//   slot 2: B columns {64 w + 32..63}     (qn = 1)
+//   slot 3: A columns {64..127, 192..255} (qm = 1)
+// Each tile runs 4 phases, one output quadrant each: (qm, qn) = (0,0) (0,1) (1,1) (1,0).
+// A phase = [this phase's transposed LDS reads; DMA of one quarter of the NEXT tile; counted
+// vmcnt; barrier; 8 MFMAs at raised priority; barrier].  Quarter j of tile t + 1 is issued in
+// phase j of tile t and first read 3-4 phases later; the wait is counted (vmcnt 4, never 0 in
+// steady state).  With PP the two N wave rows run one barrier apart (the second row takes an
+// extra barrier up front), so on every SIMD one wave multiplies while the other reads LDS and
+// issues DMA.  A wave waits for the data of phase p + 1 before its mid-phase barrier of phase
+// p: with the one-barrier stagger that still precedes every reader's phase p + 1.
+constexpr int QR = 128;       // elements per quarter row (256 B)
+constexpr int QE = TK * QR;   // elements per quarter
+constexpr int QBUF = 4 * QE;  // elements per K-tile buffer
+
+// 16 chunks per 256-B row, chunk ^= 4 (row & 3): the 4-row x 32-column transposed reads of a
+// 32-lane half hit all 64 banks once
+__device__ __forceinline__ int qswz(int row, int col) {
+  return row * QR + ((((col >> 3) ^ ((row & 3) << 2))) << 3) + (col & 7);
+}
+
+// one quarter (64 tokens x 128 region columns): region column x reads source column
+// qoff + (x >> plog) * stride + (x & (piece - 1)) of the tile; 16 four-row DMA instructions,
+// two per wave.  Columns at or past vcols (matrix edge) re-read column 0 -- they only feed
+// outputs that are never stored.
+__device__ __forceinline__ void stage_quarter(uint16_t* region, const uint16_t* src, int64_t ld, int qoff, int plog,
+                                              int stride, int vcols, int wave, int lane) {
+  const int sub = lane >> 4;
+  const int lc = (lane & 15) ^ (sub << 2);
+  const int x = lc * 8;
+  int col = qoff + (x >> plog) * stride + (x & ((1 << plog) - 1));
+  col = col < vcols ? col : 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = 2 * wave + i;
+    glds16(src + static_cast<int64_t>(4 * m + sub) * ld + col, region + 4 * m * QR);
+  }
+}
+
+__device__ __forceinline__ void phase_sync() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <typename T>
+__device__ __forceinline__ void ld_frags(typename WMF<T>::e8 (&f)[4], const uint16_t* region, int off) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) f[s] = ld_tr<T>(region, off + s * 16 * QR, off + s * 16 * QR + 8 * QR);
+}
+
+template <typename T>
+__device__ __forceinline__ void mma_quadrant(f32x16& c0, f32x16& c1, const typename WMF<T>::e8 (&a0)[4],
+                                             const typename WMF<T>::e8 (&a1)[4], const typename WMF<T>::e8 (&b)[4]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    c0 = WMF<T>::mma(a0[s], b[s], c0);
+    c1 = WMF<T>::mma(a1[s], b[s], c1);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <typename T, bool PP>
+__global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const uint16_t* __restrict__ A,
+                                                          const uint16_t* __restrict__ B, float* __restrict__ ws,
+                                                          int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
+                                                          int64_t t_split, int group) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // 2 K-tile buffers x 4 quarters
+  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
+  int split, tn, tk;
+  wg_map(tiles_n, tiles_k, group, split, tn, tk);
+  const int n0 = tn * TM, k0 = tk * TN;
+  const int64_t t_begin = split * t_split;
+  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  int aOff0, aOff1, bOff;
+  {
+    const int row = 4 * (lane >> 5) + ((lane & 15) >> 2);
+    const int c = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+    aOff0 = qswz(row, wr * 64 + c);
+    aOff1 = qswz(row, wr * 64 + 32 + c);
+    bOff = qswz(row, wc * 32 + c);
+  }
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{0.f};
+  const int vA = (N - n0) >= TM ? TM : N - n0;
+  const int vB = (K - k0) >= TN ? TN : K - k0;
+  const int64_t ntiles = t_end > t_begin ? (t_end - t_begin) / TK : 0;
+  const uint16_t* pa = A + t_begin * lda + n0;
+  const uint16_t* pb = B + t_begin * ldb + k0;
+  if (ntiles > 0) {
+    stage_quarter(smem + 0 * QE, pa, lda, 0, 6, 128, vA, wave, lane);
+    stage_quarter(smem + 1 * QE, pb, ldb, 0, 5, 64, vB, wave, lane);
+    stage_quarter(smem + 2 * QE, pb, ldb, 32, 5, 64, vB, wave, lane);
+    stage_quarter(smem + 3 * QE, pa, lda, 64, 6, 128, vA, wave, lane);
+    wait_vm<4>();  // slots 0, 1 of tile 0
+    phase_sync();
+    if (PP && wr == 1) phase_sync();
+    typename WMF<T>::e8 fa0[4], fa1[4], fb0[4], fb1[4];
+    for (int64_t t = 0; t < ntiles; ++t) {
+      const uint16_t* cb = smem + (t & 1) * QBUF;
+      uint16_t* nb = smem + ((t + 1) & 1) * QBUF;
+      const bool next = t + 1 < ntiles;
+      const uint16_t* na = pa + (t + 1) * TK * lda;
+      const uint16_t* nbp = pb + (t + 1) * TK * ldb;
+      // phase 0: (qm 0, qn 0)
+      ld_frags<T>(fa0, cb + 0 * QE, aOff0);
+      ld_frags<T>(fa1, cb + 0 * QE, aOff1);
+      ld_frags<T>(fb0, cb + 1 * QE, bOff);
+      if (next) {
+        stage_quarter(nb + 0 * QE, na, lda, 0, 6, 128, vA, wave, lane);
+        wait_vm<4>();  // slot 2 of tile t
+      } else {
+        wait_vm<0>();
+      }
+      phase_sync();
+      mma_quadrant<T>(acc[0][0], acc[1][0], fa0, fa1, fb0);
+      phase_sync();
+      // phase 1: (qm 0, qn 1)
+      ld_frags<T>(fb1, cb + 2 * QE, bOff);
+      if (next) {
+        stage_quarter(nb + 1 * QE, nbp, ldb, 0, 5, 64, vB, wave, lane);
+        wait_vm<4>();  // slot 3 of tile t
+      } else {
+        wait_vm<0>();
+      }
+      phase_sync();
+      mma_quadrant<T>(acc[0][1], acc[1][1], fa0, fa1, fb1);
+      phase_sync();
+      // phase 2: (qm 1, qn 1)
+      ld_frags<T>(fa0, cb + 3 * QE, aOff0);
+      ld_frags<T>(fa1, cb + 3 * QE, aOff1);
+      if (next) stage_quarter(nb + 2 * QE, nbp, ldb, 32, 5, 64, vB, wave, lane);
+      phase_sync();
+      mma_quadrant<T>(acc[2][1], acc[3][1], fa0, fa1, fb1);
+      phase_sync();
+      // phase 3: (qm 1, qn 0)
+      if (next) {
+        stage_quarter(nb + 3 * QE, na, lda, 64, 6, 128, vA, wave, lane);
+        wait_vm<4>();  // slots 0, 1 of tile t + 1
+      }
+      phase_sync();
+      mma_quadrant<T>(acc[2][0], acc[3][0], fa0, fa1, fb0);
+      phase_sync();
+    }
+    if (PP && wr == 0) phase_sync();
+  }
+  float* out = ws + static_cast<int64_t>(split) * N * K;
+  const int col_l = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = k0 + wc * 64 + 32 * j + col_l;
+    if (k >= K) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int nb = n0 + wr * 128 + 32 * i + 4 * hh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = nb + (r & 3) + 8 * (r >> 2);
+        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+template <typename T, bool PP>
+int launch_pp(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
+              int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
+  constexpr size_t lds = 2 * QBUF * sizeof(uint16_t);  // 128 KB
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<T, PP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr_set = true;
+  }
+  wgrad_pp_kernel<T, PP><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
+  return 0;
+}
+
+// SMP_WGRAD_PIPE: 0 = 4 waves, 2 x 64-token stages; 1 = 8 waves, 2 x 64; 2 = 8 waves,
+// 4 x 32; 3 = 8 waves, 5 x 32 (all 160 KB of LDS); 4 = phased, lockstep; 5 = phased ping-pong
+inline int wgrad_pipe() {
+  static const int v = [] {
+    const char* e = getenv("SMP_WGRAD_PIPE");
+    if (e != nullptr && e[0] >= '0' && e[0] <= '5') return e[0] - '0';
+    const char* w = getenv("SMP_WGRAD_WAVES");
+    return (w != nullptr && w[0] == '4') ? 0 : 1;
+  }();
+  return v;
+}
+
+template <typename T, int WN, int TKS, int NS>
+int launch_glds(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
+                int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
+  constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t);
+  static_assert(lds <= 160 * 1024, "LDS per CU");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<T, WN, TKS, NS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr_set = true;
+  }
+  wgrad_glds_kernel<T, WN, TKS, NS><<<grid, 128 * WN, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
+  return 0;
+}
+
+template <typename T>
+int launch_glds_pipe(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
+                     int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
+  switch (wgrad_pipe()) {
+    case 0:
+      return launch_glds<T, 2, 64, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 2:
+      return launch_glds<T, 4, 32, 4>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 3:
+      return launch_glds<T, 4, 32, 5>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 4:
+      return launch_pp<T, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 5:
+      return launch_pp<T, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    default:
+      return launch_glds<T, 4, 64, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
   }
 }
 
@@ -404,29 +681,20 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   t_split = (t_split + TK - 1) / TK * TK;
   const int grid = tiles * splits;
   if (wgrad_use_glds()) {
-    constexpr size_t lds = 2 * 2 * TK * RW * sizeof(uint16_t);  // 128 KB
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<bf16>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<f16>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-      attr_set = true;
-    }
+    const auto* pa = static_cast<const uint16_t*>(a);
+    const auto* pb = static_cast<const uint16_t*>(b);
     if (dt == BF16)
-      wgrad_glds_kernel<bf16><<<grid, kT, lds, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                                    tokens, n, k, lda, ldb, t_split);
+      launch_glds_pipe<bf16>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
     else if (dt == F16)
-      wgrad_glds_kernel<f16><<<grid, kT, lds, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                                   tokens, n, k, lda, ldb, t_split);
+      launch_glds_pipe<f16>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
     else
       return -2;
   } else if (dt == BF16)
     wgrad_kernel<bf16><<<grid, kT, 0, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                            tokens, n, k, lda, ldb, t_split);
+                                            tokens, n, k, lda, ldb, t_split, 1);
   else if (dt == F16)
     wgrad_kernel<f16><<<grid, kT, 0, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                           tokens, n, k, lda, ldb, t_split);
+                                           tokens, n, k, lda, ldb, t_split, 1);
   else
     return -2;
   hipError_t e = hipGetLastError();

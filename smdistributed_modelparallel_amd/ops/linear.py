@@ -210,10 +210,13 @@ def _wgrad_native_ok(g, dy2, x2):
             and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
-def _wgrad_kernel_wins(g, dy2, x2):
-    """Time the MFMA kernel against the library GEMM once per (T, N, K, dtypes)."""
+def _wgrad_kernel_splits(g, dy2, x2):
+    """Split count for the MFMA kernel at this (T, N, K, dtypes), or 0 for the library GEMM.
+
+    Timed once per shape: the kernel at its occupancy-model split count and at a few smaller
+    counts (fewer fp32 partials to reduce; the model ignores that traffic), and the library."""
     if _WGRAD_KERNEL == "1" or g.dtype != dy2.dtype:  # (fp32 accumulators: no library equivalent)
-        return True
+        return -1  # kernel, default split count
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype, g.dtype)
     hit = _WGRAD_KERNEL_CHOICE.get(key)
     if hit is not None:
@@ -221,9 +224,14 @@ def _wgrad_kernel_wins(g, dy2, x2):
     from ._ext import ext
 
     C = ext()
+    T = dy2.shape[0]
+    model = C.wgrad_splits(T, dy2.shape[1], x2.shape[1], torch.cuda.get_device_properties(g.device).multi_processor_count)
+    splits = sorted({s for s in (model, max(1, model // 2), 4, 2) if s <= max(1, T // 512)}, reverse=True)
+    cands = [(s, (lambda s=s: C.wgrad_(g, dy2, x2, True, s))) for s in splits]
+    cands.append((0, lambda: g.addmm_(dy2.t(), x2)))
     saved = g.clone()
     times = {}
-    for name, fn in (("kernel", lambda: C.wgrad_(g, dy2, x2, True)), ("library", lambda: g.addmm_(dy2.t(), x2))):
+    for name, fn in cands:
         fn()  # warm-up (library solution selection, allocator)
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         start.record()
@@ -234,21 +242,28 @@ def _wgrad_kernel_wins(g, dy2, x2):
         times[name] = start.elapsed_time(end)
         g.copy_(saved)
     del saved
-    win = times["kernel"] < times["library"]
-    _WGRAD_KERNEL_CHOICE[key] = win
+    best = min(times, key=times.get)
+    _WGRAD_KERNEL_CHOICE[key] = best
     if os.environ.get("SMP_WGRAD_LOG") == "1":
-        print(f"wgrad T={key[0]} N={key[1]} K={key[2]}: kernel {times['kernel'] / 3:.3f} ms, "
-              f"library {times['library'] / 3:.3f} ms -> {'kernel' if win else 'library'}", flush=True)
-    return win
+        print(f"wgrad T={key[0]} N={key[1]} K={key[2]}: "
+              + ", ".join(f"{'library' if s == 0 else f'kernel s{s}'} {t / 3:.3f} ms" for s, t in times.items())
+              + f" -> {'library' if best == 0 else f'kernel s{best}'}", flush=True)
+    return best
+
+
+def _wgrad_kernel_wins(g, dy2, x2):
+    return _wgrad_kernel_splits(g, dy2, x2) != 0
 
 
 def _wgrad_accumulate(g, dy2, x2):
     """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape."""
-    if _wgrad_native_ok(g, dy2, x2) and _wgrad_kernel_wins(g, dy2, x2):
-        from ._ext import ext
+    if _wgrad_native_ok(g, dy2, x2):
+        s = _wgrad_kernel_splits(g, dy2, x2)
+        if s != 0:
+            from ._ext import ext
 
-        ext().wgrad_(g, dy2, x2, True)
-        return
+            ext().wgrad_(g, dy2, x2, True, max(s, 0))
+            return
     method = "nn"
     if _WGRAD_TUNE and g.is_cuda and dy2.shape[0] >= _WGRAD_MIN_T and dy2.is_contiguous() and x2.is_contiguous():
         key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype)

@@ -24,7 +24,7 @@ def main(dirs):
     for d in dirs:
         for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
             k = short(r["Kernel_Name"])
-            if "smpk" not in r["Kernel_Name"]:
+            if "smpk" not in r["Kernel_Name"] and "Cijk" not in r["Kernel_Name"]:
                 continue
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
             durs[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
