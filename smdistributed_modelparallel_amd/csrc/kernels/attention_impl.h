@@ -329,6 +329,28 @@ __device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbas
   }
 }
 
+// LDS-DMA of one K or V tile (BN rows x D, D = 64 / 128: the LDS image is exactly [BN][D]):
+// each wave-instruction fills 1 KB = 1024 / (2 D) consecutive rows, lane-linear, so the
+// row's XOR swizzle moves to the SOURCE chunk (physical chunk pc of row r holds logical
+// chunk pc ^ g(r), g as in swz).  Rows at or past `sk` re-read row sk - 1 (finite data: the
+// masked path gives those keys p = 0).
+template <int D, int BN>
+__device__ __forceinline__ void dma_tile(uint16_t* lds, const uint16_t* base, int64_t ss, int row0, int sk, int wave,
+                                         int lane) {
+  constexpr int CPR = D / 8, RPI = 64 / CPR, NI = BN / RPI;  // chunks/row, rows/instr, instrs/tile
+  static_assert(NI % (kThreads / 64) == 0, "instructions split evenly over the waves");
+  const int rl = lane / CPR, pc = lane % CPR;
+#pragma unroll
+  for (int i = 0; i < NI / (kThreads / 64); ++i) {
+    const int rb = (wave * (NI / (kThreads / 64)) + i) * RPI;
+    const int r = rb + rl;
+    const int lc = (swz<D>(r, pc) - r * D) >> 3;  // chunk position of logical pc == pc ^ g(r)
+    int gr = row0 + r;
+    gr = gr < sk ? gr : sk - 1;
+    lds_dma16(base + static_cast<int64_t>(gr) * ss + lc * 8, lds + rb * D);
+  }
+}
+
 // ================================================================== forward
 // Block = 4 waves x 32 queries; K/V tiles of 64 keys.  Interior tiles (every key visible
 // to every query of the wave) take a mask-free path.
@@ -339,12 +361,18 @@ struct QInLds {
   static constexpr bool v = D >= 256;
 };
 
-template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
+// DMA: K/V tiles arrive by LDS-DMA into two buffers (no staging registers, no ds_write, one
+// barrier per tile); D = 64 / 128 without bias.
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
 __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr bool QLDS = QInLds<D>::v;
-  __shared__ __attribute__((aligned(16))) uint16_t sK[BN * DS];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[BN * DS];
+  static_assert(!DMA || (!QLDS && !BIAS && DS == D && (D == 64 || D == 128)), "DMA variant: D 64 / 128, no bias");
+  // K then V of each buffer (one array: a second LDS object beside DMA targets can make
+  // hipcc drain vmcnt before ds_reads)
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[(DMA ? 4 : 2) * BN * DS];
+  uint16_t* sK = sKV;
+  uint16_t* sV = sKV + BN * DS;
   __shared__ __attribute__((aligned(16))) uint16_t sQ[QLDS ? BM * DS : 8];
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
   __shared__ int sFlag;
@@ -402,30 +430,55 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
     const int lo = qb * BM + diag - win + 1;
     kv_begin = lo > 0 ? (lo / BN) * BN : 0;
   }
-  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
+  Stage<D, BN> stK(p.k_ss), stV(p.v_ss);  // (unused by DMA)
   const RowOff<D> ro(r, hh);
   const TrOff<D> tro(lane);
   float bstage = 0.f;
+  if constexpr (DMA) {
+    // retire the Q loads with a wait hipcc tracks: otherwise it keeps them "pending" across
+    // the loop and drains vmcnt(0) -- the in-flight K/V DMA included -- before the first MFMA
+    __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
+  }
   if (kv_begin < kv_end) {
-    stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
-    stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
-    if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
+    if constexpr (DMA) {
+      dma_tile<D, BN>(sKV, K, p.k_ss, kv_begin, sk, wave, lane);
+      dma_tile<D, BN>(sKV + BN * DS, V, p.v_ss, kv_begin, sk, wave, lane);
+    } else {
+      stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
+      stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
+      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
+    }
   }
   const int wave_last_q = q0 + 31;
+  int buf = 0;
   for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
-    __syncthreads();
-    stK.store(sK);
-    stV.store(sV);
-    if (BIAS) {
-      if (threadIdx.x < BN) sB[threadIdx.x] = bstage * inv_scale;
-      publish_bias_flag(bstage, &sFlag);
-    }
-    __syncthreads();
-    const bool tile_bias = BIAS && sFlag != 0;
-    if (kv0 + BN < kv_end) {
-      stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
-      stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
-      if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
+    bool tile_bias = false;
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the tile landed
+      __syncthreads();  // ... everyone's; and every wave is done with the other buffer
+      sK = sKV + buf * 2 * BN * DS;
+      sV = sK + BN * DS;
+      if (kv0 + BN < kv_end) {
+        uint16_t* nb = sKV + (buf ^ 1) * 2 * BN * DS;
+        dma_tile<D, BN>(nb, K, p.k_ss, kv0 + BN, sk, wave, lane);
+        dma_tile<D, BN>(nb + BN * DS, V, p.v_ss, kv0 + BN, sk, wave, lane);
+      }
+      buf ^= 1;
+    } else {
+      __syncthreads();
+      stK.store(sK);
+      stV.store(sV);
+      if (BIAS) {
+        if (threadIdx.x < BN) sB[threadIdx.x] = bstage * inv_scale;
+        publish_bias_flag(bstage, &sFlag);
+      }
+      __syncthreads();
+      tile_bias = BIAS && sFlag != 0;
+      if (kv0 + BN < kv_end) {
+        stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
+        stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
+        if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
+      }
     }
     if (CAUSAL && kv0 > wave_last_q + diag) continue;
     if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
@@ -641,7 +694,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         d_stage = qq < sq ? DL[qq] : 0.f;
       }
     }
-#pragma unroll 1
+    // D = 64 without dropout: both 32-query sub-steps in one unrolled body (the second one's S / dP MFMAs
+    // overlap the first one's exp / dS work)
+#pragma unroll(D == 64 && !DROP ? 2 : 1)
     for (int sub = 0; sub < 2; ++sub) {
       const int qs = qt + 32 * sub;  // first query of this sub-step
       if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
@@ -874,9 +929,25 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
 }
 
 // ------------------------------------------------------------------ launchers
+
+// SMP_ATTN_DMA=0 keeps the register-staged K/V path for D = 64 / 128
+inline bool attn_dma_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("SMP_ATTN_DMA");
+    return e == nullptr || e[0] != '0';
+  }();
+  return v;
+}
+
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_fwd_v(const AttnParams& p, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
+  if constexpr ((D == 64 || D == 128) && !BI) {
+    if (attn_dma_enabled()) {
+      attn_fwd_kernel<T, D, C, DR, BI, true><<<grid, kThreads, 0, s>>>(p);
+      return static_cast<int>(hipGetLastError());
+    }
+  }
   attn_fwd_kernel<T, D, C, DR, BI><<<grid, kThreads, 0, s>>>(p);
   return static_cast<int>(hipGetLastError());
 }

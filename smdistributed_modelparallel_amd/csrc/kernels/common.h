@@ -127,6 +127,17 @@ __device__ __forceinline__ float block_max(float v, float* smem) {
   return r;
 }
 
+// LDS-DMA: 16 B per lane from `src` into LDS at lds_wave_base + 16 * lane (global_load_lds,
+// lane-linear destination, base in M0).  Issued from inline asm: with the builtin, hipcc
+// (ROCm 7.2) cannot tell the LDS buffer being filled from the one being read and drains
+// vmcnt(0) before the next ds_read -- a prefetch would never overlap compute.  The caller
+// waits for it with an explicit s_waitcnt vmcnt before the barrier that publishes the data.
+__device__ __forceinline__ void lds_dma16(const void* src, const void* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
 }  // namespace smpk
 
 #define SMPK_CHECK(expr)                                                      \

@@ -245,11 +245,7 @@ __global__ __launch_bounds__(kT, 1) void wgrad_kernel(const uint16_t* __restrict
 // buffer being filled from the one being read and drains vmcnt(0) before the first ds_read
 // of every tile -- the prefetch would never overlap the MFMAs.  The loop waits for its own
 // DMA explicitly (vmcnt(0) before the end-of-tile barrier).
-__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) uint16_t*)lds_wave_base)));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
-}
+__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_wave_base) { lds_dma16(src, lds_wave_base); }
 
 // one operand tile (TKS rows x 256 cols) -> LDS by W waves; wave w issues rows
 // (TKS / W) w + 2 i + (lane >> 5), i < TKS / (2 W)
