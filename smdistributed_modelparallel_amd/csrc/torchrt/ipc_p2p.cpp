@@ -266,10 +266,12 @@ void register_ipc_p2p(py::module& m) {
 }
 
 void register_grad_tracker(py::module& m);
+void register_ipc_allreduce(py::module& m);
 
 void register_bindings(py::module& m) {
   register_grad_tracker(m);
   register_ipc_p2p(m);
+  register_ipc_allreduce(m);
 }
 
 }  // namespace smprt_torch

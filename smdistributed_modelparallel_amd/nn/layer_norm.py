@@ -15,6 +15,7 @@ import torch.nn as nn
 from ..ops.layernorm import add_layer_norm, layer_norm, layer_norm_passthrough
 from ..parallel.throttle import throttler
 from .utils import get_local_channels, get_start_pos_for_slicing, tp_group, tp_size
+from ..parallel import oneshot
 
 
 class FusedLayerNorm(nn.Module):
@@ -85,12 +86,12 @@ class _DistLNStats(torch.autograd.Function):
         s1 = xf.sum(-1, keepdim=True)
         if group is not None:
             with throttler().throttle(s1):
-                dist.all_reduce(s1, group=group)
+                oneshot.all_reduce(s1, group=group)
         mean = s1 / full_dim
         s2 = (xf - mean).pow(2).sum(-1, keepdim=True)
         if group is not None:
             with throttler().throttle(s2):
-                dist.all_reduce(s2, group=group)
+                oneshot.all_reduce(s2, group=group)
         var = s2 / full_dim
         ctx.save_for_backward(xf, mean)
         ctx.full_dim, ctx.group = full_dim, group
@@ -104,7 +105,7 @@ class _DistLNStats(torch.autograd.Function):
             # every rank's local y depends on the shared statistics: sum their grads
             g = torch.cat([gmean, gvar], dim=-1).contiguous()
             with throttler().throttle(g):
-                dist.all_reduce(g, group=ctx.group)
+                oneshot.all_reduce(g, group=ctx.group)
             gmean, gvar = g[..., :1], g[..., 1:]
         # d mean / dx = 1/n ; d var / dx = 2 (x - mean) / n  (the mean term sums to zero)
         gx = gmean / n + gvar * 2.0 * (xf - mean) / n
@@ -126,7 +127,7 @@ class _DistLayerNormHIP(torch.autograd.Function):
         st = ext().layernorm_local_stats(x2)  # (n*m, M2, n*m*m) per row of the local shard
         if group is not None:
             with throttler().throttle(st):
-                dist.all_reduce(st, group=group)
+                oneshot.all_reduce(st, group=group)
         n = float(full_dim)
         mean = st[:, 0] / n
         var = ((st[:, 1] + st[:, 2]) / n - mean * mean).clamp_min_(0.0)  # Chan's combination
@@ -146,7 +147,7 @@ class _DistLayerNormHIP(torch.autograd.Function):
         sums = ext().layernorm_bwd_local_sums(dy2, x2, w, mean, rstd)  # (sum g, sum g*xhat) local
         if ctx.group is not None:
             with throttler().throttle(sums):
-                dist.all_reduce(sums, group=ctx.group)
+                oneshot.all_reduce(sums, group=ctx.group)
         need_w = ctx.has_w and ctx.needs_input_grad[1]
         need_b = ctx.has_b and ctx.needs_input_grad[2]
         dx, dw, db = ext().layernorm_bwd(dy2, x2, w, mean, rstd, need_w, need_b, None, ext_sums=sums,

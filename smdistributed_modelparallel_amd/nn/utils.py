@@ -21,6 +21,7 @@ import torch.distributed as dist
 from ..torch.state_mod import state
 from ..ops.pack import strided_copy_
 from ..parallel.throttle import throttler
+from ..parallel import oneshot
 
 
 # --------------------------------------------------------------------- topology
@@ -149,7 +150,7 @@ def _allreduce(x, inplace=False):
     if not inplace or not x.is_contiguous():
         x = x.clone(memory_format=torch.contiguous_format)
     with throttler().throttle(x):
-        dist.all_reduce(x, group=tp_group())
+        oneshot.all_reduce(x, group=tp_group())
     return x
 
 

@@ -10,6 +10,7 @@ import torch
 import torch.distributed as dist
 
 from ._ext import ext
+from ..parallel import oneshot
 
 
 class _FusedCrossEntropy(torch.autograd.Function):
@@ -21,10 +22,10 @@ class _FusedCrossEntropy(torch.autograd.Function):
         mx, se, tl = C.xent_fwd(l2, t, vocab_start, ignore_index)
         if group is not None and dist.get_world_size(group) > 1:
             gmx = mx.clone()
-            dist.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
+            oneshot.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
             se = se * torch.exp(mx - gmx)
-            dist.all_reduce(se, group=group)
-            dist.all_reduce(tl, group=group)
+            oneshot.all_reduce(se, group=group)
+            oneshot.all_reduce(tl, group=group)
             mx = gmx
         lse = mx + torch.log(se)
         loss = lse - tl
@@ -46,7 +47,7 @@ def _ref_vocab_parallel_ce(logits, target, vocab_start, ignore_index, group):
     V = lf.shape[-1]
     mx = lf.max(dim=-1).values
     if group is not None and dist.get_world_size(group) > 1:
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
+        oneshot.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
     shifted = lf - mx.unsqueeze(-1).detach()
     se = shifted.exp().sum(dim=-1)
     local_t = target - vocab_start
@@ -65,7 +66,7 @@ class _AllreduceSum(torch.autograd.Function):
     def forward(ctx, x, group):
         ctx.group = group
         x = x.clone()
-        dist.all_reduce(x, group=group)
+        oneshot.all_reduce(x, group=group)
         return x
 
     @staticmethod

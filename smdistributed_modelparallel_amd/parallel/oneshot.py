@@ -1,0 +1,149 @@
+"""One-shot all-reduce for small tensor-parallel messages.
+
+The reference sends every TP all-reduce to NCCL (`smp/torch/nn/utils.py:548,570`,
+`nn/layer_norm.py:41-79`, `nn/cross_entropy.py:34-66`).  For the small ones -- per-row
+statistics of the distributed LayerNorm and the vocab-parallel cross entropy, small-batch
+activations -- a ring all-reduce over xGMI is latency-bound (2 (n-1) link hops).  Here
+messages up to ``SMP_ONESHOT_ALLREDUCE_MAX_BYTES`` (default 1 MiB) on TP groups of at most
+``SMP_ONESHOT_ALLREDUCE_MAX_RANKS`` (default 4) ranks on one node go to the native
+``IpcAllReduce`` (`csrc/torchrt/ipc_allreduce.cpp`): one kernel, every rank reads every
+peer's registered buffer over xGMI once and reduces in rank order (bitwise-identical results
+on every rank, as TP requires).  Larger messages, other dtypes and CPU tensors take the
+RCCL / gloo path unchanged.
+
+Safety: the first use on a group builds the buffers, exchanges the IPC handles over the
+group and runs a self-check against ``dist.all_reduce`` (sum and max, rank-dependent
+data, two epochs so both buffer slots are exercised); any mismatch, timeout or mapping
+failure disables the path for that group with a warning.  ``SMP_ONESHOT_ALLREDUCE=0``
+disables it, ``=1`` also allows it for groups whose ranks share one GPU (single-GPU
+rehearsals and tests); the default ``auto`` needs distinct GPUs on one host.
+"""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+
+from ..backend.logger import get_logger
+
+logger = get_logger()
+
+_MODE = os.environ.get("SMP_ONESHOT_ALLREDUCE", "auto")
+_MAX_BYTES = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_BYTES", str(1 << 20)))
+_MAX_RANKS = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_RANKS", "4"))
+_TIMEOUT_S = float(os.environ.get("SMP_ONESHOT_ALLREDUCE_TIMEOUT_S", "10"))
+_DTYPES = (torch.bfloat16, torch.float16, torch.float32)
+
+_instances = {}  # group key -> IpcAllReduce or None (disabled)
+
+
+def _key(group):
+    return id(group) if group is not None else "world"
+
+
+def reset():
+    for inst in _instances.values():
+        if inst is not None:
+            try:
+                inst.close()
+            except Exception:  # pragma: no cover - best effort at shutdown
+                pass
+    _instances.clear()
+
+
+def _create(group):
+    """Collective over `group`: every member calls this with the same decision inputs."""
+    ws = dist.get_world_size(group)
+    if _MODE == "0" or ws < 2 or ws > min(_MAX_RANKS, 8) or not torch.cuda.is_available():
+        return None
+    from ..ops._ext import ext
+
+    dev = torch.cuda.current_device()
+    me = (socket.gethostname(), dev)
+    peers = [None] * ws
+    dist.all_gather_object(peers, me, group=group)
+    same_host = all(p[0] == me[0] for p in peers)
+    distinct = len({p[1] for p in peers}) == ws
+    if not same_host or (not distinct and _MODE != "1"):
+        return None
+    inst, err = None, None
+    try:
+        inst = ext().IpcAllReduce(dev, dist.get_rank(group), ws, 2 * _MAX_BYTES)
+        h = inst.handles()
+    except Exception as e:  # allocation / export failure: decided collectively below
+        err, h = repr(e), None
+    hs = [None] * ws
+    dist.all_gather_object(hs, h, group=group)
+    if err is None and any(x is None for x in hs):
+        err = "a peer could not export its buffers"
+    if err is None:
+        try:
+            inst.open(hs)
+        except Exception as e:
+            err = repr(e)
+    ok = err is None and _self_check(inst, group)
+    flags = [None] * ws
+    dist.all_gather_object(flags, bool(ok), group=group)
+    if not all(flags):
+        logger.warning(f"one-shot all-reduce disabled for a TP group of {ws}: "
+                       f"{err or 'self-check against dist.all_reduce failed'}")
+        if inst is not None:
+            inst.close()
+        return None
+    logger.info(f"one-shot IPC all-reduce enabled for a TP group of {ws} (<= {_MAX_BYTES} B messages)")
+    return inst
+
+
+def _self_check(inst, group):
+    r = dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ok = True
+    for n, dt in ((4099, torch.float32), (3 * 4096 + 8, torch.bfloat16)):
+        g = torch.Generator(device="cpu").manual_seed(1234 + 7 * r)
+        x = torch.randn(n, generator=g).to(dev, dt)
+        for op, dop in ((0, dist.ReduceOp.SUM), (1, dist.ReduceOp.MAX)):
+            ref = x.float().clone()
+            dist.all_reduce(ref, op=dop, group=group)
+            out = torch.empty_like(x)
+            inst.all_reduce(x, out, op, _TIMEOUT_S)
+            torch.cuda.synchronize()
+            if inst.error(True):
+                return False
+            tol = 1e-5 if dt == torch.float32 else 2e-2
+            if not torch.allclose(out.float(), ref.to(dt).float(), rtol=tol, atol=tol):
+                ok = False
+    return ok
+
+
+def _instance(group):
+    k = _key(group)
+    if k not in _instances:
+        _instances[k] = _create(group)
+    return _instances[k]
+
+
+def all_reduce(x, op=dist.ReduceOp.SUM, group=None):
+    """In-place all-reduce of x over group: one-shot IPC kernel for small contiguous GPU
+    tensors, ``dist.all_reduce`` otherwise."""
+    # the decision depends only on what every rank of the group shares (shape, dtype, op)
+    if (x.is_cuda and x.dtype in _DTYPES and x.is_contiguous() and x.numel() * x.element_size() <= _MAX_BYTES
+            and op in (dist.ReduceOp.SUM, dist.ReduceOp.MAX) and _MODE != "0"):
+        inst = _instance(group)
+        if inst is not None:
+            code = 0 if op == dist.ReduceOp.SUM else 1
+            if x.data_ptr() % 16 == 0:
+                inst.all_reduce(x, x, code, _TIMEOUT_S)
+            else:  # a view at an odd offset: reduce an aligned copy
+                t = x.clone()
+                inst.all_reduce(t, t, code, _TIMEOUT_S)
+                x.copy_(t)
+            return x
+    dist.all_reduce(x, op=op, group=group)
+    return x
+
+
+def check_errors():
+    """Raise if any one-shot all-reduce timed out waiting for a peer (synchronises)."""
+    for inst in _instances.values():
+        if inst is not None and inst.error(True):
+            raise RuntimeError("one-shot all-reduce: a kernel timed out waiting for a peer rank")

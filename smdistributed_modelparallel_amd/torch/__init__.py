@@ -154,6 +154,9 @@ def reset():
     if state.model is not None:
         for r in state.model.reducers.values():
             r.remove_hooks()
+    from ..parallel import oneshot
+
+    oneshot.reset()  # IPC buffers belong to the process groups being torn down
     state.reset()
 
 

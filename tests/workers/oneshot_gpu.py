@@ -1,0 +1,89 @@
+"""Worker: one-shot IPC all-reduce on ranks sharing one GPU (SMP_ONESHOT_ALLREDUCE=1).
+
+argv: kernel            -- sizes x dtypes x ops x repeated epochs against a gloo fp32 reference,
+                           results bitwise identical on every rank, aligned and odd-offset views
+      tp <steps>        -- GPT with tensor_parallel_degree = world through smp; prints the losses
+"""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def kernel():
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    from smdistributed_modelparallel_amd.parallel import oneshot
+
+    r, ws = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", 0)
+    checked = 0
+    for dt in (torch.float32, torch.bfloat16, torch.float16):
+        for n in (1, 7, 8, 1000, 4099, 65536, 262147, oneshot._MAX_BYTES // (4 if dt == torch.float32 else 2)):
+            for op in (dist.ReduceOp.SUM, dist.ReduceOp.MAX):
+                for it in range(3):
+                    g = torch.Generator().manual_seed(1000 * r + 17 * it + n)
+                    host = torch.randn(n + 1, generator=g).to(dt)
+                    buf = host.to(dev)
+                    x = buf[1:] if it == 1 else buf[:n].clone()  # it 1: a view at an odd offset
+                    ref = host[1:].float().clone() if it == 1 else host[:n].float().clone()
+                    dist.all_reduce(ref, op=op)
+                    oneshot.all_reduce(x, op=op)
+                    got = x.float().cpu()
+                    tol = 1e-5 if dt == torch.float32 else (2e-2 if dt == torch.bfloat16 else 4e-3)
+                    assert torch.allclose(got, ref.to(dt).float(), rtol=tol, atol=tol * ws), (dt, n, op, it)
+                    # every rank holds the same bits
+                    allv = [torch.empty_like(got) for _ in range(ws)]
+                    dist.all_gather(allv, got)
+                    assert all(torch.equal(a, allv[0]) for a in allv), (dt, n, op, it, "ranks differ")
+                    checked += int(n * host.element_size() <= oneshot._MAX_BYTES)
+    inst = oneshot._instances.get("world")
+    assert inst is not None, "one-shot path was not enabled"
+    st = inst.stats()
+    assert st["calls"] >= checked, st
+    oneshot.check_errors()
+    print(f"rank {r} OK checked={checked} stats={st}", flush=True)
+    dist.barrier()
+
+
+def tp(steps):
+    import smdistributed_modelparallel_amd.torch as smp
+    from smdistributed_modelparallel_amd.models import build_gpt
+    from smdistributed_modelparallel_amd.parallel import oneshot
+
+    ws = int(os.environ["WORLD_SIZE"])
+    dev = torch.device("cuda", 0)
+    smp.init({"tensor_parallel_degree": ws, "ddp": True, "bf16": False, "microbatches": 1})
+    torch.manual_seed(5)
+    kw = dict(num_layers=2, hidden_size=256, num_attention_heads=4, attention_head_size=64, intermediate_size=1024,
+              vocab_size=512, num_positions=128)
+    with smp.model_creation(tensor_parallelism=True, dtype=torch.float32):
+        net = build_gpt("gpt2-small", dropout=0.0, **kw)
+    model = smp.DistributedModel(net)
+    opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.05))
+
+    @smp.step
+    def train(model, ids):
+        loss, _ = model((ids, None, None, None, ids))
+        model.backward(loss)
+        return loss
+
+    g = torch.Generator().manual_seed(11 + smp.rank())
+    losses = []
+    for _ in range(steps):
+        ids = torch.randint(0, kw["vocab_size"], (2, 64), generator=g).to(dev)
+        opt.zero_grad()
+        out = train(model, ids)
+        opt.step()
+        losses.append(float(out.reduce_mean()))
+    calls = sum(i.stats()["calls"] for i in oneshot._instances.values() if i is not None)
+    print(f"rank {smp.rank()} OK losses={','.join(f'{v:.6f}' for v in losses)} oneshot_calls={calls}", flush=True)
+    smp.barrier()
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "kernel":
+        kernel()
+    else:
+        tp(int(sys.argv[2]))
