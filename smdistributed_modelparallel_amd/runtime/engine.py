@@ -514,6 +514,8 @@ class PipelineEngine:
 
     def _dispatch_impl(self, src, stubbed, tensors):
         kind = stubbed[0]
+        if kind in ("fwd", "bwd") and stubbed[2] == 0 and not self.state.has_uploaded_metrics:
+            self.state.num_hops += 1  # reference server.py:366-368,449-451
         if kind == "fwd":
             self._spawn(self._exec_fwd, stubbed[2], "fwd", src, stubbed, tensors)
         elif kind == "res":

@@ -318,16 +318,35 @@ class ModuleManager:
                             dict(self._exec_times), dict(self._memory))
 
     # ------------------------------------------------------------- metrics
-    def get_metrics(self, model):
-        parts = defaultdict(int)
-        mods = defaultdict(int)
-        for m in model.modules():
-            p = self.get_partition(m)
-            mods[p] += 1
+    def get_metrics(self, model, pp_size):
+        """Partition metrics (reference `module_manager.py:1337-1392`): parameter bytes and the
+        fraction of traced modules per pipeline device, and the forward communication volume
+        (MB) -- traced input + output bytes of every module whose device differs from its
+        parent's, found by a walk of the module tree from the main module."""
+        var_size = [0] * pp_size
+        module_fraction = [0.0] * pp_size
+        traced = [m for m in model.modules() if m in self._output_sizes]
+        for m in traced:
+            dev = self.get_partition(m)
+            if dev is None:
+                continue
+            module_fraction[dev] += 1
             for prm in m.parameters(recurse=False):
-                parts[p] += prm.numel()
-        total = max(1, sum(mods.values()))
-        return {
-            "params_per_device": dict(parts),
-            "module_fraction_per_device": {k: v / total for k, v in mods.items()},
-        }
+                var_size[dev] += prm.numel() * prm.element_size()
+        if traced:
+            module_fraction = [x / len(traced) for x in module_fraction]
+        comm = 0
+        level = [model]
+        while level:
+            nxt = []
+            for node in level:
+                pdev = self.get_partition(node)
+                for child in node.children():
+                    cdev = self.get_partition(child)
+                    if cdev is None:
+                        continue
+                    if cdev != pdev:
+                        comm += self._input_sizes.get(child, 0) + self._output_sizes.get(child, 0)
+                    nxt.append(child)
+            level = nxt
+        return var_size, module_fraction, comm / 1e6

@@ -80,6 +80,8 @@ class PTModelParallelState:
         self.transport = None
         self.p2p_mode = "cpu"
         self.sdp = None
+        self.num_hops = 0  # execution requests received for microbatch 0 before the metrics upload
+        self.has_uploaded_metrics = False
         self._lock = threading.RLock()
 
     # ----------------------------------------------------------------- device

@@ -13,8 +13,10 @@ import torch
 
 from ..ops.linear import bump_weight_epoch
 
+from ..backend.collectives import CommGroup
 from ..backend.exceptions import DistributedModelNotWrappedError, SMPInvalidArgumentError
 from ..backend.logger import get_logger
+from ..backend.metrics import upload_metrics_to_studio
 from ..backend.split import StepOutput, TensorSplitter
 from .state_mod import state
 
@@ -98,10 +100,31 @@ class StepFunction:
         if core.pp_size() > 1 and state.model.partitioned:
             state.engine.after_step(self, time.perf_counter() - t0)
         state.step_count += 1
+        if state.model.partitioned:
+            self._upload_metrics_once()
         self.memory_metrics.record(state.step_count)
         if outputs is None:
             return None
         return StepOutput(outputs)
+
+    def _upload_metrics_once(self):
+        """Partition metrics, published once per job from rank 0 (reference `step.py:295-311`)."""
+        if state.has_uploaded_metrics:
+            return
+        state.has_uploaded_metrics = True
+        # parameter bytes per device from the owning stage (remote parameters hold no storage here)
+        local_bytes = sum(p.numel() * p.element_size() for _, p in state.model.local_named_parameters())
+        per_stage = state.comm.allgather((state.num_hops, local_bytes), CommGroup.PP_GROUP)
+        hops = sum(h for h, _ in per_stage)
+        if state.core.rank() == 0:
+            pp = state.core.pp_size()
+            _, fraction, comm_vol = state.module_manager.get_metrics(state.model.get_module(), pp)
+            var_size = [b for _, b in per_stage]
+            metrics = {"total_communication_volume(MB)": round(comm_vol, 2), "num_hops_between_devices": hops}
+            for i in range(pp):
+                metrics[f"parameter_count_on_dev_{i}"] = var_size[i]
+                metrics[f"module_fraction_on_dev_{i}"] = fraction[i]
+            upload_metrics_to_studio(metrics)
 
     def run_microbatch(self, mb, mb_args, mb_kwargs):
         """Executes the user function on one microbatch (called by the engine)."""

@@ -206,3 +206,18 @@ def test_partition_file_save_and_load(tmp_path):
     assert all("OK save" in o for o in outs)
     outs = run_workers("partition_file", 2, ["load", path], timeout=120)
     assert all("OK load" in o for o in outs)
+
+
+def test_pp2_auto_partition_metrics_published(tmp_path):
+    """Partition metrics published once from rank 0 (reference `step.py:295-311`): JSON-lines
+    file and Prometheus textfile sinks."""
+    jf, pf = tmp_path / "metrics.jsonl", tmp_path / "metrics.prom"
+    _run(2, 2, 1, 2, auto=1, steps=2, env={"SMP_METRICS_FILE": str(jf), "SMP_METRICS_PROMETHEUS_FILE": str(pf)})
+    recs = [json.loads(line) for line in jf.read_text().splitlines()]
+    assert len(recs) == 1  # once per job, rank 0 only
+    m = recs[0]["metrics"]
+    assert m["num_hops_between_devices"] > 0 and m["total_communication_volume(MB)"] > 0
+    assert m["parameter_count_on_dev_0"] > 0 and m["parameter_count_on_dev_1"] > 0
+    assert abs(m["module_fraction_on_dev_0"] + m["module_fraction_on_dev_1"] - 1.0) < 1e-6
+    prom = pf.read_text()
+    assert "smp_num_hops_between_devices" in prom and "smp_total_communication_volume_mb" in prom
