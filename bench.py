@@ -101,6 +101,7 @@ def main():
     import smdistributed_modelparallel_amd.torch as smp
     from smdistributed_modelparallel_amd.models import GPT_CONFIGS, build_gpt, gpt_inputs
     from smdistributed_modelparallel_amd.models.gpt import train_flops_per_token
+    from smdistributed_modelparallel_amd.ops.attention import FLASH_HEAD_DIMS
 
     world = int(os.environ.get("WORLD_SIZE", 1))
     cfg = {
@@ -219,7 +220,7 @@ def main():
                 "parallelism": par,
                 "micro_batch_per_gpu": args.mbs,
                 "microbatches": args.microbatches,
-                "flash_attention": (not args.no_flash) and mc["attention_head_size"] in (64, 128),
+                "flash_attention": (not args.no_flash) and mc["attention_head_size"] in FLASH_HEAD_DIMS,
                 "dropout": args.dropout,
                 "gemm_selection": "tunableop" if tmode != "off" else "heuristic",
             },

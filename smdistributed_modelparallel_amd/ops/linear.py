@@ -273,6 +273,48 @@ def _wgrad_accumulate(g, dy2, x2):
     _wgrad_run(method, g, dy2, x2)
 
 
+# Weight gradients on a side HIP stream (opt-in, SMP_WGRAD_STREAM=1): dW = dY^T X is off the
+# backward's critical path (nothing in the step reads it before the reducer / optimizer), so
+# it can run concurrently with the next input-gradient GEMMs, attention backward and the
+# memory-bound LayerNorm / GeLU kernels, filling the issue slots and CUs they leave idle.
+# Every consumer of gradients first calls wgrad_sync() (the reducer before a bucket launch
+# and fp32 fold, the step function after the backward), which orders the current stream
+# after all weight-gradient work issued so far.
+_WGRAD_STREAM = os.environ.get("SMP_WGRAD_STREAM", "0") == "1"
+_SIDE = {}
+_PENDING = [False]
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev.index)
+    if s is None:
+        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev, priority=0)
+    return s
+
+
+def wgrad_sync():
+    """Order the current stream after every side-stream weight gradient issued so far."""
+    if _PENDING[0]:
+        cur = torch.cuda.current_stream()
+        for s in _SIDE.values():
+            if s.device == cur.device:
+                cur.wait_stream(s)
+        _PENDING[0] = False
+
+
+def _wgrad_async(g, dy2, x2):
+    cur = torch.cuda.current_stream()
+    side = _side_stream(dy2.device)
+    side.wait_stream(cur)  # dY and X are complete
+    with torch.cuda.stream(side):
+        _wgrad_accumulate(g, dy2, x2)
+    # the caching allocator must not hand these blocks to main-stream work before the
+    # side stream has read them
+    dy2.record_stream(side)
+    x2.record_stream(side)
+    _PENDING[0] = True
+
+
 def _fusable(w):
     g = w.grad
     return (getattr(w, "_smp_fused_grad", False) and g is not None and g.dtype == w.dtype and g.shape == w.shape
@@ -305,7 +347,10 @@ class _LinearWGradAccum(torch.autograd.Function):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the
                 # weight's AccumulateGrad node (a no-op), so post-accumulate-grad hooks -- the
                 # reducers' bucket-ready signals -- fire exactly once, after this write
-                _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]))
+                if _WGRAD_STREAM and dy2.is_cuda:
+                    _wgrad_async(w.grad, dy2, x.reshape(-1, x.shape[-1]))
+                else:
+                    _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]))
             else:
                 # grad slot re-bound/removed since forward: hand the gradient to autograd
                 return dx, dy2.t().mm(x.reshape(-1, x.shape[-1])), db
