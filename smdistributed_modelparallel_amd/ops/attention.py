@@ -169,10 +169,16 @@ def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, t
                      window=window, training=training, use_flash=use_flash, mask_value=mask_value)
 
 
-# Score elements per materialised chunk.  On MI355X (torch 2.10 + ROCm 7), the backward of the
-# strided batched score GEMMs faulted with an illegal address at b*h*sq*sk = 2^28 (GPT-J 6B
-# head dim 256 at b4 s2048: tools/gptj_isolate.py attn_torch); b1 (2^26) runs.  Chunking over
-# the batch keeps every GEMM at a verified size and bounds the [b, h, sq, sk] score memory.
+# Score elements per materialised chunk.  Root cause of the round-1 GPT-J fault
+# (profiles/r2/gptj_fault_root_cause.md): torch's bundled hipBLASLt picks a stream-K solution
+# (Custom_Cijk_Alik_Bljk_..._SK3_..._MT256x256x64_..._shortname0_gfx950) for the batched
+# "A @ B^T" product [bh, s, s] x [bh, d, s]^T -> [bh, s, d], and that kernel faults from
+# bh = 32, s = 2048, d = 256 (A = 2^27 elements); the same product with B contiguous
+# [bh, s, d] ("A @ B") runs at every size tried (up to 2^28).  That layout arises when the
+# score GEMM's K^T operand is a materialised copy (packed-QKV views); this path feeds the GEMMs
+# contiguous [b, h, s, d] q/k/v, so every score GEMM and its backward run as NN / TN / "Q K^T
+# on a K view" (tests/test_attention_chunking.py checks the layouts).  Chunking over the
+# batch additionally bounds the [b, h, sq, sk] score memory.
 _MAX_SCORE_ELEMS = 1 << 26
 
 

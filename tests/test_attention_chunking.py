@@ -59,3 +59,29 @@ def test_checkpoint_attentions_saves_no_scores_and_matches(monkeypatch):
         torch.testing.assert_close(g, r, rtol=1e-5, atol=1e-6)
     assert any(sh[-2:] == (s, s) for sh in saved_ref)
     assert not any(len(sh) == 4 and sh[-2:] == (s, s) for sh in saved_ck)
+
+
+def test_materialised_gemm_layouts_avoid_faulting_nt_product():
+    """Regression for the GPT-J illegal address (profiles/r2/gptj_fault_root_cause.md): no
+    batched GEMM of the materialised path (fwd + bwd) multiplies a score-sized [bh, sq, sk]
+    operand by a TRANSPOSED view of a contiguous [bh, d, sk] tensor -- the layout whose
+    hipBLASLt stream-K solution faults on MI355X."""
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    b, s, h, d = 2, 32, 4, 16
+    bad = []
+
+    class Spy(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            if func in (torch.ops.aten.bmm.default, torch.ops.aten.baddbmm.default):
+                a, bm = (args[0], args[1]) if func == torch.ops.aten.bmm.default else (args[1], args[2])
+                if a.shape[-1] == s and a.shape[-2] == s and bm.shape[-1] == d and bm.stride(-1) != 1:
+                    bad.append((tuple(a.shape), tuple(bm.shape), tuple(bm.stride())))
+            return func(*args, **(kwargs or {}))
+
+    for causal in (True, False):
+        q, k, v = (torch.randn(b, s, h, d, requires_grad=True) for _ in range(3))
+        with Spy():
+            o = A.attention(q, k, v, causal=causal, use_flash=False)
+            o.backward(torch.ones_like(o))
+    assert not bad, bad
