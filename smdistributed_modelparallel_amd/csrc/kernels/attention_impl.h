@@ -340,6 +340,18 @@ __device__ __forceinline__ void dma_tile(uint16_t* lds, const uint16_t* base, in
   constexpr int CPR = D / 8, RPI = 64 / CPR, NI = BN / RPI;  // chunks/row, rows/instr, instrs/tile
   static_assert(NI % (kThreads / 64) == 0, "instructions split evenly over the waves");
   const int rl = lane / CPR, pc = lane % CPR;
+  if (row0 + BN <= sk && ss < (1 << 24)) {
+    // whole tile in range (wave-uniform): scalar tile base + loop-invariant lane offsets
+    const uint16_t* tb = base + static_cast<int64_t>(row0) * ss;
+#pragma unroll
+    for (int i = 0; i < NI / (kThreads / 64); ++i) {
+      const int rb = (wave * (NI / (kThreads / 64)) + i) * RPI;
+      const int r = rb + rl;
+      const int lc = (swz<D>(r, pc) - r * D) >> 3;
+      lds_dma16_sv(tb, static_cast<uint32_t>((r * static_cast<int>(ss) + lc * 8) * 2), lds + rb * D);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < NI / (kThreads / 64); ++i) {
     const int rb = (wave * (NI / (kThreads / 64)) + i) * RPI;
@@ -376,7 +388,9 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   __shared__ __attribute__((aligned(16))) uint16_t sQ[QLDS ? BM * DS : 8];
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
   __shared__ int sFlag;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index as a scalar: every wave-derived tile condition (causal / window / edge) then
+  // branches on SGPRs instead of being if-converted into per-lane selects on every tile
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
   int tile;
@@ -598,7 +612,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * DS];
   __shared__ __attribute__((aligned(16))) float sL[BQ], sDl[BQ];
   const AttnParams& p = P.f;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index as a scalar: every wave-derived tile condition (causal / window / edge) then
+  // branches on SGPRs instead of being if-converted into per-lane selects on every tile
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hh = lane >> 5;
   int kb;
   int64_t bh;
@@ -782,7 +798,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
   __shared__ int sFlag;
   const AttnParams& p = P.f;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index as a scalar: every wave-derived tile condition (causal / window / edge) then
+  // branches on SGPRs instead of being if-converted into per-lane selects on every tile
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
   int tile;

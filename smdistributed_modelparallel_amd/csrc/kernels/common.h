@@ -138,6 +138,22 @@ __device__ __forceinline__ void lds_dma16(const void* src, const void* lds_wave_
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
 
+// Same, saddr form: scalar 64-bit base + 32-bit per-lane byte offset.  Interior tiles use
+// this so the only per-lane address term is loop-invariant (no 64-bit row * stride multiply
+// and add per load per tile).
+__device__ __forceinline__ void lds_dma16_sv(const void* sbase, uint32_t voff_bytes, const void* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)lds_wave_base)));
+  const uint64_t b = reinterpret_cast<uint64_t>(sbase);
+  // (readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends
+  // into the high word)
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b >> 32)));
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b)));
+  const uint64_t sb = (static_cast<uint64_t>(hi) << 32) | static_cast<uint64_t>(lo);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff_bytes), "s"(sb), "s"(lds)
+               : "memory", "m0");
+}
+
 }  // namespace smpk
 
 #define SMPK_CHECK(expr)                                                      \
