@@ -235,6 +235,8 @@ class DistributedModel(nn.Module):
             patch_module_forwards(self)
             state.transport.warmup(state.core.get_pp_group())
         self.partitioned = True
+        if state.core.rank() == 0 and state.core.pp_size() > 1:
+            self.display_partition()  # reference model.py:709-710
         if self._deferred_load is not None:
             self.load_state_dict(self._deferred_load["model"], **self._deferred_load.get("kwargs", {}))
             self._deferred_load = None
@@ -736,9 +738,49 @@ class DistributedModel(nn.Module):
                                      same_partition_load=same_partition_load)
 
     def display_partition(self):
+        """Log the truncated partition tree (reference `model.py:668-701`): a breadth-first
+        walk that stops descending once a subtree lives on a single partition, then (TP > 1)
+        the tensor-parallel distributed modules.  Returns the logged lines."""
+        from collections import deque
+
+        from ..nn.transformer import DistributedModule
+
         mm = state.module_manager
-        for n, m in self.module.named_modules():
-            logger.info(f"{n or 'main'}: partition {mm.get_partition(m)}")
+        parts = {}
+
+        def collect(m):  # partitions used anywhere in m's subtree
+            ps = {mm.get_partition(m)}
+            for c in m.children():
+                ps |= collect(c)
+            parts[m] = ps
+            return ps
+
+        collect(self.module)
+        lines = ["Partition assignments:"]
+        queue, seen = deque([self.module]), set()
+        while queue:
+            m = queue.popleft()
+            if m in seen:
+                continue
+            seen.add(m)
+            lines.append(f"{mm.get_module_name(m) or 'main'}: {mm.get_partition(m)}")
+            if len(parts[m]) > 1:
+                queue.extend(m.children())
+        if state.cfg is not None and state.cfg.tensor_parallel_degree > 1:
+            lines.append("Tensor-parallel distributed modules:")
+            queue, seen = deque([self.module]), set()
+            while queue:
+                m = queue.popleft()
+                if m in seen:
+                    continue
+                seen.add(m)
+                if isinstance(m, DistributedModule):
+                    lines.append(mm.get_module_name(m))
+                else:
+                    queue.extend(m.children())
+        for line in lines:
+            logger.info(line)
+        return lines
 
     def load_saved_partition(self, partition_info):
         state.module_manager.load_partition(partition_info)

@@ -221,3 +221,12 @@ def test_pp2_auto_partition_metrics_published(tmp_path):
     assert abs(m["module_fraction_on_dev_0"] + m["module_fraction_on_dev_1"] - 1.0) < 1e-6
     prom = pf.read_text()
     assert "smp_num_hops_between_devices" in prom and "smp_total_communication_volume_mb" in prom
+
+
+def test_display_partition_truncated_tree():
+    """display_partition walks the module tree breadth-first and stops at subtrees held by a
+    single partition (reference model.py:668-701)."""
+    outs = run_workers("pp_gpt", 2, [2, 1, 2, "interleaved", 0, 1, json.dumps({"display_partition": True})],
+                       timeout=200)
+    assert all("OK" in o for o in outs)
+    assert "DISPLAY main: 0" in outs[0]

@@ -167,6 +167,12 @@ def main():
         assert st["offloaded_bytes"] > 0 and st["loaded_bytes"] == st["offloaded_bytes"], st
         if extra.get("expect_task_prefetch"):
             assert st["task_prefetches"] > 0, st
+    if extra.get("display_partition") and smp.rank() == 0:
+        lines = model.display_partition()
+        assert lines[0] == "Partition assignments:" and any("seq_layers" in x for x in lines), lines
+        # a subtree held by one partition is not expanded: no layer internals are listed
+        assert not any(".attention" in x or "/attention" in x for x in lines), lines
+        print("\n".join("DISPLAY " + x for x in lines[1:]), flush=True)
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
 
