@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kT, 1) void wgrad_kernel(const uint16_t* __restrict
   const int n0 = tn * TM, k0 = tk * TN;
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
   const int hh = lane >> 5;
 
@@ -255,6 +255,19 @@ __device__ __forceinline__ void stage_glds(uint16_t* lds, const uint16_t* src, i
   constexpr int RPW = TKS / W;
   static_assert(RPW >= 2 && RPW % 2 == 0, "each wave stages whole row pairs");
   const int pc = lane & 31, half = lane >> 5;
+  if (ld < (1 << 24)) {
+    // saddr form: `src` (the tile base) is wave-uniform, the per-lane byte offset is
+    // loop-invariant -- no 64-bit address arithmetic per load per tile
+#pragma unroll
+    for (int i = 0; i < RPW / 2; ++i) {
+      const int r = RPW * wave + 2 * i + half;
+      const int g = ((r & 3) << 2) | ((r >> 2) & 3);
+      int c = pc ^ g;
+      c = c < vc ? c : vc - 1;
+      lds_dma16_sv(src, static_cast<uint32_t>((r * static_cast<int>(ld) + c * 8) * 2), lds + (RPW * wave + 2 * i) * RW);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < RPW / 2; ++i) {
     const int r = RPW * wave + 2 * i + half;
@@ -290,7 +303,7 @@ __global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t*
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
   constexpr int W = 2 * WN, NJ = 8 / WN, WCOLS = 32 * NJ;
   constexpr int L = 2 * (TKS / W / 2);  // DMA instructions per wave per tile (A and B)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int hh = lane >> 5;
   int aLo[4], aHi[4], bLo[NJ], bHi[NJ];
@@ -464,7 +477,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const uint16_t* __rest
   const int n0 = tn * TM, k0 = tk * TN;
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   int aOff0, aOff1, bOff;
   {
