@@ -482,10 +482,68 @@ class DistributedOptimizer:
     def load_local_fp16_state_dict(self, sd):
         self.loss_scaler.load_state_dict(sd["loss_scaler"])
 
+    # torch optimizer-state keys of the reference's wrapped optimizers -> our domain buffers
+    _REF_KEYS = {"m": ("exp_avg", "momentum_buffer"), "v": ("exp_avg_sq", "sum")}
+
+    @staticmethod
+    def is_reference_format(sd):
+        """A reference `smp` optimizer state: the wrapped torch optimizer's state_dict (partial:
+        `_smp_is_partial`, `optimizers/optimizer.py:125-200`), optionally inside the fp16 wrapper
+        dict (`optimizer_state_dict` + `fp32_from_fp16`, `backcompat_opt.py:136-154`)."""
+        return isinstance(sd, dict) and ("optimizer_state_dict" in sd or ("state" in sd and "param_groups" in sd))
+
+    def _from_reference_format(self, sd):
+        """Reference-format state -> this optimizer's per-parameter format.  Parameter indices
+        are the positions in the optimizer's parameter groups (reference `param_name_to_index`),
+        so the model and the optimizer's groups must be built as in the saving job."""
+        masters = sd.get("fp32_from_fp16")
+        inner = sd["optimizer_state_dict"] if "optimizer_state_dict" in sd else sd
+        i2n = self.param_index_to_name()
+        names = {p: n for n, p in state.model.module.named_parameters()}
+        master_of = {}
+        if masters is not None:
+            if len(masters) != len(self._orig_param_groups):
+                raise SMPInvalidArgumentError("reference optimizer state: fp32_from_fp16 groups do not match the "
+                                              "optimizer's parameter groups")
+            for g, ms in zip(self._orig_param_groups, masters):
+                lowp = [p for p in g["params"] if p.dtype in (torch.float16, torch.bfloat16)]
+                if len(lowp) != len(ms):
+                    raise SMPInvalidArgumentError("reference optimizer state: fp32_from_fp16 does not match the "
+                                                  "low-precision parameters of a group")
+                for p, m in zip(lowp, ms):
+                    master_of[names[p]] = m
+        params = {}
+        steps = [0] * len(self._orig_param_groups)
+        by_name = {n: p for n, p in state.model.module.named_parameters()}
+        gidx = self._group_index_of()
+        for idx, st in inner.get("state", {}).items():
+            name = i2n.get(int(idx))
+            if name is None or not st:
+                continue  # not a parameter of this optimizer / state kept on another TP rank
+            p = by_name[name]
+            n = p.numel()
+            piece = {"lo": 0, "hi": n}
+            for ours, theirs in self._REF_KEYS.items():
+                for k in theirs:
+                    if isinstance(st.get(k), torch.Tensor):
+                        piece[ours] = st[k].detach().reshape(-1).float().cpu()
+                        break
+            mt_ = master_of.get(name)
+            piece["master"] = (mt_ if mt_ is not None else p.detach()).reshape(-1).float().cpu()
+            params[name] = {"numel": n, "pieces": [piece]}
+            if "step" in st:
+                steps[gidx[p]] = max(steps[gidx[p]], int(float(st["step"])))
+            elif "m" in piece:  # torch SGD keeps no step: a momentum buffer means >= 1 step taken
+                steps[gidx[p]] = max(steps[gidx[p]], 1)
+        return {"format": "smp_amd_per_param_v1", "kind": self.kind, "params": params, "step_count": steps,
+                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in inner.get("param_groups", [])]}
+
     def load_state_dict(self, sd):
         if not self._built:
             self._deferred_load = sd
             return
+        if self.is_reference_format(sd):
+            sd = self._from_reference_format(sd)
         self.load_local_optimizer_state_dict(sd)
         if "fp16_state" in sd:
             self.load_local_fp16_state_dict(sd["fp16_state"])

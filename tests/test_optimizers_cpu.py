@@ -19,3 +19,12 @@ def test_lamb_chunk_table_covers_pieces(monkeypatch):
     assert rows[:3] == [(0, 0, 5), (0, 5, 10), (0, 10, 12)] and rows[3] == (1, 12, 13)
     assert sum(e - s for _, s, e in rows) == 12 + 1 + 11
     assert all(e - s <= 5 for _, s, e in rows)
+
+
+def test_reference_format_optimizer_state_import():
+    """Reference partial optimizer states (torch state_dict + `_smp_is_partial`, and the fp16
+    wrapper with fp32_from_fp16 masters) load into DistributedOptimizer and training continues
+    on the reference trajectory."""
+    for kind, prec in (("adamw", "fp32"), ("sgd", "fp32"), ("adamw", "bf16")):
+        outs = run_workers("ref_opt_import", 1, [kind, prec], timeout=120)
+        assert f"OK {kind} {prec}" in outs[0], outs
