@@ -789,7 +789,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 // ========================================================================= dQ
 // Block = 4 waves x 32 queries (query on the lane: S^T = K Q^T, dP^T = V dO^T); K/V tiles
 // of 64 keys; dQ^T += K^T dS^T with K^T from transposed LDS reads.
-template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
+// FD (fused delta): the block computes delta = rowsum(dO o O) of its own query rows from the dO
+// fragments it holds anyway plus one read of the O rows, and publishes it for the dK/dV kernel
+// launched after it -- no separate delta pass over O and dO.
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool FD = false>
 __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(AttnBwdParams P) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr int NSPLIT = DkdvSplit<D>::v, DO = D / NSPLIT;  // dQ columns per block
@@ -838,7 +841,25 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   const float sl2 = p.scale * kLog2e;
   const float inv_scale = 1.f / p.scale;
   const float s_init = -lse * kLog2e / sl2;
-  const float dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
+  float dl;
+  if constexpr (FD) {
+    // lane (r, hh) holds elements [16 t + 8 hh, +8) of dO row qrow: the matching O elements,
+    // a lane-local partial dot product, and the other half-row from lane ^ 32
+    const uint16_t* Orow = static_cast<const uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh;
+    float part = 0.f;
+    if (qrow < sq) {
+#pragma unroll
+      for (int t = 0; t < D / 16; ++t) {
+        const typename MF<T>::e8 o8 = ld8<T>(Orow + static_cast<int64_t>(qrow) * p.o_ss + 16 * t + 8 * hh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part = fmaf(static_cast<float>(df[t][j]), static_cast<float>(o8[j]), part);
+      }
+    }
+    dl = part + xor32(part);
+    if (col0 == 0 && hh == 0 && qrow < sq) P.delta[bh * p.sq + qrow] = dl;
+  } else {
+    dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
+  }
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
   const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 1) >> 1);
   const uint32_t thr16 = p.drop_thr << 16;
@@ -970,12 +991,27 @@ int launch_fwd_v(const AttnParams& p, hipStream_t s) {
   return static_cast<int>(hipGetLastError());
 }
 
+// SMP_ATTN_FUSED_DELTA=0: separate delta kernel, then dK/dV, then dQ (A/B switch)
+inline bool attn_fused_delta() {
+  static const bool v = [] {
+    const char* e = getenv("SMP_ATTN_FUSED_DELTA");
+    return e == nullptr || e[0] != '0';
+  }();
+  return v;
+}
+
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_bwd_v(const AttnBwdParams& p, hipStream_t s) {
-  const int64_t rows = p.f.b * p.f.h * p.f.sq;
-  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
   const unsigned gk = static_cast<unsigned>(((p.f.sk + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
   const unsigned gq = static_cast<unsigned>(((p.f.sq + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
+  if (attn_fused_delta()) {
+    // dQ first: it writes delta for the dK/dV kernel (same stream)
+    attn_bwd_dq_kernel<T, D, C, DR, BI, true><<<gq, kThreads, 0, s>>>(p);
+    attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
+    return static_cast<int>(hipGetLastError());
+  }
+  const int64_t rows = p.f.b * p.f.h * p.f.sq;
+  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
   attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
   attn_bwd_dq_kernel<T, D, C, DR, BI><<<gq, kThreads, 0, s>>>(p);
   return static_cast<int>(hipGetLastError());
