@@ -76,6 +76,7 @@ class _Unit:
         self.shard_start = 0  # offset of this unit's shard inside the rank's flat buffers
         self.full = None
         self.work = None
+        self.mid = None  # hierarchical gather: cross-node stage output kept until the gather ends
         self.full_grad = None
         self.ready = 0
         self.expected = sum(1 for p in params if p.requires_grad)
@@ -147,6 +148,20 @@ class ShardedDataParallel:
         self.R = replica_size
         self.device = device
         self.rank_in_shard = dist.get_rank(shard_group) if shard_group is not None else 0
+        # Hierarchical all-gather (sdp_hierarchical_allgather, reference C22 / DeepSpeed
+        # zero2d_hierarchy_allgather): when the shard group spans several nodes, parameters
+        # are gathered cross-node first (1/L of the bytes on the slow links), then over xGMI
+        # inside the node; gradients are reduce-scattered in the reverse order.  The rank at
+        # (node n, local l) owns slice l * N + n of every unit, which makes both stages plain
+        # all_gather_into_tensor / reduce_scatter_tensor calls with no re-ordering copy.
+        self.intra = state.pgs.shard_intra
+        self.inter = state.pgs.shard_inter
+        self.hier = self.intra is not None and self.inter is not None
+        if self.hier:
+            n_nodes = dist.get_world_size(self.inter)
+            self.slot = dist.get_rank(self.intra) * n_nodes + dist.get_rank(self.inter)
+        else:
+            self.slot = self.rank_in_shard
         total = sum(p.numel() for p in model.module.parameters())
         # at least ~16 units so gathers pipeline and memory actually drops
         self.unit_cap = int(min(cfg.sdp_reduce_bucket_size, max(total // 16, 1)))
@@ -267,7 +282,7 @@ class ShardedDataParallel:
             full[o:o + t.numel()].copy_(t.reshape(-1))
         if broadcast and state.core.dp_size() > 1 and state.pgs.dp is not None:
             dist.broadcast(full, dist.get_global_rank(state.pgs.dp, 0), group=state.pgs.dp)
-        lo = self.rank_in_shard * u.shard_numel
+        lo = self.slot * u.shard_numel
         self.flat.shard(u).copy_(full[lo:lo + u.shard_numel])
 
     def _make_pieces(self):
@@ -275,7 +290,7 @@ class ShardedDataParallel:
         unit's per-param-group segments (so one domain = one hyper-parameter set)."""
         self.flat.buckets = []
         for u in self.units:
-            lo, hi = self.rank_in_shard * u.shard_numel, (self.rank_in_shard + 1) * u.shard_numel
+            lo, hi = self.slot * u.shard_numel, (self.slot + 1) * u.shard_numel
             segs = []
             for p, o, n in zip(u.params, u.offsets, u.numels):
                 g = self._group_of.get(p, 0)
@@ -328,6 +343,15 @@ class ShardedDataParallel:
         if self.group is None:
             full.copy_(shard)
             u.work = None
+        elif self.hier:
+            # cross-node gather of the N slices [l*N, l*N+N) this local rank index owns,
+            # then the node-local gather of those blocks (ordered by local rank)
+            mid = torch.empty(u.shard_numel * dist.get_world_size(self.inter), dtype=u.dtype, device=self.device)
+            dist.all_gather_into_tensor(mid, shard, group=self.inter, async_op=True).wait()
+            u.work = dist.all_gather_into_tensor(full, mid, group=self.intra, async_op=async_op)
+            u.mid = mid
+            if not async_op:
+                u.work = None
         else:
             u.work = dist.all_gather_into_tensor(full, shard, group=self.group, async_op=async_op)
             if not async_op:
@@ -341,6 +365,7 @@ class ShardedDataParallel:
         if u.work is not None:
             u.work.wait()
             u.work = None
+        u.mid = None
         if not u.in_use:
             for p, o, n, shp in zip(u.params, u.offsets, u.numels, u.shapes):
                 p.data = u.full[o:o + n].view(shp)
@@ -360,6 +385,7 @@ class ShardedDataParallel:
         for p in u.params:
             p.data = empty
         u.full = None
+        u.mid = None
         u.in_use = False
         self.live -= u.padded
 
@@ -466,6 +492,14 @@ class ShardedDataParallel:
         fg.mul_(1.0 / (self.num_mb * self.S * self.R))
         if self.group is None:
             self.flat.grad_shard(u).add_(fg)
+        elif self.hier:
+            # node-local reduce-scatter to this local rank's N-slice block, then the
+            # cross-node reduce-scatter of that block to slice l * N + n
+            mid = torch.empty(u.shard_numel * dist.get_world_size(self.inter), dtype=u.dtype, device=self.device)
+            dist.reduce_scatter_tensor(mid, fg, group=self.intra, async_op=True).wait()
+            out = torch.empty(u.shard_numel, dtype=u.dtype, device=self.device)
+            work = dist.reduce_scatter_tensor(out, mid, group=self.inter, async_op=True)
+            self._pending_rs.append((u, out, (fg, mid), work))
         else:
             out = torch.empty(u.shard_numel, dtype=u.dtype, device=self.device)
             work = dist.reduce_scatter_tensor(out, fg, group=self.group, async_op=True)
@@ -538,7 +572,7 @@ class ShardedDataParallel:
                         missing.append(n)
                         continue
                     full[o:o + k].copy_(sd[n].reshape(-1).to(full.device, full.dtype))
-                lo = self.rank_in_shard * u.shard_numel
+                lo = self.slot * u.shard_numel
                 self.flat.shard(u).copy_(full[lo:lo + u.shard_numel])
                 self._release(u, force=True)
             for n, b in self.root.named_buffers():
@@ -554,7 +588,7 @@ class ShardedDataParallel:
         return {
             "_smp_zero2d": True,
             "shard_size": self.S,
-            "shard_rank": self.rank_in_shard,
+            "shard_rank": self.slot,  # index of the unit slice held (file model_{slot}.pt)
             "units": [{"names": u.names, "shapes": u.shapes, "numel": u.numel, "padded": u.padded} for u in self.units],
             "shard": self.flat.data.detach().cpu(),
             "buffers": {n: b.detach().cpu() for n, b in self.root.named_buffers() if b is not None},
@@ -588,7 +622,8 @@ def _flatten(obj):
 
 # ---------------------------------------------------------------- checkpoints
 def _shard_rank():
-    return state.sdp.rank_in_shard if state.sdp is not None else 0
+    # files are named by the slice they hold, so flat and hierarchical layouts load each other
+    return state.sdp.slot if state.sdp is not None else 0
 
 
 def _writes():

@@ -35,6 +35,8 @@ class ProcessGroups:
         self.cpu_tp = None  # gloo twin of the TP group (object/CPU traffic)
         self.shard = None  # sharded data parallel: S consecutive ranks
         self.shard_replica = None  # same shard index across the dp / S replicas
+        self.shard_intra = None  # hierarchical sharded DP: this node's ranks of the shard group
+        self.shard_inter = None  # ... and the same local rank on the shard group's other nodes
 
     def get(self, group):
         return {
@@ -132,6 +134,22 @@ class PTModelParallelState:
                     g = dist.new_group(ranks, backend=backend)
                     if me in ranks:
                         self.pgs.shard_replica = g
+            L = core.local_size()
+            if self.cfg.zero2d_config_dict().get("zero_optimization", {}).get("zero2d_hierarchy_allgather") \
+                    and 1 < L < S and S % L == 0:
+                # shard spans S / L nodes: node-local and cross-node sub-groups of every
+                # shard group (parallel/sharded_dp.py: two-level gather / reduce-scatter)
+                for i in range(n // S):
+                    for nd in range(S // L):
+                        ranks = list(range(i * S + nd * L, i * S + (nd + 1) * L))
+                        g = dist.new_group(ranks, backend=backend)
+                        if me in ranks:
+                            self.pgs.shard_intra = g
+                    for lr in range(L):
+                        ranks = list(range(i * S + lr, (i + 1) * S, L))
+                        g = dist.new_group(ranks, backend=backend)
+                        if me in ranks:
+                            self.pgs.shard_inter = g
         if self.use_gpu and core.tp_size() > 1:
             # CPU twin for host-side TP traffic (offload broadcast of host tensors)
             mine = None

@@ -28,6 +28,8 @@ def run_workers(module, world, args=(), timeout=240, env_extra=None):
                    SMP_CONNECT_TIMEOUT="60")
         if env_extra:
             env.update({k: str(v) for k, v in env_extra.items()})
+            if "LOCAL_WORLD_SIZE" in env_extra:  # emulate several nodes of LOCAL_WORLD_SIZE ranks
+                env["LOCAL_RANK"] = str(r % int(env_extra["LOCAL_WORLD_SIZE"]))
         procs.append(subprocess.Popen([sys.executable, "-m", f"tests.workers.{module}", *map(str, args)], cwd=ROOT,
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs, failed = [], False

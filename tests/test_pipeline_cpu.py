@@ -126,6 +126,15 @@ def test_ddp_features(mode):
     assert all("OK" in o for o in outs)
 
 
+@pytest.mark.parametrize("hier", [True, False])
+def test_sharded_dp4_hierarchical_allgather_two_nodes(hier):
+    """sdp_hierarchical_allgather with the shard group spanning 2 emulated nodes of 2 ranks:
+    cross-node then node-local gathers (reverse for the reduce-scatter) train exactly like the
+    flat unsharded reference (reference C22, DeepSpeed zero2d_hierarchy_allgather)."""
+    cfg = dict(_SDP, sharded_data_parallel_degree=4, sdp_hierarchical_allgather=hier)
+    _run(4, 1, 1, 2, extra={"cfg": cfg, "expect_hier": hier}, env={"LOCAL_WORLD_SIZE": 2})
+
+
 def test_sharded_dp2_gradient_clipping():
     cfg = dict(_SDP, sharded_data_parallel_degree=2, sdp_gradient_clipping=0.05)
     _run(2, 1, 1, 2, extra={"cfg": cfg, "ref_clip": 0.05})

@@ -157,6 +157,10 @@ def main():
         if d > worst:
             worst, worst_name = d, n
     assert worst < 2e-4, (worst, worst_name if worst > 0 else None)
+    if extra.get("expect_hier") is not None:
+        sdp = smp.state.sdp
+        assert sdp.hier == extra["expect_hier"], (sdp.hier, extra["expect_hier"])
+        print(f"rank {smp.rank()} sharded-DP slot {sdp.slot} hierarchical {sdp.hier}", flush=True)
     if extra.get("expect_replay"):
         eng = smp.state.engine
         assert eng._replay, "schedule was never frozen"
