@@ -9,17 +9,73 @@ allocated with ``to_empty`` on the device and re-initialised by its own
 ``reset_parameters`` (or the module's ``_init_weights`` for HF-style models), non-local
 meta parameters become empty tensors.
 """
+import os
 from contextlib import contextmanager
 
 import torch
+import torch.nn as nn
 
 from ..torch.state_mod import state
+
+# SMP_USE_FLOAT32_INIT=1 (reference `parameter.py:20,45-110`): random initialisers called on a
+# 16-bit CPU parameter run on an fp32 copy that is cast back -- host fp32 RNG kernels are much
+# faster than the 16-bit ones for multi-billion-parameter models built in fp16 / bf16.
+_INIT_FNS = ("normal_", "uniform_", "trunc_normal_", "xavier_uniform_", "xavier_normal_", "kaiming_uniform_",
+             "kaiming_normal_", "constant_", "zeros_", "ones_")
+_PARAM_FNS = ("normal_", "uniform_", "fill_", "zero_")
+
+
+def use_fp32_init():
+    return os.environ.get("SMP_USE_FLOAT32_INIT", "0") not in ("", "0")
+
+
+def _fp32_wrap(fn):
+    def init(tensor, *args, **kwargs):
+        if isinstance(tensor, torch.Tensor) and tensor.dtype in (torch.float16, torch.bfloat16) \
+                and tensor.device.type == "cpu":
+            with torch.no_grad():
+                t32 = tensor.detach().to(torch.float32)
+                fn(t32, *args, **kwargs)
+                tensor.detach().copy_(t32)
+            return tensor
+        return fn(tensor, *args, **kwargs)
+
+    init.__wrapped__ = fn
+    return init
+
+
+@contextmanager
+def fp32_init_scope(enabled=None):
+    """Run nn.init initialisers and Parameter.{normal_,uniform_,fill_,zero_} of 16-bit CPU
+    parameters in fp32 (no-op unless SMP_USE_FLOAT32_INIT is set)."""
+    if enabled is None:
+        enabled = use_fp32_init()
+    if not enabled:
+        yield
+        return
+    saved_init = {n: getattr(nn.init, n) for n in _INIT_FNS if hasattr(nn.init, n)}
+    saved_param = {n: nn.Parameter.__dict__.get(n) for n in _PARAM_FNS}
+    for n, f in saved_init.items():
+        setattr(nn.init, n, _fp32_wrap(f))
+    for n in _PARAM_FNS:
+        setattr(nn.Parameter, n, _fp32_wrap(getattr(torch.Tensor, n)))
+    try:
+        yield
+    finally:
+        for n, f in saved_init.items():
+            setattr(nn.init, n, f)
+        for n, f in saved_param.items():
+            if f is None:
+                delattr(nn.Parameter, n)
+            else:
+                setattr(nn.Parameter, n, f)
 
 
 @contextmanager
 def delay_param_initialization(enabled=True):
     if not enabled:
-        yield
+        with fp32_init_scope():
+            yield
         return
     state.delay_param_initialization_enabled = True
     try:

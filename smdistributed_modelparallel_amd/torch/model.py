@@ -838,11 +838,14 @@ def model_creation(tensor_parallelism=False, dtype=None, distribute_embedding=Fa
     cfg = dict(tp_config)
     if distribute_embedding:
         cfg["distribute_embedding"] = True
+    from ..parallel.delayed_init import fp32_init_scope
+
     try:
-        if mm is not None:
-            with mm.tensor_parallelism(tensor_parallelism, **cfg):
+        with fp32_init_scope(enabled=None if not state.delay_param_initialization_enabled else False):
+            if mm is not None:
+                with mm.tensor_parallelism(tensor_parallelism, **cfg):
+                    yield
+            else:
                 yield
-        else:
-            yield
     finally:
         torch.set_default_dtype(prev_dtype)

@@ -376,3 +376,28 @@ def test_config_legacy_dp_backends():
         ModelParallelConfig({"herring": True})
     c = ModelParallelConfig({"horovod": True})
     assert c.ddp and c.horovod  # Horovod configs run on the native RCCL reducer
+
+
+def test_fp32_init_of_16bit_params(monkeypatch):
+    """SMP_USE_FLOAT32_INIT (reference parameter.py:20,45-110): initialisers of 16-bit CPU
+    parameters run in fp32 and are cast back; patches are removed on exit."""
+    import torch.nn as nn
+
+    import smdistributed_modelparallel_amd.torch as smp
+
+    monkeypatch.setenv("SMP_USE_FLOAT32_INIT", "1")
+    torch.manual_seed(0)
+    ref = nn.Linear(96, 64)
+    with smp.model_creation(dtype=torch.bfloat16):
+        torch.manual_seed(0)
+        lin = nn.Linear(96, 64)
+        torch.manual_seed(1)
+        p = nn.Parameter(torch.empty(32, 32, dtype=torch.bfloat16))
+        p.normal_(0.0, 0.02)
+    torch.manual_seed(1)
+    q = torch.empty(32, 32).normal_(0.0, 0.02)
+    assert lin.weight.dtype == torch.bfloat16
+    assert torch.equal(lin.weight.data, ref.weight.data.bfloat16())
+    assert torch.equal(lin.bias.data, ref.bias.data.bfloat16())
+    assert torch.equal(p.data, q.bfloat16())
+    assert not hasattr(nn.init.normal_, "__wrapped__") and "normal_" not in nn.Parameter.__dict__
