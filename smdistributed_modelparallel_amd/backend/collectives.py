@@ -106,17 +106,21 @@ class CollectiveCommunicator:
 
     def broadcast(self, obj, group=CommGroup.WORLD, is_user_api=False, root=None):
         """Root sends `obj` to every other group member; returns nothing on the root."""
+        # one point-to-point message per member, numbered in the (root, member) sequence that
+        # send / recv_from use: a receiver may take it with recv_from(root) -- the reference's
+        # broadcast + recv_from pairing (`test/backend/test_collectives.py:54-72`) -- or with
+        # recv_broadcast; messages between a pair are matched in program order
         ranks = self._group_ranks(group)
         root = self.core.rank() if root is None else root
-        tid = self.tids.next("bcast", (tuple(ranks), root), is_user_api)
         others = [r for r in ranks if r != root]
-        if others:
-            self.mailbox.broadcast(others, tid, USER_CHANNEL, dumps(obj))
+        if not others:
+            return
+        payload = dumps(obj)
+        for dst in others:
+            self.mailbox.send(dst, self.tids.next("p2p", (root, dst), is_user_api), USER_CHANNEL, payload)
 
     def recv_broadcast(self, root, group=CommGroup.WORLD, is_user_api=False):
-        ranks = self._group_ranks(group)
-        tid = self.tids.next("bcast", (tuple(ranks), root), is_user_api)
-        return loads(self.mailbox.recv(root, tid, self.timeout))
+        return self.recv_from(root, RankType.WORLD_RANK, is_user_api)
 
     def bcast(self, obj, root, group=CommGroup.WORLD, is_user_api=False):
         """Symmetric broadcast: every member calls, the root's object is returned everywhere."""

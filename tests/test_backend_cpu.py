@@ -401,3 +401,13 @@ def test_fp32_init_of_16bit_params(monkeypatch):
     assert torch.equal(lin.bias.data, ref.bias.data.bfloat16())
     assert torch.equal(p.data, q.bfloat16())
     assert not hasattr(nn.init.normal_, "__wrapped__") and "normal_" not in nn.Parameter.__dict__
+
+
+@pytest.mark.parametrize("placement", ["cluster", "spread"])
+def test_object_collectives_all_groups(placement):
+    """smp.broadcast / send / recv_from / allgather / gather / barriers over WORLD, PP, DP and
+    TP on pp2 x tp2 (gloo, 4 ranks), both placements, plus 12 000 in-flight messages."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("obj_comm", 4, [placement], timeout=240)
+    assert all("OBJ_COMM_OK" in o for o in outs)

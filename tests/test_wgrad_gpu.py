@@ -60,7 +60,7 @@ def test_wgrad_kernel_matches_fp32(shape, gdtype):
     err = (g.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < (1e-2 if gdtype == torch.bfloat16 else 1e-5), err
     # explicit split counts give the same sums; accumulate=False overwrites
-    for splits in (1, 3):
+    for splits in (1, 3, 5, 6, 8):
         h = torch.empty(N, K, device="cuda", dtype=torch.float32)
         ext().wgrad_(h, dy, x, False, splits)
         torch.testing.assert_close(h, dy.float().t() @ x.float(), rtol=1e-4, atol=1e-3 * ref.abs().max().item())
