@@ -37,6 +37,9 @@ class DistributedEmbedding(nn.Module):
         self.vocab_parallel = vocab_parallel
         self.skip_allgather = _skip_allgather
         self.output_full_batch = _output_full_batch
+        # TP degree fixed at construction (as for DistributedModule): an embedding built before
+        # smp.init, or outside tensor parallelism, stays whole and never communicates
+        self._tp = tp_size()
         if vocab_parallel:
             self.local_vocab = get_local_channels(num_embeddings)
             self.vocab_start_idx = get_start_pos_for_slicing(num_embeddings)
@@ -57,7 +60,7 @@ class DistributedEmbedding(nn.Module):
             self.weight.normal_(0.0, self.initializer_range)
 
     def forward(self, ids):
-        if tp_size() == 1:
+        if self._tp == 1:
             return F.embedding(ids, self.weight, self.padding_idx)
         b = ids.shape[0]
         full_ids = ids if self.skip_allgather else _allgather(ids, 0)
@@ -75,7 +78,7 @@ class DistributedEmbedding(nn.Module):
 
     def gather_vocab(self, logits):
         """Full-vocabulary logits from vocab-parallel shards."""
-        if tp_size() == 1:
+        if self._tp == 1:
             return logits
         return fused_allgather_for_tp(logits, logits.dim() - 1, merge_shapes=get_merge_shapes(self.num_embeddings))
 

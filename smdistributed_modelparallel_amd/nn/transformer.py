@@ -711,8 +711,12 @@ class DistributedTransformerLMHead(DistributedModule):
         if self.distribute_embedding:
             from .embedding import DistributedEmbedding
 
+            # prescaled batch: every TP rank already holds the same batch -- no id all-gather,
+            # the partial lookups are summed over the TP group (reference `transformer.py:245-253`)
+            pre = _prescaled()
             self.word_embedding = DistributedEmbedding(self.vocab_size, h, initializer_range=self.initializer_range,
-                                                       vocab_parallel=True)
+                                                       vocab_parallel=True, _skip_allgather=pre,
+                                                       _output_full_batch=pre)
         else:
             self.word_embedding = nn.Embedding(self.vocab_size, h, dtype=dtype)
             _normal_init(self.word_embedding, self.initializer_range)
@@ -721,12 +725,24 @@ class DistributedTransformerLMHead(DistributedModule):
             _normal_init(self.position_embedding, self.initializer_range)
         if self.num_token_types > 0:
             self.token_type_embedding = nn.Embedding(self.num_token_types, h, dtype=dtype)
+        if self.distribute_embedding and self._tp > 1 and _prescaled():
+            # prescaled batch: position / token-type embeddings see the whole (identical) batch
+            # on every TP rank and receive the TP-scaled CE gradient -> averaged over the TP
+            # group (reference `transformer.py:280-289` divides their gradients by tp)
+            for m in (getattr(self, "position_embedding", None), getattr(self, "token_type_embedding", None)):
+                if m is not None:
+                    m.weight._smp_scaled_batch = True
         self.dropout = _Dropout(self.embedding_dropout_prob)
         tcfg = {k: cfg[k] for k in DistributedTransformer._KEYS if k in cfg}
         tcfg["_output_full_batch"] = self.distribute_embedding
         self.transformer = DistributedTransformer(**tcfg)
         if self.final_layernorm:
             self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            if self.distribute_embedding and self._tp > 1:
+                # applied to the full TP-group batch, with the TP-scaled CE gradient: averaged
+                # over the TP group like the tensor-parallel weights (scaled-batch divisor)
+                for p in self.layernorm.parameters():
+                    p._smp_scaled_batch = True
         if self.add_lm_head:
             if self.distribute_embedding:
                 self.lm_head_weight_local = None  # tied to the vocab-parallel embedding shard
@@ -784,11 +800,14 @@ class DistributedTransformerLMHead(DistributedModule):
             logits = F.linear(hidden, self.word_embedding.weight)
             if labels is None:
                 return self.word_embedding.gather_vocab(logits)
-            if not _prescaled():
+            if self._tp > 1 and not _prescaled():
                 labels = allgather_for_tp(labels, 0)
             shift_logits = logits[..., :-1, :]
             shift_labels = labels[..., 1:]
-            rows = cross_entropy(shift_logits, shift_labels, vocab_start=self.word_embedding.vocab_start_idx,
+            from .cross_entropy import scale_grad_for_tp
+
+            rows = cross_entropy(scale_grad_for_tp(shift_logits, self._tp), shift_labels,
+                                 vocab_start=self.word_embedding.vocab_start_idx,
                                  group=tp_group() if self._tp > 1 else None, reduction="none")
             return rows.mean(), shift_logits
 

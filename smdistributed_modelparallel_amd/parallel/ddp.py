@@ -21,6 +21,8 @@ cap is sized for ring all-reduce over xGMI (7 x ~153 GB/s links): ~200 MB keeps 
 step long enough to amortise launch latency while leaving >10 buckets of overlap for a
 1.5 B-parameter model.
 """
+import weakref
+
 import torch
 import torch.distributed as dist
 
@@ -57,9 +59,19 @@ class BucketReducer:
 
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
+        # the hook lives on the parameter's C++ autograd meta, which the garbage collector
+        # cannot traverse: a strong reference back to the reducer (-> flat buffer -> params)
+        # would keep a dropped model alive, so the hook holds the reducer weakly
+        ref = weakref.ref(self)
+
+        def on_grad(p):
+            r = ref()
+            if r is not None:
+                r._on_grad(p)
+
         for p in self.flat.params():
             if p.requires_grad:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(p.register_post_accumulate_grad_hook(on_grad))
 
     def remove_hooks(self):
         for h in self._hooks:

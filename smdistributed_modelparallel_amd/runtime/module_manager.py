@@ -6,6 +6,7 @@ simplification, activation-checkpoint configs, trace data, partition load/save).
 reference also keeps its backward-termination bookkeeping here; ours lives in the
 pipeline engine (`runtime/engine.py`), which uses a different (ack-tree) protocol.
 """
+import weakref
 from collections import defaultdict
 from contextlib import contextmanager
 
@@ -53,26 +54,28 @@ class ModuleManager:
 
     def reset(self):
         self._cur_partition = None
-        self._module_partitions = {}
-        self._module_to_name = {}
-        self._name_to_module = {}
-        self._parent = {}
-        self._main = None
+        # modules are held weakly everywhere: a model the user drops is freed without smp.reset
+        # (the reference's leak test had to reset the module manager by hand)
+        self._module_partitions = weakref.WeakKeyDictionary()
+        self._module_to_name = weakref.WeakKeyDictionary()
+        self._name_to_module = weakref.WeakValueDictionary()
+        self._parent = weakref.WeakKeyDictionary()  # child -> weakref(parent)
+        self._main_ref = None
         self._tp_enabled = False
         self._current_tp_config = {}
-        self._tp_modules = set()
-        self._tp_config = {}
-        self._distributed_modules = set()
-        self._ckpt_config = {}
+        self._tp_modules = weakref.WeakSet()
+        self._tp_config = weakref.WeakKeyDictionary()
+        self._distributed_modules = weakref.WeakSet()
+        self._ckpt_config = weakref.WeakKeyDictionary()
         self.partition_loaded = False
         self.clear_trace()
 
     def clear_trace(self):
-        self._exec_order = []
-        self._input_sizes = {}
-        self._output_sizes = {}
-        self._exec_times = {}
-        self._memory = {}
+        self._exec_order = []  # weakrefs
+        self._input_sizes = weakref.WeakKeyDictionary()
+        self._output_sizes = weakref.WeakKeyDictionary()
+        self._exec_times = weakref.WeakKeyDictionary()
+        self._memory = weakref.WeakKeyDictionary()
         self._measure = False
 
     # ----------------------------------------------------------- partitions
@@ -140,8 +143,12 @@ class ModuleManager:
         return len(parts) == 1
 
     # --------------------------------------------------------------- naming
+    @property
+    def _main(self):
+        return self._main_ref() if self._main_ref is not None else None
+
     def set_main_module(self, module):
-        self._main = module
+        self._main_ref = weakref.ref(module)
         self._module_partitions[module] = 0
 
     def is_main_module(self, module):
@@ -163,7 +170,7 @@ class ModuleManager:
                 if child is None:
                     continue
                 if child not in self._parent:
-                    self._parent[child] = mod
+                    self._parent[child] = weakref.ref(mod)
                 visit(child, f"{name}/{cname}")
 
         visit(self._main, "main")
@@ -175,7 +182,8 @@ class ModuleManager:
         return self._name_to_module[name]
 
     def get_parent_module(self, module):
-        return self._parent.get(module)
+        ref = self._parent.get(module)
+        return ref() if ref is not None else None
 
     def modules_in_order(self):
         return list(self._name_to_module.values())
@@ -286,7 +294,7 @@ class ModuleManager:
 
     # --------------------------------------------------------------- tracing
     def record_execution_order(self, module):
-        self._exec_order.append(module)
+        self._exec_order.append(weakref.ref(module))
 
     def save_input_size(self, module, size):
         self._input_sizes[module] = size
@@ -314,7 +322,7 @@ class ModuleManager:
         return self._measure
 
     def trace_results(self):
-        return TraceResults(list(self._exec_order), dict(self._input_sizes), dict(self._output_sizes),
+        return TraceResults([m for m in (r() for r in self._exec_order) if m is not None], dict(self._input_sizes), dict(self._output_sizes),
                             dict(self._exec_times), dict(self._memory))
 
     # ------------------------------------------------------------- metrics

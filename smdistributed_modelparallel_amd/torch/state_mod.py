@@ -9,6 +9,7 @@ Reference parity: `smp/torch/state_mod.py:31-418`.  Differences by design:
   that the two directions never share a stream (see `runtime/transport.py`).
 """
 import os
+import weakref
 import threading
 from contextlib import contextmanager
 
@@ -75,7 +76,8 @@ class PTModelParallelState:
         self.step_count = 0
         self.loaded_model_state = None
         self.loaded_optimizer_state = None
-        self.param_initializers = {}
+        # module -> initializer replayed by delayed init; weak keys so that a dropped model is freed
+        self.param_initializers = weakref.WeakKeyDictionary()
         self.delay_param_initialization_enabled = False
         self.offloaders = {}
         self.current_offloader = None

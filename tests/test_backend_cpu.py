@@ -411,3 +411,51 @@ def test_object_collectives_all_groups(placement):
 
     outs = run_workers("obj_comm", 4, [placement], timeout=240)
     assert all("OBJ_COMM_OK" in o for o in outs)
+
+
+_LEAK_CODE = r"""
+import gc, weakref, torch
+import smdistributed_modelparallel_amd.torch as smp
+from smdistributed_modelparallel_amd.models import build_gpt, gpt_inputs
+smp.init({"microbatches": 2})
+
+def run():
+    torch.manual_seed(0)
+    model = smp.DistributedModel(build_gpt("gpt2-tiny", dropout=0.1, num_layers=2))
+    opt = smp.DistributedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-3))
+
+    @smp.step
+    def train(model, ids, labels):
+        loss, _ = model((ids, None, None, None, labels))
+        model.backward(loss)
+        return loss
+
+    ids, _, _, _, labels = gpt_inputs(4, 32, 512, smp.state.device)
+    for _ in range(2):
+        opt.zero_grad(); train(model, ids, labels); opt.step()
+    smp.state.model = None
+    smp.state.optimizer = None
+    return weakref.ref(model), [weakref.ref(p) for p in model.get_module().parameters()]
+
+wm, wps = run()
+for _ in range(3):
+    gc.collect()
+alive = sum(r() is not None for r in wps)
+assert wm() is None and alive == 0, (wm() is not None, alive, len(wps))
+print("LEAK_OK")
+"""
+
+
+def test_dropped_model_is_freed(tmp_path):
+    """Reference test/torch/mpi/test_leak.py, without its manual module-manager reset: the
+    module manager holds modules weakly and gradient hooks hold their reducer weakly, so a
+    model (and its flat parameter buffers) is freed once the user drops it."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SMP_FORCE_CPU="1", PYTHONPATH=root, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29000 + os.getpid() % 1000))
+    r = subprocess.run([sys.executable, "-c", _LEAK_CODE], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "LEAK_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

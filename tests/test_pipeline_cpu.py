@@ -56,6 +56,16 @@ def test_tp2_uneven_heads():
                                       "intermediate_size": 96}})
 
 
+@pytest.mark.parametrize("prescaled", [False, True])
+def test_tp2_distribute_embedding(prescaled):
+    """distribute_embedding (reference transformer.py:217,245-306): vocab-parallel word
+    embedding with full-batch outputs, with and without prescaled_batch."""
+    extra = {"model": {"distribute_embedding": True}}
+    if prescaled:
+        extra["cfg"] = {"prescaled_batch": True}
+    _run(2, 1, 2, 2, extra=extra)
+
+
 def test_pp2_tp2():
     _run(4, 2, 2, 2)
 

@@ -106,8 +106,9 @@ def main():
             chunk = ids_all[d * local_bs:(d + 1) * local_bs]
             for m in range(mbs):
                 x = chunk[m * 2:(m + 1) * 2]
-                if prescaled:
+                if prescaled and not kw.get("distribute_embedding"):
                     # objective = mean over TP ranks of each rank's sequence-shard loss
+                    # (a vocab-parallel head computes the whole batch's loss on every TP rank)
                     _, logits = ref((x, None, None, None, x))
                     lab = torch.nn.functional.pad(x[:, 1:], (0, 1), value=-100)
                     half = x.shape[1] // 2
