@@ -35,6 +35,7 @@ MI355X design:
   recomputation (forward hooks firing inside backward) keeps the unit gathered.
 """
 import os
+import weakref
 from collections import deque
 
 import torch
@@ -407,10 +408,23 @@ class ShardedDataParallel:
         for m, u in self.unit_of_module.items():
             self._hooks.append(m.register_forward_pre_hook(self._make_pre(u)))
             self._hooks.append(m.register_forward_hook(self._make_post(u)))
+        # parameter hooks live on C++ autograd meta (not traversed by the garbage collector):
+        # they reach this engine through a weak reference so a dropped model is freed
+        ref = weakref.ref(self)
+
+        def make(ui):
+            def on_grad(p):
+                me = ref()
+                if me is not None:
+                    me._grad_hooks[ui](p)
+            return on_grad
+
+        self._grad_hooks = {}
         for u in self.units:
+            self._grad_hooks[u.index] = self._make_grad_hook(u)
             for p in u.params:
                 if p.requires_grad:
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._make_grad_hook(u)))
+                    self._hooks.append(p.register_post_accumulate_grad_hook(make(u.index)))
 
     def remove_hooks(self):
         for h in self._hooks:
