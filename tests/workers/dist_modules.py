@@ -89,8 +89,15 @@ def main():
     V = [6, 5]
     lo = sum(V[:r])
     ce = DistributedCrossEntropy(vocab_range=(lo, lo + V[r]))
-    mine = ce(logits[:, lo:lo + V[r]].contiguous(), target)
+    shard = logits[:, lo:lo + V[r]].contiguous().requires_grad_(True)
+    mine = ce(shard, target)
     close(mine, ref_loss, 1e-5, "dist CE")
+    # backward: the shard of the full softmax gradient, multiplied by tp (every TP rank holds
+    # the same loss; reference nn/cross_entropy.py:95-96)
+    full = logits.clone().requires_grad_(True)
+    F.cross_entropy(full, target, reduction="none").sum().backward()
+    mine.sum().backward()
+    close(shard.grad, full.grad[:, lo:lo + V[r]] * tp, 1e-5, "dist CE grad")
     # ---- tensor collectives
     counts = [3, 5]
     t = torch.arange(10, dtype=torch.float32) + 100 * r
