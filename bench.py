@@ -30,13 +30,23 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-xl")
     ap.add_argument("--seq", type=int, default=2048)
-    ap.add_argument("--mbs", type=int, default=32,
-                    help="per-GPU micro-batch size: 32 x 2048 tokens (GEMM M = 65536) amortises the per-step "
-                         "optimizer / LM-head / transposition work and fills the chip with attention blocks; "
-                         "~190 GB of the 288 GB HBM3E (same-box A/B vs 16: +4.4 %% samples/s)")
-    ap.add_argument("--microbatches", type=int, default=1)
-    ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--layers", type=int, default=None, help="override the model's layer count (tests only)")
+    ap.add_argument("--layout", choices=["auto", "dp", "pp"], default="auto",
+                    help="auto: N >= 4 GPUs (N %% 4 == 0) run BASELINE config 2 = GPT-2 XL PP=4 interleaved "
+                         "x DP=N/4; fewer GPUs run data parallel.  dp: pure data parallel.  pp: PP=4 (x DP)")
+    ap.add_argument("--mbs", type=int, default=None,
+                    help="micro-batch size.  DP layout default 32 x 2048 tokens (GEMM M = 65536): amortises the "
+                         "per-step optimizer / LM-head / transposition work and fills the chip with attention "
+                         "blocks, ~190 GB of the 288 GB HBM3E (same-box A/B vs 16: +4.4 %% samples/s).  PP layout "
+                         "default 4")
+    ap.add_argument("--microbatches", type=int, default=None,
+                    help="DP default 1; PP default 32 (pipeline bubble (pp-1)/(m+pp-1) = 8.6 %% at PP=4, and "
+                         "4 x 32 = 128 samples per pipeline per step = the DP layout's per-GPU work)")
+    ap.add_argument("--pp", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--head-cost", type=float, default=float(os.environ.get("SMP_BENCH_HEAD_COST", "2.4")),
+                    help="PP layer split: cost of stage 0's tied embedding + LM head + loss in transformer-layer "
+                         "units (2 h V vs 24 h^2 + attention FLOPs per token, plus the CE kernels)")
     ap.add_argument("--dropout", type=float, default=0.0)
     ap.add_argument("--no-flash", action="store_true")
     ap.add_argument("--activation-checkpointing", action="store_true")
@@ -48,6 +58,47 @@ def parse():
                          "per-shape winners measured on MI355X (configs/tunableop), 'tune' re-measures them "
                          "during warmup; auto = use when a results file exists")
     return ap.parse_args()
+
+
+def resolve_layout(args, world):
+    """Fill pp / mbs / microbatches from the layout (explicit flags win)."""
+    layout = args.layout
+    if layout == "auto":
+        layout = "pp" if (args.pp is None and world >= 4 and world % 4 == 0 and args.tp == 1) else "dp"
+        if args.pp is not None and args.pp > 1:
+            layout = "pp"
+    if layout == "pp":
+        args.pp = args.pp or 4
+        args.mbs = args.mbs or 4
+        args.microbatches = args.microbatches or 32
+    else:
+        args.pp = args.pp or 1
+        args.mbs = args.mbs or 32
+        args.microbatches = args.microbatches or 1
+    args.layout = layout
+    return args
+
+
+def balanced_layer_split(num_layers, pp, head_cost):
+    """Contiguous layer counts per stage minimising the most loaded stage, where stage 0 also
+    runs the tied embedding + LM head + loss (cost `head_cost` layers): the main module and
+    every module sharing the embedding weight stay on partition 0."""
+    best = None
+
+    def rec(i, left, counts):
+        nonlocal best
+        if i == pp - 1:
+            counts = counts + [left]
+            # most loaded stage first, then the next ones (prefer [10, 13, 13, 12] to [9, 13, 13, 13])
+            key = sorted((c + (head_cost if j == 0 else 0.0) for j, c in enumerate(counts)), reverse=True)
+            if best is None or key < best[0]:
+                best = (key, counts)
+            return
+        for c in range(1, left - (pp - 1 - i) + 1):
+            rec(i + 1, left - c, counts + [c])
+
+    rec(0, num_layers, [])
+    return best[1]
 
 
 def tunableop_file(args):
@@ -104,6 +155,7 @@ def main():
     from smdistributed_modelparallel_amd.ops.attention import FLASH_HEAD_DIMS
 
     world = int(os.environ.get("WORLD_SIZE", 1))
+    resolve_layout(args, world)
     cfg = {
         "pipeline_parallel_degree": args.pp,
         "tensor_parallel_degree": args.tp,
@@ -114,14 +166,29 @@ def main():
         "shard_optimizer_state": args.shard_optimizer_state,
         "amd_offload_optimizer_state": args.offload_optimizer_state,
     }
+    split = None
     if args.pp > 1:
-        cfg["auto_partition"] = True
+        cfg["pipeline"] = "interleaved"
+        if os.environ.get("SMP_BENCH_AUTO_PARTITION", "0") == "1":
+            cfg["auto_partition"] = True
+        else:
+            cfg["auto_partition"] = False
+            cfg["default_partition"] = 0
+            split = balanced_layer_split(args.layers or GPT_CONFIGS[args.model]["num_layers"], args.pp,
+                                         args.head_cost)
     smp.init(cfg)
     tmode = setup_tunableop(args)
     torch.manual_seed(1234 + smp.dp_rank())
     mc = GPT_CONFIGS[args.model]
     with smp.model_creation(tensor_parallelism=args.tp > 1, dtype=torch.float32):
-        model = build_gpt(args.model, dropout=args.dropout, num_positions=max(args.seq, mc["num_positions"]))
+        extra = {"num_layers": args.layers} if args.layers else {}
+        model = build_gpt(args.model, dropout=args.dropout, num_positions=max(args.seq, mc["num_positions"]), **extra)
+    if split is not None:
+        layer_idx = 0
+        for stage, cnt in enumerate(split):
+            for _ in range(cnt):
+                smp.set_partition(model.transformer.seq_layers[layer_idx], stage)
+                layer_idx += 1
     model = smp.DistributedModel(model)
     if args.activation_checkpointing:
         for layer in model.get_module().transformer.seq_layers:
@@ -220,6 +287,10 @@ def main():
                 "parallelism": par,
                 "micro_batch_per_gpu": args.mbs,
                 "microbatches": args.microbatches,
+                "layout": args.layout,
+                "pipeline": "interleaved" if args.pp > 1 else None,
+                "layer_split": split,
+                "p2p": smp.state.transport.mode if args.pp > 1 else None,
                 "flash_attention": (not args.no_flash) and mc["attention_head_size"] in FLASH_HEAD_DIMS,
                 "dropout": args.dropout,
                 "gemm_selection": "tunableop" if tmode != "off" else "heuristic",

@@ -16,7 +16,9 @@ PYBIND11_MODULE(_smprt, m) {
       .def_readonly("msgs_sent", &TransportStats::msgs_sent)
       .def_readonly("msgs_recv", &TransportStats::msgs_recv)
       .def_readonly("bytes_sent", &TransportStats::bytes_sent)
-      .def_readonly("bytes_recv", &TransportStats::bytes_recv);
+      .def_readonly("bytes_recv", &TransportStats::bytes_recv)
+      .def_readonly("gated_sent", &TransportStats::gated_sent)
+      .def_readonly("gate_wait_us", &TransportStats::gate_wait_us);
 
   py::class_<Mailbox>(m, "Mailbox")
       .def(py::init<int, int>())
@@ -30,6 +32,16 @@ PYBIND11_MODULE(_smprt, m) {
             mb.send(dst, tid, static_cast<uint8_t>(channel), std::move(s));
           },
           py::arg("dst"), py::arg("tid"), py::arg("channel"), py::arg("payload"))
+      .def(
+          "send_gated",
+          [](Mailbox& mb, int dst, int64_t tid, int channel, py::bytes payload, uintptr_t gate_fn, uintptr_t ctx) {
+            std::string s = payload;
+            py::gil_scoped_release nogil;
+            mb.send_gated(dst, tid, static_cast<uint8_t>(channel), std::move(s), reinterpret_cast<GateFn>(gate_fn),
+                          ctx);
+          },
+          py::arg("dst"), py::arg("tid"), py::arg("channel"), py::arg("payload"), py::arg("gate_fn"),
+          py::arg("gate_ctx"))
       .def(
           "send_buffer",
           [](Mailbox& mb, int dst, int64_t tid, int channel, py::buffer buf) {

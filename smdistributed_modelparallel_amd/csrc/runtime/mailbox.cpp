@@ -195,7 +195,32 @@ void Mailbox::send(int dst, int64_t tid, uint8_t channel, std::string payload) {
   Peer& p = *peers_[dst];
   {
     std::lock_guard<std::mutex> g(p.mu);
-    p.outq.push_back(std::move(f));
+    p.outq.push_back(OutMsg{std::move(f), nullptr, 0});
+  }
+  p.cv.notify_all();
+}
+
+void Mailbox::send_gated(int dst, int64_t tid, uint8_t channel, std::string payload, GateFn gate, uintptr_t ctx) {
+  if (gate == nullptr || dst == rank_) {
+    // a message to self is consumed by this process after everything it enqueued so far:
+    // wait for the gate here (it only covers this process's own device work)
+    if (gate != nullptr) {
+      while (gate(ctx) == 0) std::this_thread::yield();
+    }
+    send(dst, tid, channel, std::move(payload));
+    return;
+  }
+  if (dst < 0 || dst >= world_) throw std::runtime_error("mailbox: bad destination rank");
+  {
+    std::lock_guard<std::mutex> g(stats_mu_);
+    stats_.msgs_sent++;
+    stats_.bytes_sent += payload.size();
+  }
+  auto f = frame(tid, channel, payload);
+  Peer& p = *peers_[dst];
+  {
+    std::lock_guard<std::mutex> g(p.mu);
+    p.outq.push_back(OutMsg{std::move(f), gate, ctx});
   }
   p.cv.notify_all();
 }
@@ -217,7 +242,7 @@ void Mailbox::broadcast(const std::vector<int>& dsts, int64_t tid, uint8_t chann
     Peer& p = *peers_[d];
     {
       std::lock_guard<std::mutex> g(p.mu);
-      p.outq.push_back(f);
+      p.outq.push_back(OutMsg{f, nullptr, 0});
     }
     p.cv.notify_all();
   }
@@ -226,15 +251,42 @@ void Mailbox::broadcast(const std::vector<int>& dsts, int64_t tid, uint8_t chann
 void Mailbox::send_loop(int peer) {
   Peer& p = *peers_[peer];
   while (true) {
-    std::shared_ptr<const std::string> f;
+    OutMsg m;
     {
       std::unique_lock<std::mutex> lk(p.mu);
       p.cv.wait(lk, [&] { return stop_.load() || !p.outq.empty(); });
       if (p.outq.empty()) return;  // stop requested and drained
-      f = p.outq.front();
+      m = std::move(p.outq.front());
       p.outq.pop_front();
       p.writing = true;
     }
+    if (m.gate != nullptr) {
+      // wait (outside every lock) until the device work this message describes is done;
+      // later messages to this peer stay queued behind it (per-destination FIFO)
+      const auto t0 = std::chrono::steady_clock::now();
+      int r;
+      int spins = 0;
+      while ((r = m.gate(m.ctx)) == 0) {
+        if (stop_.load() && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) break;
+        if (++spins < 64) {
+          std::this_thread::yield();
+        } else {
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        }
+      }
+      const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0);
+      {
+        std::lock_guard<std::mutex> g(stats_mu_);
+        stats_.gated_sent++;
+        stats_.gate_wait_us += static_cast<uint64_t>(us.count());
+      }
+      if (r < 0) {
+        std::lock_guard<std::mutex> g(in_mu_);
+        if (error_.empty()) error_ = "mailbox: readiness gate of a message to rank " + std::to_string(peer) + " failed";
+        in_cv_.notify_all();
+      }
+    }
+    const std::shared_ptr<const std::string>& f = m.frame;
     try {
       write_all(p.fd, f->data(), f->size());
     } catch (const std::exception& e) {
@@ -428,7 +480,7 @@ void Mailbox::shutdown(bool success) {
       Peer& p = *peers_[d];
       {
         std::lock_guard<std::mutex> g(p.mu);
-        p.outq.push_back(f);
+        p.outq.push_back(OutMsg{f, nullptr, 0});
       }
       p.cv.notify_all();
     }

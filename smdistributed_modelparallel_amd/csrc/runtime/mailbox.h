@@ -44,7 +44,17 @@ struct Message {
 
 struct TransportStats {
   uint64_t msgs_sent = 0, msgs_recv = 0, bytes_sent = 0, bytes_recv = 0;
+  uint64_t gated_sent = 0;      // messages that waited for a readiness gate
+  uint64_t gate_wait_us = 0;    // total time the peer sender threads spent on gates
 };
+
+// Readiness gate of a gated send: returns 1 when the message may go out, 0 while it must
+// wait, < 0 on error (the message then goes out anyway and the error is recorded).  Called
+// from the destination's sender thread, never under a lock.  The pipeline transport passes
+// a HIP event query here (`csrc/torchrt/ipc_p2p.cpp`): a control message describing device
+// tensors leaves only once the kernels that produced them have completed, so the receiver
+// can pull the bytes without any device-side cross-process wait.
+using GateFn = int (*)(uintptr_t ctx);
 
 class Mailbox {
  public:
@@ -58,6 +68,9 @@ class Mailbox {
                double timeout_s);
 
   void send(int dst, int64_t tid, uint8_t channel, std::string payload);
+  // FIFO per destination like send(): this message and every later one to `dst` wait until
+  // gate(ctx) reports ready.
+  void send_gated(int dst, int64_t tid, uint8_t channel, std::string payload, GateFn gate, uintptr_t ctx);
   // Multi-destination send of one payload (smp_async_bcast).
   void broadcast(const std::vector<int>& dsts, int64_t tid, uint8_t channel,
                  const std::string& payload);
@@ -87,11 +100,16 @@ class Mailbox {
   int world() const { return world_; }
 
  private:
+  struct OutMsg {
+    std::shared_ptr<const std::string> frame;
+    GateFn gate = nullptr;
+    uintptr_t ctx = 0;
+  };
   struct Peer {
     int fd = -1;
     std::mutex mu;
     std::condition_variable cv;
-    std::deque<std::shared_ptr<const std::string>> outq;  // framed messages
+    std::deque<OutMsg> outq;  // framed messages (optionally gated)
     std::thread sender;
     bool writing = false;
   };

@@ -13,10 +13,15 @@
 //   2. system-scope release, then PUSH the epoch into every peer's flag array
 //      (flag[src rank][chunk]) -- remote stores over xGMI,
 //   3. poll the LOCAL flag array (peers pushed into it) until every peer's epoch arrived,
-//      bounded by a wall-clock timeout (an error flag is raised and the kernel exits: a dead
-//      peer can never hang the GPU),
+//      bounded by a wall-clock timeout,
 //   4. read the chunk from every peer's slot (xGMI) and reduce in rank order 0..world-1 in
 //      fp32 -- bitwise the same result on every rank, as TP requires.
+// Failure is never silent: a timeout (a peer skipped a call, died or drifted past the
+// timeout) writes the error word in host-mapped pinned memory (the host reads it without any
+// synchronisation at step end and raises), pushes an ABORT word into every peer's flag array
+// (their next or current kernels fail too, so the error surfaces on every rank), and the
+// kernel writes NaN -- not the stale slots -- into its output.  Once an instance has failed,
+// every later call on it fails the same way.
 // Slot reuse is safe with two slots: a rank writes slot (e % 2) at epoch e + 2 only after
 // every peer's chunk pushed epoch e + 1, which a peer does after its epoch-e kernel finished
 // reading.  All calls of one instance must be issued in the same order on every rank, on
@@ -41,6 +46,8 @@ namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 128;
 constexpr int kThreads = 256;
+constexpr int kAbortWord = kMaxRanks * kMaxBlocks;  // index of the abort word in a flag array
+constexpr int kFlagWords = kAbortWord + 64;          // the abort word on a line of its own
 
 void ar_check(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "IpcAllReduce: ", what, " failed: ", hipGetErrorString(e));
@@ -54,7 +61,7 @@ struct ArParams {
   const char* slot[kMaxRanks];      // data slot of every rank for this epoch (own included)
   uint32_t* peer_flags[kMaxRanks];  // flag array of every rank (mapped)
   uint32_t* my_flags;
-  int* err;
+  int* err;  // host-mapped pinned word
   int rank, world, op;  // op 0 = sum, 1 = max
   uint32_t epoch;
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
@@ -81,6 +88,8 @@ __global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(ArParams p)
   const int64_t hi = lo + p.chunk < p.n ? lo + p.chunk : p.n;
   constexpr int V = 16 / sizeof(T);  // elements per 16-byte vector
   const int64_t vlo = lo / V, vhi = hi / V;  // lo is a multiple of 8 >= V
+  __shared__ int s_fail;
+  if (tid == 0) s_fail = 0;
   // 1. input chunk -> own slot
   {
     const uint4* src = static_cast<const uint4*>(p.in);
@@ -97,20 +106,38 @@ __global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(ArParams p)
     __hip_atomic_store(p.peer_flags[tid] + p.rank * kMaxBlocks + b, p.epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 3. wait for every peer's chunk (bounded)
+  // 3. wait for every peer's chunk (bounded; a peer's abort ends the wait too)
   if (tid < p.world && tid != p.rank) {
     const uint32_t* f = p.my_flags + tid * kMaxBlocks + b;
+    const uint32_t* ab = p.my_flags + kAbortWord;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - p.epoch) < 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
-        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+    bool fail = __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    while (!fail &&
+           static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - p.epoch) < 0) {
+      if (__hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+        fail = true;
+      } else if (__builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
+        fail = true;
+        // tell every peer: their pending and future calls on this group fail as well
+        for (int r = 0; r < p.world; ++r)
+          __hip_atomic_store(p.peer_flags[r] + kAbortWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
+    }
+    if (fail) {
+      __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      s_fail = 1;
     }
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (system-scope acquire by the polling lanes above)
+  if (s_fail) {  // never reduce stale slots: the output is poisoned, the host raises at step end
+    T* out = static_cast<T*>(p.out);
+    const T nan = from_f<T>(__builtin_nanf(""));
+    for (int64_t i = lo + tid; i < hi; i += kThreads) out[i] = nan;
+    return;
+  }
   // 4. reduce in rank order (identical on every rank)
   T* out = static_cast<T*>(p.out);
   for (int64_t i = vlo + tid; i < vhi; i += kThreads) {
@@ -153,7 +180,7 @@ class IpcAllReduce {
     TORCH_CHECK(rank >= 0 && rank < world, "IpcAllReduce: bad rank");
     ar_check(hipSetDevice(device_), "hipSetDevice");
     ar_check(hipMalloc(&data_, 2 * max_bytes_), "hipMalloc(data)");
-    const size_t fbytes = sizeof(uint32_t) * kMaxRanks * kMaxBlocks;
+    const size_t fbytes = sizeof(uint32_t) * kFlagWords;
     // flags: uncached device memory (peers' pushes land in HBM, the poll reads HBM);
     // plain device memory if this allocation kind cannot be exported
     uncached_flags_ = hipExtMallocWithFlags(&flags_, fbytes, hipDeviceMallocUncached) == hipSuccess;
@@ -169,8 +196,12 @@ class IpcAllReduce {
     }
     if (!uncached_flags_) ar_check(hipMalloc(&flags_, fbytes), "hipMalloc(flags)");
     ar_check(hipMemset(flags_, 0, fbytes), "hipMemset(flags)");
-    ar_check(hipMalloc(reinterpret_cast<void**>(&err_), sizeof(int)), "hipMalloc(err)");
-    ar_check(hipMemset(err_, 0, sizeof(int)), "hipMemset(err)");
+    // error word in host-mapped pinned memory: kernels store into it, the host polls it with
+    // a plain load (no stream or device synchronisation on the step path)
+    ar_check(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(int), hipHostMallocMapped | hipHostMallocCoherent),
+             "hipHostMalloc(err)");
+    *err_host_ = 0;
+    ar_check(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_), err_host_, 0), "hipHostGetDevicePointer(err)");
     ar_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
     peer_data_.assign(world_, nullptr);
     peer_flags_.assign(world_, nullptr);
@@ -268,12 +299,22 @@ class IpcAllReduce {
     calls_++;
   }
 
-  // 1 if any kernel timed out waiting for a peer since the last reset (synchronises)
+  // 1 if a kernel of this instance failed (own timeout or a peer's abort).  Non-blocking: a
+  // plain read of the host-mapped error word; kernels still running are seen by a later call.
   int error(bool reset) {
-    int h = 0;
-    ar_check(hipMemcpy(&h, err_, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy(err)");
-    if (reset && h) ar_check(hipMemset(err_, 0, sizeof(int)), "hipMemset(err)");
+    const int h = __atomic_load_n(err_host_, __ATOMIC_ACQUIRE);
+    if (reset && h) __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE);
     return h;
+  }
+
+  // Test hook: this rank behaves as if its kernel had timed out (own error + abort pushed to
+  // every peer's flag array); used to exercise the failure path without a 10-minute wait.
+  void inject_abort() {
+    ar_check(hipSetDevice(device_), "hipSetDevice");
+    const uint32_t one = 1;
+    for (int r = 0; r < world_; ++r)
+      ar_check(hipMemcpy(peer_flags_[r] + kAbortWord, &one, sizeof(one), hipMemcpyHostToDevice), "hipMemcpy(abort)");
+    __atomic_store_n(err_host_, 1, __ATOMIC_RELEASE);
   }
 
   void close() {
@@ -284,7 +325,9 @@ class IpcAllReduce {
     opened_.clear();
     hipFree(data_);
     hipFree(flags_);
-    hipFree(err_);
+    hipHostFree(err_host_);
+    err_host_ = nullptr;
+    err_ = nullptr;
     data_ = nullptr;
     ready_ = false;
   }
@@ -305,7 +348,8 @@ class IpcAllReduce {
   int64_t max_bytes_;
   void* data_ = nullptr;
   void* flags_ = nullptr;
-  int* err_ = nullptr;
+  int* err_ = nullptr;       // device view of err_host_
+  int* err_host_ = nullptr;  // hipHostMalloc'd, mapped + coherent
   bool uncached_flags_ = false;
   bool ready_ = false;
   uint32_t epoch_ = 0;
@@ -325,6 +369,7 @@ void register_ipc_allreduce(py::module& m) {
       .def("all_reduce", &IpcAllReduce::all_reduce, py::arg("input"), py::arg("output"), py::arg("op") = 0,
            py::arg("timeout_s") = 5.0)
       .def("error", &IpcAllReduce::error, py::arg("reset") = true)
+      .def("inject_abort", &IpcAllReduce::inject_abort)
       .def("close", &IpcAllReduce::close)
       .def("stats", &IpcAllReduce::stats)
       .def_property_readonly("max_bytes", &IpcAllReduce::max_bytes);

@@ -6,19 +6,22 @@
 // MI355X design (ours):
 //  * export(t): the sender publishes the allocation that holds `t` (hipIpcGetMemHandle of
 //    the caching-allocator segment, cached per segment and invalidated when the allocator
-//    returns the segment to the driver) and records an inter-process event on its compute
-//    stream right after the producer kernels.  Nothing is copied on the sender.
+//    returns the segment to the driver).  Nothing is copied on the sender.
+//  * record_event(): one plain HIP event per control message, recorded on the sender's
+//    compute stream right after the producer kernels.  The control message is handed to the
+//    native mailbox as a GATED send (`csrc/runtime/mailbox.h`): the destination's sender
+//    thread releases it (and everything queued after it for that peer, FIFO) only once this
+//    event has completed -- `gate_fn()` is the hipEventQuery predicate it calls.  So when a
+//    receiver sees the message, the bytes are final: no cross-process device wait (inter-
+//    process events) is ever needed.  The sender's host does not block, and neither does the
+//    receiver's.
 //  * import_copy(dst, ...): the receiver maps the segment once (hipIpcOpenMemHandle with
 //    lazy peer enable -- over xGMI when the ranks own different GPUs, plain HBM when they
-//    share one), makes its compute stream wait on the sender's event (device-side, no host
-//    blocking) and pulls the bytes with one hipMemcpyAsync D2D on that stream.  The copy
-//    is enqueued the moment the control message arrives, i.e. the "receive" is posted as
-//    early as the data can exist; no receive pool is needed because the destination is an
-//    ordinary caching-allocator tensor of the receiver.
-//  * lifetime: the sender keeps the source tensor and the event slot until the receiver
-//    reports (release message, Python side) that its copy has completed; event slots are
-//    therefore never re-recorded while a peer may still wait on them (re-recording a slot
-//    a peer has not waited on yet could create a cross-process wait cycle).
+//    share one) and pulls the bytes with one hipMemcpyAsync D2D on its current stream (the
+//    transport's communication stream).  No receive pool is needed because the destination
+//    is an ordinary caching-allocator tensor of the receiver.
+//  * lifetime: the sender keeps the source tensors and the event slot until the receiver
+//    reports (release message, Python side) that its copy has completed.
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
@@ -79,7 +82,7 @@ class IpcP2P {
 
   ~IpcP2P() { close(); }
 
-  // -> (segment_base, generation, mem_handle_bytes, offset, nbytes, event_slot, event_handle_bytes)
+  // -> (segment_base, generation, mem_handle_bytes, offset, nbytes)
   py::tuple export_tensor(const at::Tensor& t) {
     TORCH_CHECK(t.is_cuda(), "IpcP2P.export: tensor must be on the GPU");
     TORCH_CHECK(t.is_contiguous(), "IpcP2P.export: tensor must be contiguous");
@@ -102,15 +105,30 @@ class IpcP2P {
     }
     const int64_t offset = static_cast<int64_t>(reinterpret_cast<uintptr_t>(ptr) - b);
     const int64_t nbytes = static_cast<int64_t>(t.numel() * t.element_size());
-    int slot = acquire_event_locked();
-    hip_check(hipEventRecord(events_[slot].ev, at::hip::getCurrentHIPStream(device_).stream()), "hipEventRecord");
     stats_exports_++;
     stats_bytes_out_ += nbytes;
     return py::make_tuple(static_cast<int64_t>(b), it->second.gen,
                           py::bytes(reinterpret_cast<const char*>(&it->second.handle), sizeof(hipIpcMemHandle_t)),
-                          offset, nbytes, slot,
-                          py::bytes(reinterpret_cast<const char*>(&events_[slot].handle), sizeof(hipIpcEventHandle_t)));
+                          offset, nbytes);
   }
+
+  // Sender side: record the readiness event of one control message on the current stream.
+  // -> (slot, gate context for gate_fn)
+  py::tuple record_event() {
+    std::lock_guard<std::mutex> g(mu_);
+    int slot = acquire_event_locked();
+    hip_check(hipEventRecord(events_[slot].ev, at::hip::getCurrentHIPStream(device_).stream()), "hipEventRecord");
+    return py::make_tuple(slot, static_cast<uint64_t>(reinterpret_cast<uintptr_t>(events_[slot].ev)));
+  }
+
+  // hipEventQuery predicate for the mailbox's gated sends: 1 done, 0 pending, -1 error.
+  static int event_gate(uintptr_t ctx) {
+    const hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(ctx));
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return -1;
+  }
+  static uint64_t gate_fn() { return static_cast<uint64_t>(reinterpret_cast<uintptr_t>(&IpcP2P::event_gate)); }
 
   // Sender side: the peer's copy out of `slot` completed (release message).
   void release_event(int slot) {
@@ -122,16 +140,16 @@ class IpcP2P {
     }
   }
 
-  // Receiver side: enqueue (wait sender event) + (copy nbytes into dst) on the current stream.
+  // Receiver side: enqueue one D2D pull of nbytes into dst on the current stream.  The
+  // message that carried the handle was gated on the producer's completion, so the bytes
+  // are final.
   void import_copy(at::Tensor dst, int src, int64_t base, int64_t gen, py::bytes mem_handle, int64_t offset,
-                   int64_t nbytes, int slot, py::bytes ev_handle) {
+                   int64_t nbytes) {
     TORCH_CHECK(dst.is_cuda() && dst.is_contiguous(), "IpcP2P.import: dst must be a contiguous GPU tensor");
     TORCH_CHECK(dst.numel() * dst.element_size() == nbytes, "IpcP2P.import: size mismatch (dst ",
                 dst.numel() * dst.element_size(), " B, message ", nbytes, " B)");
     std::string mh = mem_handle;
-    std::string eh = ev_handle;
-    TORCH_CHECK(mh.size() == sizeof(hipIpcMemHandle_t) && eh.size() == sizeof(hipIpcEventHandle_t),
-                "IpcP2P.import: malformed handles");
+    TORCH_CHECK(mh.size() == sizeof(hipIpcMemHandle_t), "IpcP2P.import: malformed handle");
     std::lock_guard<std::mutex> g(mu_);
     // ---- mapping of the sender's segment
     auto key = std::make_pair(src, base);
@@ -150,20 +168,7 @@ class IpcP2P {
       it = imports_.find(key);
       stats_maps_++;
     }
-    // ---- the sender's event slot
-    auto ek = std::make_pair(src, slot);
-    auto eit = peer_events_.find(ek);
-    if (eit == peer_events_.end() || eit->second.handle_bytes != eh) {
-      if (eit != peer_events_.end()) hipEventDestroy(eit->second.ev);
-      hipIpcEventHandle_t h;
-      std::memcpy(&h, eh.data(), sizeof(h));
-      hipEvent_t ev;
-      hip_check(hipIpcOpenEventHandle(&ev, h), "hipIpcOpenEventHandle");
-      peer_events_[ek] = PeerEvent{ev, eh};
-      eit = peer_events_.find(ek);
-    }
     hipStream_t s = at::hip::getCurrentHIPStream(device_).stream();
-    hip_check(hipStreamWaitEvent(s, eit->second.ev, 0), "hipStreamWaitEvent");
     if (nbytes > 0) {
       hip_check(hipMemcpyAsync(dst.data_ptr(), static_cast<char*>(it->second.ptr) + offset, nbytes,
                                hipMemcpyDeviceToDevice, s),
@@ -177,8 +182,6 @@ class IpcP2P {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& kv : imports_) hipIpcCloseMemHandle(kv.second.ptr);
     imports_.clear();
-    for (auto& kv : peer_events_) hipEventDestroy(kv.second.ev);
-    peer_events_.clear();
     for (auto& e : events_) hipEventDestroy(e.ev);
     events_.clear();
     free_slots_.clear();
@@ -204,25 +207,18 @@ class IpcP2P {
  private:
   struct LocalEvent {
     hipEvent_t ev;
-    hipIpcEventHandle_t handle;
     bool busy;
   };
   struct Mapping {
     int64_t gen;
     void* ptr;
   };
-  struct PeerEvent {
-    hipEvent_t ev;
-    std::string handle_bytes;
-  };
 
   int acquire_event_locked() {
     if (free_slots_.empty()) {
       LocalEvent e;
       hip_check(hipSetDevice(device_), "hipSetDevice");
-      hip_check(hipEventCreateWithFlags(&e.ev, hipEventInterprocess | hipEventDisableTiming),
-                "hipEventCreateWithFlags(interprocess)");
-      hip_check(hipIpcGetEventHandle(&e.handle, e.ev), "hipIpcGetEventHandle");
+      hip_check(hipEventCreateWithFlags(&e.ev, hipEventDisableTiming), "hipEventCreateWithFlags");
       e.busy = false;
       events_.push_back(e);
       free_slots_.push_back(static_cast<int>(events_.size()) - 1);
@@ -249,7 +245,6 @@ class IpcP2P {
   std::vector<LocalEvent> events_;
   std::vector<int> free_slots_;
   std::map<std::pair<int, int64_t>, Mapping> imports_;
-  std::map<std::pair<int, int>, PeerEvent> peer_events_;
   int64_t stats_exports_ = 0, stats_exports_new_ = 0, stats_imports_ = 0, stats_maps_ = 0;
   int64_t stats_bytes_out_ = 0, stats_bytes_in_ = 0;
 };
@@ -258,8 +253,10 @@ void register_ipc_p2p(py::module& m) {
   py::class_<IpcP2P>(m, "IpcP2P")
       .def(py::init<int>(), py::arg("device"))
       .def("export_tensor", &IpcP2P::export_tensor)
+      .def("record_event", &IpcP2P::record_event)
+      .def_static("gate_fn", &IpcP2P::gate_fn)
       .def("import_copy", &IpcP2P::import_copy, py::arg("dst"), py::arg("src"), py::arg("base"), py::arg("gen"),
-           py::arg("mem_handle"), py::arg("offset"), py::arg("nbytes"), py::arg("slot"), py::arg("ev_handle"))
+           py::arg("mem_handle"), py::arg("offset"), py::arg("nbytes"))
       .def("release_event", &IpcP2P::release_event)
       .def("close", &IpcP2P::close)
       .def("stats", &IpcP2P::stats);

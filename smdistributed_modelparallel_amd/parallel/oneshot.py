@@ -14,9 +14,20 @@ RCCL / gloo path unchanged.
 Safety: the first use on a group builds the buffers, exchanges the IPC handles over the
 group and runs a self-check against ``dist.all_reduce`` (sum and max, rank-dependent
 data, two epochs so both buffer slots are exercised); any mismatch, timeout or mapping
-failure disables the path for that group with a warning.  ``SMP_ONESHOT_ALLREDUCE=0``
-disables it, ``=1`` also allows it for groups whose ranks share one GPU (single-GPU
-rehearsals and tests); the default ``auto`` needs distinct GPUs on one host.
+failure disables the path for that group with a warning.  Every step of that set-up runs
+the same collectives on every rank whatever fails where (the failures are agreed first).
+``SMP_ONESHOT_ALLREDUCE=0`` disables it, ``=1`` also allows it for groups whose ranks share
+one GPU (single-GPU rehearsals and tests); the default ``auto`` needs distinct GPUs on one
+host.
+
+Failures after set-up are never silent: a kernel that waits longer than
+``SMP_ONESHOT_ALLREDUCE_TIMEOUT_S`` (default 600 s, the RCCL process-group timeout) for a
+peer -- a rank skipped a call, died, or drifted away -- writes NaN instead of reducing stale
+slots, raises the instance's host-mapped error word and pushes an abort into every peer's
+flag array, so the peers' kernels fail too.  ``check_errors()`` (called by
+``DistributedModel`` at the end of every step: a host read, no synchronisation) raises
+``OneShotAllReduceError`` on every rank of the group, and the failed instance refuses all
+later calls.
 """
 import os
 import socket
@@ -24,6 +35,7 @@ import socket
 import torch
 import torch.distributed as dist
 
+from ..backend.exceptions import SMPRuntimeError
 from ..backend.logger import get_logger
 
 logger = get_logger()
@@ -31,10 +43,15 @@ logger = get_logger()
 _MODE = os.environ.get("SMP_ONESHOT_ALLREDUCE", "auto")
 _MAX_BYTES = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_BYTES", str(1 << 20)))
 _MAX_RANKS = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_RANKS", "4"))
-_TIMEOUT_S = float(os.environ.get("SMP_ONESHOT_ALLREDUCE_TIMEOUT_S", "10"))
+_TIMEOUT_S = float(os.environ.get("SMP_ONESHOT_ALLREDUCE_TIMEOUT_S", "600"))
 _DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
 _instances = {}  # group key -> IpcAllReduce or None (disabled)
+_failed = set()  # group keys whose instance reported a failure
+
+
+class OneShotAllReduceError(SMPRuntimeError):
+    pass
 
 
 def _key(group):
@@ -49,6 +66,7 @@ def reset():
             except Exception:  # pragma: no cover - best effort at shutdown
                 pass
     _instances.clear()
+    _failed.clear()
 
 
 def _create(group):
@@ -81,12 +99,16 @@ def _create(group):
             inst.open(hs)
         except Exception as e:
             err = repr(e)
-    ok = err is None and _self_check(inst, group)
+    # agree before the self-check: it runs collectives, so it runs on every rank or on none
+    errs = [None] * ws
+    dist.all_gather_object(errs, err, group=group)
+    first_err = next((e for e in errs if e is not None), None)
+    ok = first_err is None and _self_check(inst, group)
     flags = [None] * ws
     dist.all_gather_object(flags, bool(ok), group=group)
     if not all(flags):
         logger.warning(f"one-shot all-reduce disabled for a TP group of {ws}: "
-                       f"{err or 'self-check against dist.all_reduce failed'}")
+                       f"{first_err or 'self-check against dist.all_reduce failed'}")
         if inst is not None:
             inst.close()
         return None
@@ -95,9 +117,12 @@ def _create(group):
 
 
 def _self_check(inst, group):
+    """Every iteration runs on every rank (no early exit: the dist.all_reduce calls must
+    stay matched); failures are accumulated and agreed by the caller."""
     r = dist.get_rank(group)
     dev = torch.device("cuda", torch.cuda.current_device())
     ok = True
+    check_timeout = min(_TIMEOUT_S, 60.0)
     for n, dt in ((4099, torch.float32), (3 * 4096 + 8, torch.bfloat16)):
         g = torch.Generator(device="cpu").manual_seed(1234 + 7 * r)
         x = torch.randn(n, generator=g).to(dev, dt)
@@ -105,10 +130,14 @@ def _self_check(inst, group):
             ref = x.float().clone()
             dist.all_reduce(ref, op=dop, group=group)
             out = torch.empty_like(x)
-            inst.all_reduce(x, out, op, _TIMEOUT_S)
-            torch.cuda.synchronize()
-            if inst.error(True):
-                return False
+            try:
+                inst.all_reduce(x, out, op, check_timeout)
+                torch.cuda.synchronize()
+            except Exception:  # noqa: B902 - a failed launch fails the check, collectives continue
+                ok = False
+                continue
+            if inst.error(False):
+                ok = False
             tol = 1e-5 if dt == torch.float32 else 2e-2
             if not torch.allclose(out.float(), ref.to(dt).float(), rtol=tol, atol=tol):
                 ok = False
@@ -130,6 +159,9 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None):
             and op in (dist.ReduceOp.SUM, dist.ReduceOp.MAX) and _MODE != "0"):
         inst = _instance(group)
         if inst is not None:
+            if _key(group) in _failed:
+                raise OneShotAllReduceError("one-shot all-reduce: this TP group failed earlier (a peer timed out "
+                                            "or aborted); its results can no longer be trusted")
             code = 0 if op == dist.ReduceOp.SUM else 1
             if x.data_ptr() % 16 == 0:
                 inst.all_reduce(x, x, code, _TIMEOUT_S)
@@ -143,7 +175,19 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None):
 
 
 def check_errors():
-    """Raise if any one-shot all-reduce timed out waiting for a peer (synchronises)."""
-    for inst in _instances.values():
-        if inst is not None and inst.error(True):
-            raise RuntimeError("one-shot all-reduce: a kernel timed out waiting for a peer rank")
+    """Raise ``OneShotAllReduceError`` if a one-shot all-reduce of any group failed (own
+    timeout, or a peer's abort).  Non-blocking: reads the host-mapped error words; a kernel
+    still waiting is caught by a later call.  The failed instance stays disabled."""
+    for k, inst in _instances.items():
+        if inst is not None and (k in _failed or inst.error(False)):
+            _failed.add(k)
+    if _failed:
+        raise OneShotAllReduceError(f"one-shot all-reduce failed on {len(_failed)} TP group(s): a kernel timed out "
+                                    f"waiting for a peer rank (or a peer aborted); outputs were poisoned with NaN")
+
+
+def inject_failure(group=None):
+    """Test hook: this rank acts as if its one-shot kernel had timed out on `group`."""
+    inst = _instances.get(_key(group))
+    if inst is not None:
+        inst.inject_abort()

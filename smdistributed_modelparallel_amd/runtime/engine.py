@@ -217,14 +217,16 @@ class PipelineEngine:
         self.mb_inputs = mb_inputs
         if leader:
             self.pipeline = create_pipeline(cfg.pipeline, n, cfg.active_microbatches)
+        failed = True
         try:
             self._serve(leader)
+            failed = False
         except SMPRuntimeError:
             raise
         except BaseException as e:  # noqa: B902 - tell the other stages before dying
             self._abort(e)
         finally:
-            self.state.transport.drain()
+            self.state.transport.drain(release_timeout=0.0 if failed else None)
         outs = [self.results[i] for i in range(n)]
         self.reset_step()
         return outs

@@ -122,10 +122,12 @@ def init(config=None):
     state.tp_registry.register_builtins()
     seed = cfg.tensor_parallel_seed + 1000 * core.pp_rank() + 100000 * core.rdp_rank()
     state.rng_manager = RngManager(seed, state.device)
-    from ..runtime.transport import choose_mode
+    from ..runtime.transport import resolve_mode
 
     be = dist.get_backend()
-    state.p2p_mode = choose_mode(core, state.device, "nccl" if "nccl" in str(be) else "gloo")
+    # IPC between stages is self-checked on every directed pair; a failure anywhere moves
+    # every rank to RCCL (or host staging on gloo) before the P2P groups are created
+    state.p2p_mode = resolve_mode(core, state.device, "nccl" if "nccl" in str(be) else "gloo")
     state.create_process_groups()
     if cfg.offload_activations:
         from ..runtime.offload import create_offloader

@@ -449,6 +449,11 @@ class DistributedModel(nn.Module):
             if name not in self._post_step_hooks_run:
                 self._post_step_hooks_run.add(name)
                 hook(self, state.optimizer)
+        # a one-shot TP all-reduce that timed out (or whose peer aborted) poisoned its output:
+        # surface it on every rank of the group now (a host read, no device synchronisation)
+        from ..parallel import oneshot
+
+        oneshot.check_errors()
         if state.core.pp_size() > 1:
             state.comm.barrier(CommGroup.PP_GROUP)
 

@@ -43,3 +43,31 @@ def test_bench_json_line(nproc):
     assert cfg["parallelism"] == f"pp1xtp1xdp{nproc}"
     # value is the whole-job aggregate: global batch x steps / max-over-ranks wall time
     assert abs(rec["value"] - cfg["global_batch"] / (rec["ms_per_step"] / 1000.0)) < 0.02 * rec["value"] + 1e-3
+
+
+def test_bench_pp_layout_four_ranks():
+    """N = 4 defaults to BASELINE config 2's layout (PP=4 interleaved): the JSON line says so."""
+    args = ["bench.py", "--gpus", "4", "--model", "gpt2-tiny", "--layers", "4", "--seq", "32", "--mbs", "1",
+            "--microbatches", "4", "--steps", "1", "--warmup", "1"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    cfg = rec["config"]
+    assert cfg["parallelism"] == "pp4xtp1xdp1" and cfg["layout"] == "pp" and cfg["pipeline"] == "interleaved"
+    assert cfg["microbatches"] == 4 and cfg["global_batch"] == 4 and sum(cfg["layer_split"]) == 4
+    assert rec["n_gpus"] == 4
+
+
+def test_balanced_layer_split():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    s = bench.balanced_layer_split(48, 4, 2.4)
+    assert sum(s) == 48 and s[0] == 10 and max(s[1:]) == 13  # stage 0 carries the tied LM head
+    assert bench.balanced_layer_split(48, 4, 0.0) == [12, 12, 12, 12]
+    assert sum(bench.balanced_layer_split(8, 2, 1.0)) == 8

@@ -34,3 +34,11 @@ def test_tp2_gpt_same_losses_with_oneshot():
     assert calls_on > 0 and calls_off == 0
     for a, b in zip(on, off):
         assert abs(a - b) < 1e-4 * max(1.0, abs(b)), (on, off)
+
+
+def test_oneshot_skipped_call_raises_on_every_rank():
+    # rank 1 skips one call: rank 0 times out (3 s here), writes NaN instead of stale sums and
+    # aborts the group; the error surfaces on both ranks and the instance refuses later calls
+    outs = run_workers("oneshot_gpu", 2, ["skip"], timeout=110,
+                       env_extra=dict(_ENV, SMP_ONESHOT_ALLREDUCE_TIMEOUT_S="3"))
+    assert all("OK raised" in o for o in outs)

@@ -44,3 +44,15 @@ def test_pp2_bf16_ipc():
 
 def test_pp2_host_staged_transport():
     _run(2, 2, 2, env={"SMP_P2P": "host"})
+
+
+def test_pp2_ipc_on_compute_stream():
+    # SMP_P2P_COMM_STREAM=0: pulls enqueued on the compute stream (the pre-comm-stream path)
+    _run(2, 2, 2, env={"SMP_P2P_COMM_STREAM": "0"})
+
+
+def test_pp4_ipc_selfcheck_forced_failure_falls_back_to_host():
+    # the init-time IPC self-check fails on rank 2 only: every rank must agree on the
+    # fallback (host staging, the process groups being gloo) and still train exactly
+    env = {"SMP_P2P": "", "SMP_P2P_SELFCHECK_FAIL": "2"}
+    _run(4, 4, 4, extra={"expect_mode": "host", "model": {"num_layers": 4}}, env=env)

@@ -47,6 +47,46 @@ def kernel():
     dist.barrier()
 
 
+def skip():
+    """Rank 1 skips one one-shot call: rank 0's kernel must time out and poison its output,
+    the abort must reach rank 1, and check_errors() must raise on BOTH ranks."""
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    from smdistributed_modelparallel_amd.parallel import oneshot
+
+    r = dist.get_rank()
+    dev = torch.device("cuda", 0)
+    x = torch.ones(4096, device=dev)
+    oneshot.all_reduce(x)  # set-up + one good call on both ranks
+    torch.cuda.synchronize()
+    assert torch.all(x == dist.get_world_size()), x[:4]
+    oneshot.check_errors()
+    if r == 0:
+        y = torch.ones(4096, device=dev)
+        oneshot.all_reduce(y)  # rank 1 never joins this one: times out
+        torch.cuda.synchronize()
+        assert torch.isnan(y).all(), "timed-out call must not return stale sums"
+    dist.barrier()
+    z = torch.ones(4096, device=dev)
+    oneshot.all_reduce(z)
+    torch.cuda.synchronize()
+    assert torch.isnan(z).all(), f"rank {r}: call after a peer's abort must fail"
+    try:
+        oneshot.check_errors()
+    except oneshot.OneShotAllReduceError as e:
+        raised = str(e)
+    else:
+        raise AssertionError(f"rank {r}: check_errors did not raise")
+    try:
+        oneshot.all_reduce(torch.ones(8, device=dev))
+    except oneshot.OneShotAllReduceError:
+        pass
+    else:
+        raise AssertionError("a failed instance must refuse later calls")
+    print(f"rank {r} OK raised: {raised[:60]}", flush=True)
+    dist.barrier()
+
+
 def tp(steps):
     import smdistributed_modelparallel_amd.torch as smp
     from smdistributed_modelparallel_amd.models import build_gpt
@@ -85,5 +125,7 @@ def tp(steps):
 if __name__ == "__main__":
     if sys.argv[1] == "kernel":
         kernel()
+    elif sys.argv[1] == "skip":
+        skip()
     else:
         tp(int(sys.argv[2]))

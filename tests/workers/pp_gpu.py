@@ -33,7 +33,8 @@ def main():
     if not extra.get("auto"):
         cfg["default_partition"] = 0
     smp.init(cfg)
-    assert smp.state.transport.mode == os.environ.get("SMP_P2P", "ipc"), smp.state.transport.mode
+    want_mode = extra.get("expect_mode", os.environ.get("SMP_P2P", "ipc"))
+    assert smp.state.transport.mode == want_mode, (smp.state.transport.mode, want_mode)
     net = build_gpt("gpt2-small", dropout=0.0, **kw)
     net.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
     if not extra.get("auto") and pp > 1:
@@ -84,6 +85,9 @@ def main():
     st = smp.state.transport.stats()
     if pp > 1 and st["mode"] == "ipc":
         assert st["imports"] > 0 and st["exports"] > 0, st
+        # every exported activation / gradient was released by its receiver at step end
+        assert st["held"] == 0 and st["event_slots_busy"] == 0 and st["release_wait_timeouts"] == 0, st
+        assert st["comm_stream"] == (os.environ.get("SMP_P2P_COMM_STREAM", "1") != "0"), st
     print(f"rank {smp.rank()} OK pp={pp} loss={ref_loss.item():.5f} worst_param_diff={worst:.2e} p2p={st}", flush=True)
     smp.barrier()
 
