@@ -738,6 +738,21 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * DS), kf[t], s);
         dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * DS), vf[t], dp);
       }
+      // dO^T / Q^T fragments of the dV / dK MFMAs now (independent of the exp / dS work below),
+      // so those MFMAs issue back to back instead of each waiting on its own LDS reads
+      constexpr bool TPRE = D <= 128 && !BIAS;
+      typename MF<T>::e8 tdo[TPRE ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
+      if constexpr (TPRE) {
+        const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
+#pragma unroll
+        for (int i = 0; i < DO / 32; ++i) {
+          tdo[i][0] = ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0);
+          tdo[i][1] = ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1);
+          tq[i][0] = ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0);
+          tq[i][1] = ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (blk_bias) {
 #pragma unroll
         for (int j = 0; j < 16; ++j) s[j] += kbias;
@@ -772,10 +787,17 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
       for (int i = 0; i < DO / 32; ++i) {
         const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
-        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
-        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
-        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
-        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
+        if constexpr (TPRE) {
+          dv[i] = MF<T>::mma(tdo[i][0], pf0, dv[i]);
+          dv[i] = MF<T>::mma(tdo[i][1], pf1, dv[i]);
+          dk[i] = MF<T>::mma(tq[i][0], sf0, dk[i]);
+          dk[i] = MF<T>::mma(tq[i][1], sf1, dk[i]);
+        } else {
+          dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
+          dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
+          dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
+          dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
+        }
       }
     }
   }
@@ -908,6 +930,15 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     // overlap each other's softmax VALU work).  D = 256: half by half, so only one half's
     // S / dP accumulators are live next to the 16 Q / dO fragments.
     constexpr bool SEQ = D >= 256;
+    // K^T fragments of the dQ MFMAs (independent of the softmax work): read up front
+    constexpr bool KPRE = !SEQ && !BIAS;
+    typename MF<T>::e8 ktf[KPRE ? DO / 32 : 1][4];
+    if constexpr (KPRE) {
+#pragma unroll
+      for (int i = 0; i < DO / 32; ++i)
+#pragma unroll
+        for (int st = 0; st < 4; ++st) ktf[i][st] = ld_tr<T>(sK, tro.lo[i] + 16 * st * DS, tro.hi[i] + 16 * st * DS);
+    }
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -958,7 +989,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       for (int i = 0; i < DO / 32; ++i) {
 #pragma unroll
         for (int st = 0; st < 4; ++st)
-          dq[i] = MF<T>::mma(ld_tr<T>(sK, tro.lo[i] + 16 * st * DS, tro.hi[i] + 16 * st * DS), sf[st], dq[i]);
+          dq[i] = MF<T>::mma(KPRE ? ktf[i][st] : ld_tr<T>(sK, tro.lo[i] + 16 * st * DS, tro.hi[i] + 16 * st * DS),
+                             sf[st], dq[i]);
       }
     }
   }
