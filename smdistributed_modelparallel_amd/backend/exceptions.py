@@ -97,6 +97,19 @@ class MissingPathFromModuleInputToModuleOutputError(SMPRuntimeError):
                 "gradient)")
 
 
+class NotSupportedByFastModeError(SMPRuntimeError):
+    """Reference `smp/torch/exceptions.py:355-362`: the model cannot run in fast mode (the
+    parent used a tensor that was transmitted child-to-child), or its graph changed after
+    the direct-consumer maps were recorded."""
+
+    def __init__(self, graph_change=False, detail=""):
+        self.graph_change = graph_change
+        msg = ("A change in model graph is detected. Graph changes are not supported in fast mode, please set "
+               "'fast_mode' to False." if graph_change else
+               "Model is not supported by fast mode, please set 'fast_mode' to False.")
+        super().__init__(msg + (f" ({detail})" if detail else ""))
+
+
 class DistributedModelNotWrappedError(SMPRuntimeError):
     pass
 

@@ -54,6 +54,20 @@ def config_to_kwargs(config):
         "scale_attn_by_layer_idx": bool(getattr(config, "scale_attn_by_inverse_layer_idx", False)),
         "add_lm_head": True,
         "tie_input_output_embedding": True,
+        **_attention_flags(config),
+    }
+
+
+def _attention_flags(config):
+    """Score scaling / precision fields of the HF GPT-2 config (reference
+    `torch/nn/huggingface/gpt2.py:75-78`): ``scale_attn_weights`` -> divide scores by
+    sqrt(d); ``reorder_and_upcast_attn`` -> layer-idx query/key scaling with the scores and
+    softmax in fp32."""
+    upcast = bool(getattr(config, "reorder_and_upcast_attn", False))
+    return {
+        "scale_attention_scores": bool(getattr(config, "scale_attn_weights", True)),
+        "query_key_layer_scaling": upcast,
+        "attention_in_fp32": upcast,
     }
 
 
@@ -143,6 +157,7 @@ def layer_config_to_kwargs(config, layer_idx=None):
         "causal_mask_size": config.n_positions,
         "scale_attn_by_layer_idx": bool(getattr(config, "scale_attn_by_inverse_layer_idx", False)),
         "layer_idx": layer_idx or 0,
+        **_attention_flags(config),
     }
 
 

@@ -46,6 +46,7 @@ from .layer_norm import DistributedLayerNorm, FusedLayerNorm
 from .utils import (
     allgather_for_tp,
     bwd_allreduce_for_tp,
+    dx_allreduce_async,
     fwd_allreduce_for_tp,
     get_local_channels,
     get_merge_shapes,
@@ -365,17 +366,19 @@ class DistributedAttentionLayer(DistributedModule):
             self._note_causal_mask(mask)
         if self._mem:
             return self._core_memory(a, mask)
-        a = (bwd_allreduce_for_tp(a, inplace_grad=True) if self._tp > 1 else a)
+        # speed mode: the QKV GEMM's backward all-reduces dX itself, asynchronously, while it
+        # computes the weight gradient (reference: the bwd all-reduce of `nn/utils.py:570`)
+        ar = dx_allreduce_async if self._tp > 1 else None
         B, s, _ = a.shape
         lh, d = self.local_heads, self.attention_head_size
         if self.cross_attention:
-            q = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, lh, d)
+            q = linear(a, self.qkv_weight, self.qkv_bias, dx_allreduce=ar).view(B, s, lh, d)
             c = (bwd_allreduce_for_tp(cross_states) if self._tp > 1 else cross_states)
             kv = linear(c, self.kv_weight, self.kv_bias).view(B, c.shape[1], 2, lh, d)
             k, v = kv[:, :, 0], kv[:, :, 1]
             causal, mask = False, cross_mask
         else:
-            qkv = linear(a, self.qkv_weight, self.qkv_bias).view(B, s, 3, lh, d)
+            qkv = linear(a, self.qkv_weight, self.qkv_bias, dx_allreduce=ar).view(B, s, 3, lh, d)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
             if not self.rotary_dim and not self.attention_in_fp32:
@@ -540,8 +543,8 @@ class DistributedTransformerOutputLayer(DistributedModule):
             x = _activation(x, self.activation, None, self._tanh_gelu)
             out = linear(x, self.dense2_weight, self.dense2_bias)
             return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
-        m = (bwd_allreduce_for_tp(m, inplace_grad=True) if self._tp > 1 else m)
-        x = linear(m, self.dense1_weight)
+        # dense1's backward all-reduces dX asynchronously behind its weight-gradient GEMM
+        x = linear(m, self.dense1_weight, dx_allreduce=dx_allreduce_async if self._tp > 1 else None)
         x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu)
         out = linear(x, self.dense2_weight, self.dense2_bias)
         return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)

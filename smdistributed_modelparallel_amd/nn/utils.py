@@ -253,6 +253,17 @@ class _BwdAllreduce(torch.autograd.Function):
         return _allreduce(g, inplace=ctx.inplace), None
 
 
+def dx_allreduce_async(dx):
+    """Input-gradient all-reduce of a column-parallel layer, started without waiting (the
+    layer's backward runs its weight-gradient GEMM, then waits).  dx is a fresh gradient:
+    reduced in place."""
+    if tp_size() == 1:
+        return None
+    if not dx.is_contiguous():
+        raise RuntimeError("dx_allreduce_async: the input gradient must be contiguous")
+    return oneshot.all_reduce(dx, group=tp_group(), async_op=True)
+
+
 class _Allgather(torch.autograd.Function):
     """fwd all-gather along dim; bwd narrow (each rank keeps its own slice)."""
 

@@ -211,17 +211,33 @@ def _wgrad_native_ok(g, dy2, x2):
             and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
+# Fixed picks (SMP_WGRAD_PICK=static, or torch.use_deterministic_algorithms(True)): the
+# per-shape winners measured on MI355X at T = 65536 (profiles/r2/session4_wgrad_pick_ab.md),
+# keyed by (N, K); other shapes use the library GEMM.  No timing trials, no host sync in the
+# backward, and the same split-K accumulation order in every run and on every rank.
+_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7}
+_WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "time")
+
+
+def _wgrad_static_pick(dy2, x2):
+    return _WGRAD_STATIC.get((dy2.shape[1], x2.shape[1]), 0) if dy2.shape[0] >= 16384 else 0
+
+
 def _wgrad_kernel_splits(g, dy2, x2):
     """Split count for the MFMA kernel at this (T, N, K, dtypes), or 0 for the library GEMM.
 
     Timed once per shape: the kernel at its occupancy-model split count and at a few smaller
-    counts (fewer fp32 partials to reduce; the model ignores that traffic), and the library."""
+    counts (fewer fp32 partials to reduce; the model ignores that traffic), and the library.
+    ``SMP_WGRAD_PICK=static`` or deterministic algorithms: the fixed table above instead."""
     if _WGRAD_KERNEL == "1" or g.dtype != dy2.dtype:  # (fp32 accumulators: no library equivalent)
         return -1  # kernel, default split count
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype, g.dtype)
     hit = _WGRAD_KERNEL_CHOICE.get(key)
     if hit is not None:
         return hit
+    if _WGRAD_PICK == "static" or torch.are_deterministic_algorithms_enabled():
+        _WGRAD_KERNEL_CHOICE[key] = _wgrad_static_pick(dy2, x2)
+        return _WGRAD_KERNEL_CHOICE[key]
     from ._ext import ext
 
     C = ext()
@@ -330,22 +346,41 @@ def _fusable(w):
             and g.is_contiguous())
 
 
+# SMP_TRACE_TP_OVERLAP=1 records the backward's order of (dX all-reduce start, weight
+# gradient, dX all-reduce wait) -- tests check that the weight gradient runs while the
+# tensor-parallel all-reduce of the input gradient is in flight
+TRACE_TP_OVERLAP = os.environ.get("SMP_TRACE_TP_OVERLAP", "0") == "1"
+TP_OVERLAP_TRACE = []
+
+
 class _LinearWGradAccum(torch.autograd.Function):
+    """y = x W^T + b with (a) the weight gradient accumulated by a GEMM straight into the
+    flat gradient buffer and (b) optionally the tensor-parallel all-reduce of the input
+    gradient (column-parallel layer of the speed mode; reference `nn/utils.py:548-570`
+    BackwardAllreduceForTP) issued asynchronously right after dX and waited for only after
+    the weight-gradient GEMM, so the two overlap."""
+
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, dx_allreduce=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias = bias
+        ctx.dx_allreduce = dx_allreduce
         ctx.wt = _transposed(weight) if _use_transposed(weight) else None
         return F.linear(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = db = None
+        dx = db = dw = None
+        work = None
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.needs_input_grad[0]:
             dx = F.linear(dy, ctx.wt) if ctx.wt is not None else torch.matmul(dy, w)
+            if ctx.dx_allreduce is not None:
+                work = ctx.dx_allreduce(dx)  # fresh tensor: reduced in place, async when large
+                if TRACE_TP_OVERLAP:
+                    TP_OVERLAP_TRACE.append("dx_allreduce_start")
         if ctx.has_bias and ctx.needs_input_grad[2]:
             if _fusable(ctx.bias) and dy2.is_cuda:
                 _col_sum(dy2, ctx.bias.grad)  # into the bound flat-buffer view (no temp + add)
@@ -362,12 +397,23 @@ class _LinearWGradAccum(torch.autograd.Function):
                     _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]))
             else:
                 # grad slot re-bound/removed since forward: hand the gradient to autograd
-                return dx, dy2.t().mm(x.reshape(-1, x.shape[-1])), db
-        return dx, None, db
+                dw = dy2.t().mm(x.reshape(-1, x.shape[-1]))
+            if TRACE_TP_OVERLAP:
+                TP_OVERLAP_TRACE.append("wgrad")
+        if work is not None:
+            work.wait()
+            if TRACE_TP_OVERLAP:
+                TP_OVERLAP_TRACE.append("dx_allreduce_wait")
+        return dx, dw, db, None
 
 
-def linear(x, weight, bias=None):
-    """F.linear with GEMM-fused weight-gradient accumulation into the flat grad buffer."""
+def linear(x, weight, bias=None, dx_allreduce=None):
+    """F.linear with GEMM-fused weight-gradient accumulation into the flat grad buffer.
+    ``dx_allreduce(dx) -> work | None``: the column-parallel layer's input-gradient
+    all-reduce, overlapped with the weight-gradient GEMM (the caller then applies no
+    separate backward all-reduce to x)."""
+    if torch.is_grad_enabled() and (weight.requires_grad or x.requires_grad) and dx_allreduce is not None:
+        return _LinearWGradAccum.apply(x, weight, bias, dx_allreduce)
     if torch.is_grad_enabled() and weight.requires_grad and _fusable(weight):
-        return _LinearWGradAccum.apply(x, weight, bias)
+        return _LinearWGradAccum.apply(x, weight, bias, None)
     return F.linear(x, weight, bias)

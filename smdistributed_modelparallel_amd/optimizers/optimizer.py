@@ -506,7 +506,8 @@ class DistributedOptimizer:
                 raise SMPInvalidArgumentError("reference optimizer state: fp32_from_fp16 groups do not match the "
                                               "optimizer's parameter groups")
             for g, ms in zip(self._orig_param_groups, masters):
-                lowp = [p for p in g["params"] if p.dtype in (torch.float16, torch.bfloat16)]
+                # the reference builds fp32_from_fp16 from trainable params only (fp16_optimizer.py:45)
+                lowp = [p for p in g["params"] if p.dtype in (torch.float16, torch.bfloat16) and p.requires_grad]
                 if len(lowp) != len(ms):
                     raise SMPInvalidArgumentError("reference optimizer state: fp32_from_fp16 does not match the "
                                                   "low-precision parameters of a group")
@@ -535,8 +536,16 @@ class DistributedOptimizer:
                 steps[gidx[p]] = max(steps[gidx[p]], int(float(st["step"])))
             elif "m" in piece:  # torch SGD keeps no step: a momentum buffer means >= 1 step taken
                 steps[gidx[p]] = max(steps[gidx[p]], 1)
-        return {"format": "smp_amd_per_param_v1", "kind": self.kind, "params": params, "step_count": steps,
-                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in inner.get("param_groups", [])]}
+        out = {"format": "smp_amd_per_param_v1", "kind": self.kind, "params": params, "step_count": steps,
+               "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in inner.get("param_groups", [])]}
+        # the fp16 wrapper's dynamic loss scale (reference `fp16/fp16.py:668-700`: "loss_scaler" with
+        # cur_scale / cur_iter / last_overflow_iter): carried over when readable, else it restarts
+        ls = sd.get("loss_scaler") if masters is not None else None
+        cur = getattr(ls, "cur_scale", None) if ls is not None and not isinstance(ls, dict) else \
+            (ls.get("cur_scale") if isinstance(ls, dict) else None)
+        if cur is not None:
+            out["loss_scale"] = float(cur)
+        return out
 
     def load_state_dict(self, sd):
         if not self._built:
@@ -547,6 +556,8 @@ class DistributedOptimizer:
         self.load_local_optimizer_state_dict(sd)
         if "fp16_state" in sd:
             self.load_local_fp16_state_dict(sd["fp16_state"])
+        elif sd.get("loss_scale") is not None and self.loss_scaler is not None:
+            self.loss_scaler.cur_scale = float(sd["loss_scale"])  # a reference fp16 wrapper's scale
 
     def load_optimizer_checkpoint(self, sd):
         self.load_state_dict(sd)

@@ -151,9 +151,10 @@ def _instance(group):
     return _instances[k]
 
 
-def all_reduce(x, op=dist.ReduceOp.SUM, group=None):
+def all_reduce(x, op=dist.ReduceOp.SUM, group=None, async_op=False):
     """In-place all-reduce of x over group: one-shot IPC kernel for small contiguous GPU
-    tensors, ``dist.all_reduce`` otherwise."""
+    tensors, ``dist.all_reduce`` otherwise.  ``async_op=True`` returns the RCCL work handle
+    (None when the one-shot kernel ran: it is already ordered on the current stream)."""
     # the decision depends only on what every rank of the group shares (shape, dtype, op)
     if (x.is_cuda and x.dtype in _DTYPES and x.is_contiguous() and x.numel() * x.element_size() <= _MAX_BYTES
             and op in (dist.ReduceOp.SUM, dist.ReduceOp.MAX) and _MODE != "0"):
@@ -169,7 +170,9 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None):
                 t = x.clone()
                 inst.all_reduce(t, t, code, _TIMEOUT_S)
                 x.copy_(t)
-            return x
+            return None if async_op else x
+    if async_op:
+        return dist.all_reduce(x, op=op, group=group, async_op=True)
     dist.all_reduce(x, op=op, group=group)
     return x
 

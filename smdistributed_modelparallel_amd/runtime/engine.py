@@ -42,6 +42,18 @@ How it is built here (our design, not the reference's):
   orders are one feasible global execution.  ``static_mode`` turns this on without TP.
   With the IPC transport a tensor is pulled the moment its control message is dispatched,
   so the reference's pre-registered receptions (`:488`) have nothing left to pre-post.
+* **Fast mode** (``fast_mode``; reference `torch/serialization.py:365-473`, `step.py:150-230`,
+  `patches/execution.py:283,362`, `worker.py:329,397,473`): during microbatch 0 of a step
+  function's first step every parent records which stage / module call consumes each
+  output of a remote module call (``(call target, call count), output index``), local uses
+  included; the maps are merged over PP at the end of that step.  From then on a producer
+  whose output is consumed only by other children sends it STRAIGHT to the consuming
+  stage(s) ("dtx") and returns a dummy to the parent -- a meta-device tensor, so any real
+  use by the parent fails loudly.  Passing the dummy on to the consumer sends a
+  ``DirectStub``; the consumer resolves it from what it received out of band (waiting if
+  the parent's request overtook the tensor), and the consumer's input gradient goes
+  straight back to the producing stage ("dout").  A dummy that reaches a call the maps do
+  not name raises ``NotSupportedByFastModeError(graph_change=True)``.
 """
 import os
 import time
@@ -54,12 +66,13 @@ from greenlet import greenlet
 from ..backend.exceptions import (
     MissingPathFromComputationToModuleOutputError,
     MissingPathFromModuleInputToModuleOutputError,
+    NotSupportedByFastModeError,
     PipelineParallelBWDError,
     SMPRuntimeError,
 )
 from ..backend.logger import get_logger
 from .pipeline import MbStatus, create_pipeline
-from .serialization import stubify, unstubify
+from .serialization import DirectStub, find_direct, iter_tensors, stubify, unstubify
 
 logger = get_logger()
 
@@ -106,12 +119,23 @@ class _Worker:
 
 
 class _MbState:
-    __slots__ = ("sent", "leaves", "out")
+    __slots__ = ("sent", "leaves", "out", "out_direct", "dleaves")
 
     def __init__(self):
         self.sent = {}
         self.leaves = {}
         self.out = {}
+        self.out_direct = {}  # (rid, mi) -> output tensor sent child-to-child   [fast mode producer]
+        self.dleaves = {}  # rid -> [(leaf, producer rank, ("dout", prid, mi))]  [fast mode consumer]
+
+
+class _FastMode:
+    """Per step function: consumer maps recorded on microbatch 0 of its first step."""
+    __slots__ = ("rec", "map")
+
+    def __init__(self):
+        self.rec = {}  # mi -> {(consumer pp_rank, call target, call count)}  (this rank's calls)
+        self.map = None  # merged over PP after the recording step: mi -> [(pp_rank, target, count)]
 
 
 class PipelineEngine:
@@ -134,6 +158,8 @@ class PipelineEngine:
 
     def reset_step(self):
         self.mbstate = {}
+        self._callcount = {}  # (mb, call target) -> calls so far (fast-mode call identity)
+        self._direct_in = {}  # (mb, mi) -> (tensor, producer rank, producer call id)
         self.tokens = {}
         self.waiting = {}  # wait key -> worker
         self.workers = []
@@ -183,6 +209,57 @@ class PipelineEngine:
         for r in self.core.get_pp_group():
             if r != me:
                 self._send(r, msg)
+
+    # ============================================================= fast mode
+    def _fm(self):
+        """(state, recording now, maps in use) for the running step function."""
+        cfg = self.state.cfg
+        sf = getattr(self, "step_fn", None)
+        if cfg is None or not cfg.fast_mode or sf is None or self.core.pp_size() == 1:
+            return None, False, False
+        fm = sf.__dict__.get("_fm")
+        if fm is None:
+            fm = sf.__dict__["_fm"] = _FastMode()
+        recording = sf.calls == 0 and self.state.microbatch == 0
+        return fm, recording, fm.map is not None
+
+    def fm_note_local(self, obj):
+        """Recording step: tensors of remote module outputs used on THIS rank (a local module
+        call, the step function's outputs, model.backward) must reach the parent for real."""
+        fm, recording, _ = self._fm()
+        if not recording:
+            return
+        me = self.core.pp_rank()
+        for t in iter_tensors(obj):
+            mi = getattr(t, "_smp_mi", None)
+            if mi is not None:
+                fm.rec.setdefault(mi, set()).add((me, None, None))
+
+    def _fm_merge(self, step_fn):
+        """End of the recording step (every rank, symmetric): merge the consumer maps over PP."""
+        fm = step_fn.__dict__.get("_fm")
+        if fm is None or fm.map is not None:
+            return
+        from ..backend.collectives import CommGroup
+
+        merged = {}
+        for rec in self.state.comm.allgather(fm.rec, CommGroup.PP_GROUP):
+            for mi, cons in rec.items():
+                merged.setdefault(mi, set()).update(cons)
+        fm.map = {mi: sorted(c, key=repr) for mi, c in merged.items()}
+        logger.info(f"fast mode: direct-consumer maps merged for step function {step_fn.id} "
+                    f"({len(fm.map)} module outputs)")
+
+    def _dummy_stub(self, fm, t, owner_pp, target, count):
+        """Parent side: a fast-mode dummy passed on to a remote call becomes a DirectStub."""
+        if t.device.type != "meta":
+            return None
+        mi = getattr(t, "_smp_mi", None)
+        if mi is None:
+            raise NotSupportedByFastModeError(detail="a tensor transmitted child-to-child was transformed by the parent")
+        if (owner_pp, target, count) not in (fm.map or {}).get(mi, ()):
+            raise NotSupportedByFastModeError(graph_change=True, detail=f"{mi} reached {target} #{count}")
+        return DirectStub(mi, t.shape, t.dtype, t.requires_grad)
 
     # ============================================================== run_step
     def run_step(self, step_fn, mb_inputs):
@@ -243,6 +320,8 @@ class PipelineEngine:
 
     def after_step(self, step_fn, seconds):
         """Called on every rank after every pipelined step (symmetric collectives)."""
+        if self.state.cfg.fast_mode:
+            self._fm_merge(step_fn)
         if not self.replay_enabled():
             return
         sid = step_fn.id
@@ -338,6 +417,8 @@ class PipelineEngine:
             return (kind, self.core.ranker.get_pp_rank(src), stubbed[1])
         if kind == "mbdone":
             return (kind, stubbed[1])
+        if kind == "dtx":
+            return (kind, stubbed[1], stubbed[2])
         return (kind,)
 
     def _announce(self, key, mb=None):
@@ -354,7 +435,7 @@ class PipelineEngine:
         src, stubbed, tensors = m
         if stubbed[0] not in ("abort", "dec"):
             kind = stubbed[0]
-            mb = stubbed[2] if kind in ("fwd", "res", "bwd") else (stubbed[1] if kind == "mbdone" else None)
+            mb = stubbed[2] if kind in ("fwd", "res", "bwd") else (stubbed[1] if kind in ("mbdone", "dtx") else None)
             self._announce(self._event_key(src, stubbed), mb)
         self._dispatch(src, stubbed, tensors)
 
@@ -533,6 +614,13 @@ class PipelineEngine:
             self._process_bwd(src, key, mb, grads, remote_token)
         elif kind == "ack":
             self._ack(stubbed[1])
+        elif kind == "dtx":
+            # fast mode: a module output sent straight from its producer to this consumer
+            _, mb, mi, prid = stubbed
+            self._direct_in[(mb, mi)] = (tensors[0], src, prid)
+            w = self.waiting.pop(("dtx", mb, mi), None)
+            if w is not None:
+                self._resume(w, None)
         elif kind == "mbdone":
             _, mb, out_stubbed = stubbed
             self.results[mb] = unstubify(out_stubbed, tensors)
@@ -559,6 +647,7 @@ class PipelineEngine:
         self._spawn(run, mb, "root")
 
     def _finish_microbatch(self, mb, out):
+        self.fm_note_local(out)
         self.pipeline.mark_done(mb)
         self.results[mb] = out
         self.mbstate.pop(mb, None)
@@ -584,20 +673,44 @@ class PipelineEngine:
         mb = st.microbatch
         rid = self._new_id()
         grad_enabled = torch.is_grad_enabled()
-        stubbed, tensors = stubify(payload)
+        count = self._callcount.get((mb, target), 0)
+        self._callcount[(mb, target)] = count + 1
+        fm, recording, using = self._fm()
+        direct = None
+        if fm is not None:
+            owner_pp = self.core.ranker.get_pp_rank(owner)
+            if recording:
+                for t in iter_tensors(payload):
+                    mi = getattr(t, "_smp_mi", None)
+                    if mi is not None:
+                        fm.rec.setdefault(mi, set()).add((owner_pp, target, count))
+            if using:
+                def direct(t):
+                    return self._dummy_stub(fm, t, owner_pp, target, count)
+        stubbed, tensors = stubify(payload, direct)
         sent = []
         if grad_enabled:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
                 self._mb(mb).sent[rid] = sent
                 st.model._track_segment(sent)
-        st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled), tensors)
+        mi_base = (target, count) if fm is not None else None
+        st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled, mi_base),
+                          tensors)
         out_stubbed, out_tensors, holder, out_key = self._suspend(("res", rid))
         producer = target[1] if target[0] == "module" else f"{target[1]}[{target[2]}:]"
         return self._materialize_outputs(out_stubbed, out_tensors, holder, out_key, mb, grad_enabled, producer, sent)
 
     def _materialize_outputs(self, out_stubbed, tensors, holder, out_key, mb, grad_enabled, producer=None, sent=()):
         _, stubs = _stubs_of(out_stubbed)
+        dummies = {}
+        for d in find_direct(out_stubbed):
+            # fast mode: the real tensor went straight to its consumer(s); any real use here fails
+            t = torch.empty(d.shape, dtype=d.dtype, device="meta")
+            if d.requires_grad and grad_enabled:
+                t.requires_grad_(True)
+            t._smp_mi = d.mi
+            dummies[d.mi] = t
         rg_idx = [s.index for s in stubs if s.requires_grad] if grad_enabled else []
         if rg_idx:
             tensors = list(tensors)
@@ -611,15 +724,21 @@ class PipelineEngine:
                 tensors[i] = w
             if self._cur_worker is not None:
                 self._cur_worker.routs.append((wrapped[0], producer, sent))
-        return unstubify(out_stubbed, tensors)
+        for st_ in stubs:
+            if st_.mi is not None:
+                if not isinstance(tensors, list):
+                    tensors = list(tensors)
+                tensors[st_.index]._smp_mi = st_.mi
+        return unstubify(out_stubbed, tensors, dummies)
 
     def _exec_fwd(self, src, msg, tensors):
-        _, rid, mb, target, stubbed, reply_to, result_id, grad_enabled = msg
+        _, rid, mb, target, stubbed, reply_to, result_id, grad_enabled, mi_base = msg
         st = self.state
         st.microbatch = mb
         torch.set_grad_enabled(grad_enabled)
         _, stubs = _stubs_of(stubbed)
         tensors = list(tensors)
+        dvals = self._resolve_direct(stubbed, mb, rid, grad_enabled)
         leaves, leaf_idx = [], []
         if grad_enabled:
             for s in stubs:
@@ -631,19 +750,42 @@ class PipelineEngine:
                     leaf_idx.append(s.index)
             if leaves:
                 self._mb(mb).leaves[rid] = (leaves, src)
-        args, kwargs = unstubify(stubbed, tensors)
+        args, kwargs = unstubify(stubbed, tensors, dvals)
         mm = st.module_manager
         if target[0] == "module":
             module = mm.get_module(target[1])
             out = st.model._call_local(module, args, kwargs)
             if grad_enabled:
                 self.validate_frame(target[1], out, leaves, leaf_idx)
-            self._send_result(reply_to, result_id, mb, out, rid, grad_enabled)
+            self._send_result(reply_to, result_id, mb, out, rid, grad_enabled, mi_base)
         else:
             seq = mm.get_module(target[1])
-            h = self.run_chain(seq, target[2], args[0], reply_to, result_id, mb, rid, grad_enabled)
+            h = self.run_chain(seq, target[2], args[0], reply_to, result_id, mb, rid, grad_enabled, mi_base)
             if grad_enabled:
                 self.validate_frame(f"{target[1]}[{target[2]}:]", h, leaves, leaf_idx)
+
+    def _resolve_direct(self, stubbed, mb, rid, grad_enabled):
+        """Consumer side of fast mode: the tensors a request names by DirectStub, waiting for
+        any that has not arrived yet.  A tensor from another stage becomes a leaf whose
+        gradient goes straight back to its producer."""
+        directs = find_direct(stubbed)
+        if not directs:
+            return None
+        me = self.core.rank()
+        out = {}
+        for d in directs:
+            ent = self._direct_in.get((mb, d.mi))
+            while ent is None:
+                self._suspend(("dtx", mb, d.mi))
+                ent = self._direct_in.get((mb, d.mi))
+            t, prod, prid = ent
+            if prod != me and grad_enabled and d.requires_grad:
+                leaf = t.detach()
+                leaf.requires_grad_(True)
+                self._mb(mb).dleaves.setdefault(rid, []).append((leaf, prod, ("dout", prid, d.mi)))
+                t = leaf
+            out[d.mi] = t
+        return out
 
     def validate_frame(self, name, out, leaves=(), leaf_idx=()):
         """Graph validation (reference `patches/execution.py:57-72`): every result of a
@@ -682,7 +824,7 @@ class PipelineEngine:
         if self._cur_worker is not None:
             self._cur_worker.routs = []
 
-    def run_chain(self, seq, start, h, reply_to, result_id, mb, rid, grad_enabled):
+    def run_chain(self, seq, start, h, reply_to, result_id, mb, rid, grad_enabled, mi_base=None):
         """Execute seq's children from `start` while they are local; hand the rest to the
         next stage directly (child-to-child)."""
         mm = self.state.module_manager
@@ -694,7 +836,7 @@ class PipelineEngine:
             j += 1
         h = self.state.model._run_local_chain(seq, children, i, j, h)
         if j == len(children):
-            self._send_result(reply_to, result_id, mb, h, rid, grad_enabled)
+            self._send_result(reply_to, result_id, mb, h, rid, grad_enabled, mi_base)
             return h
         nxt = self._pp_peer(mm.get_partition(children[j]))
         rid2 = self._new_id()
@@ -705,13 +847,18 @@ class PipelineEngine:
                 self._mb(mb).sent[rid2] = sent
                 self.state.model._track_segment(sent)
         self.state.transport.send(
-            nxt, ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled),
+            nxt,
+            ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled,
+             mi_base),
             tensors,
         )
         return h
 
-    def _send_result(self, reply_to, result_id, mb, out, rid, grad_enabled):
-        stubbed, tensors = stubify(out)
+    def _send_result(self, reply_to, result_id, mb, out, rid, grad_enabled, mi_base=None):
+        if mi_base is None:
+            stubbed, tensors = stubify(out)
+        else:
+            stubbed, tensors = self._stubify_result(reply_to, mb, out, rid, grad_enabled, mi_base)
         if grad_enabled:
             rg = [t for t in tensors if t.requires_grad]
             if rg:
@@ -726,9 +873,52 @@ class PipelineEngine:
         else:
             self.state.transport.send(reply_to, msg, tensors)
 
+    def _stubify_result(self, reply_to, mb, out, rid, grad_enabled, mi_base):
+        """Fast mode, producer side: outputs tagged with their module info; once the consumer
+        maps are merged, an output consumed only by OTHER children goes straight to them
+        ("dtx") and the parent gets a DirectStub (reference `serialization.py:365-473`)."""
+        fm, _, using = self._fm()
+        order = {id(t): k for k, t in enumerate(iter_tensors(out))}
+        direct_to = {}
+        if using:
+            parent_pp = self.core.ranker.get_pp_rank(reply_to)
+            for t in iter_tensors(out):
+                mi = (mi_base, order[id(t)])
+                cons = fm.map.get(mi)
+                if cons and all(c[0] != parent_pp for c in cons):
+                    direct_to[id(t)] = (mi, sorted({c[0] for c in cons}))
+
+        def direct(t):
+            d = direct_to.get(id(t))
+            return None if d is None else DirectStub(d[0], t.shape, t.dtype, t.requires_grad)
+
+        stubbed, tensors = stubify(out, direct if direct_to else None)
+        _, stubs = _stubs_of(stubbed)
+        for st_ in stubs:
+            st_.mi = (mi_base, order[id(tensors[st_.index])])
+        if direct_to:
+            me = self.core.rank()
+            s = self._mb(mb)
+            for t in iter_tensors(out):
+                d = direct_to.get(id(t))
+                if d is None:
+                    continue
+                mi, pps = d
+                if grad_enabled and t.requires_grad:
+                    s.out_direct[(rid, mi)] = [t]
+                    self.state.model._track_segment([t])
+                for pp in pps:
+                    dst = self._pp_peer(pp)
+                    if dst == me:
+                        self._direct_in[(mb, mi)] = (t, me, rid)
+                    else:
+                        self.state.transport.send(dst, ("dtx", mb, mi, rid), [t])
+        return stubbed, tensors
+
     # --------------------------------------------------------------- backward
     def backward_root(self, tensors, grads):
         """model.backward() on pp_rank 0 inside a microbatch worker."""
+        self.fm_note_local(list(tensors))
         mb = self.state.microbatch
         # register the loss segment before the scheduler marks this microbatch's forward
         # done: the last microbatch's mark must never see an incomplete expected count
@@ -775,11 +965,19 @@ class PipelineEngine:
                 for l in leaves:
                     l.grad = None
                 self._send_bwd(provider, ("in", rid), mb, gs)
+        for lst in s.dleaves.values():
+            for leaf, producer, key in lst:
+                if leaf.grad is not None:
+                    g, leaf.grad = leaf.grad, None
+                    self._send_bwd(producer, key, mb, [g])
 
     def _process_bwd(self, src, key, mb, grads, remote_token):
         s = self._mb(mb)
-        kind, rid = key
-        saved = s.sent.get(rid) if kind == "in" else s.out.get(rid)
+        kind, rid = key[0], key[1]
+        if kind == "dout":  # fast mode: a consumer's gradient for an output sent child-to-child
+            saved = s.out_direct.get((rid, key[2]))
+        else:
+            saved = s.sent.get(rid) if kind == "in" else s.out.get(rid)
         if saved is None:
             raise PipelineParallelBWDError(f"no saved tensors for {key} (mb {mb}) on rank {self.core.rank()}")
         tid = self._new_token(src, remote_token, mb)

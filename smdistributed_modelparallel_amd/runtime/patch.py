@@ -40,6 +40,8 @@ def _dist_forward(module, *args, **kwargs):
         return _maybe_checkpointed(module, _orig(module), args, kwargs)
     mm = st.module_manager
     if mm.get_partition(module) == st.core.pp_rank():
+        if st.cfg.fast_mode:
+            st.engine.fm_note_local((args, kwargs))  # fast mode: a local consumer of remote outputs
         return _maybe_checkpointed(module, _orig(module), args, kwargs)
     return st.engine.remote_module_call(module, args, kwargs)
 
@@ -81,6 +83,8 @@ def _seq_forward(seq, inp):
     me = st.core.pp_rank()
     if mm.get_partition(seq) != me:
         return st.engine.remote_module_call(seq, (inp,), {})
+    if st.cfg.fast_mode and children and mm.get_partition(children[0]) == me:
+        st.engine.fm_note_local(inp)
     i, h = 0, inp
     while i < len(children):
         if mm.get_partition(children[i]) == me:

@@ -13,7 +13,8 @@ import torch
 
 
 class TensorStub:
-    __slots__ = ("index", "shape", "dtype", "requires_grad", "device_type", "holder_key")
+    # mi: fast-mode module info of a module output ((call target, call count), output index)
+    __slots__ = ("index", "shape", "dtype", "requires_grad", "device_type", "mi")
 
     def __init__(self, index, shape, dtype, requires_grad, device_type):
         self.index = index
@@ -21,16 +22,40 @@ class TensorStub:
         self.dtype = dtype
         self.requires_grad = requires_grad
         self.device_type = device_type
-        self.holder_key = None
+        self.mi = None
 
     def __getstate__(self):
-        return (self.index, self.shape, self.dtype, self.requires_grad, self.device_type, self.holder_key)
+        return (self.index, self.shape, self.dtype, self.requires_grad, self.device_type, self.mi)
 
     def __setstate__(self, s):
-        self.index, self.shape, self.dtype, self.requires_grad, self.device_type, self.holder_key = s
+        self.index, self.shape, self.dtype, self.requires_grad, self.device_type, self.mi = s
 
     def __repr__(self):
         return f"TensorStub({self.index}, {self.shape}, {self.dtype}, rg={self.requires_grad})"
+
+
+class DirectStub:
+    """A tensor that does not travel in this message (fast mode, reference
+    `smp/torch/serialization.py:365-473` child-to-child transmission): ``mi`` names the
+    module output it stands for; the tensor itself went straight from the producing stage
+    to the consuming one.  At the parent it becomes a dummy (meta-device) tensor; passed on
+    to the consumer it is resolved from the tensors received out of band."""
+    __slots__ = ("mi", "shape", "dtype", "requires_grad")
+
+    def __init__(self, mi, shape, dtype, requires_grad):
+        self.mi = mi
+        self.shape = tuple(shape)
+        self.dtype = dtype
+        self.requires_grad = requires_grad
+
+    def __getstate__(self):
+        return (self.mi, self.shape, self.dtype, self.requires_grad)
+
+    def __setstate__(self, s):
+        self.mi, self.shape, self.dtype, self.requires_grad = s
+
+    def __repr__(self):
+        return f"DirectStub({self.mi}, {self.shape}, {self.dtype})"
 
 
 def _map(obj, fn, memo):
@@ -72,8 +97,9 @@ def _map(obj, fn, memo):
     return out
 
 
-def stubify(obj):
-    """Returns (structure with TensorStubs, list of tensors)."""
+def stubify(obj, direct=None):
+    """Returns (structure with TensorStubs, list of tensors).  ``direct(t)`` may return a
+    ``DirectStub`` for a tensor that must not travel in this message (fast mode)."""
     tensors = []
     seen = {}
 
@@ -81,18 +107,55 @@ def stubify(obj):
         key = id(t)
         if key in seen:
             return seen[key]
-        stub = TensorStub(len(tensors), t.shape, t.dtype, t.requires_grad, t.device.type)
-        tensors.append(t)
+        stub = direct(t) if direct is not None else None
+        if stub is None:
+            stub = TensorStub(len(tensors), t.shape, t.dtype, t.requires_grad, t.device.type)
+            tensors.append(t)
         seen[key] = stub
         return stub
 
     return _map(obj, fn, {}), tensors
 
 
-def unstubify(obj, tensors):
+def find_direct(stubbed):
+    """Every DirectStub in a stubbed structure (in traversal order, unique by module info)."""
+    found = {}
+
+    def walk(o, memo):
+        if isinstance(o, DirectStub):
+            found.setdefault(o.mi, o)
+            return
+        if isinstance(o, TensorStub):
+            return
+        oid = id(o)
+        if oid in memo:
+            return
+        memo.add(oid)
+        if isinstance(o, (list, tuple, set)):
+            for x in o:
+                walk(x, memo)
+        elif isinstance(o, dict):
+            for x in o.values():
+                walk(x, memo)
+        elif hasattr(o, "__dict__") and not isinstance(o, type) and not callable(o):
+            for x in vars(o).values():
+                walk(x, memo)
+
+    walk(stubbed, set())
+    return list(found.values())
+
+
+def unstubify(obj, tensors, direct=None):
+    """Inverse of stubify; ``direct`` maps a DirectStub's module info to its tensor."""
     def walk(o, memo):
         if isinstance(o, TensorStub):
             return tensors[o.index]
+        if isinstance(o, DirectStub):
+            if direct is None or o.mi not in direct:
+                from ..backend.exceptions import SMPRuntimeError
+
+                raise SMPRuntimeError(f"fast mode: no tensor for {o!r}")
+            return direct[o.mi]
         oid = id(o)
         if oid in memo:
             return memo[oid]

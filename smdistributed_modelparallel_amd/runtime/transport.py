@@ -194,12 +194,12 @@ class PipelineTransport:
     def send(self, dst, stubbed, tensors):
         meta, rccl, exported = [], [], []
         for t in tensors:
+            nbytes = t.numel() * t.element_size()
+            self.bytes_sent += nbytes
             if not t.is_cuda:
                 meta.append(("cpu", t.detach()))
                 continue
             t = t.detach()
-            nbytes = t.numel() * t.element_size()
-            self.bytes_sent += nbytes
             if self.mode == "ipc":
                 t = t.contiguous()
                 rec = tuple(self._ipc.export_tensor(t))
@@ -280,8 +280,10 @@ class PipelineTransport:
     def _materialize(self, src, m):
         kind = m[0]
         if kind == "cpu":
+            self.bytes_recv += m[1].numel() * m[1].element_size()
             return m[1]
         if kind == "host":
+            self.bytes_recv += m[1].numel() * m[1].element_size()
             return m[1].to(self.device, non_blocking=False)
         if kind == "ipc":
             _, shape, dtype, rec = m

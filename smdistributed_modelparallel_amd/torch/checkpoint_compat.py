@@ -15,8 +15,10 @@ has identical names.
 
 ``model.load_state_dict`` recognises a reference-layout dict by its keys and converts it
 automatically; ``to_reference_state_dict`` produces the reference layout for export.
-Optimizer states of the reference (torch per-index states of its fp16/fp32 wrapper) are not
-converted: resume them with a fresh optimizer.
+Optimizer states of the reference (the wrapped torch optimizer's per-index state, inside the
+fp16 wrapper with its ``fp32_from_fp16`` masters and dynamic loss scale when present) are
+converted by ``DistributedOptimizer.load_state_dict`` (`optimizers/optimizer.py`,
+``_from_reference_format``): moments, masters, step counts and the loss scale carry over.
 """
 import re
 

@@ -822,15 +822,55 @@ class DistributedModel(nn.Module):
         self.module.cpu()
         return self
 
-    def cuda(self, *args, **kwargs):
-        if not self.partitioned:
-            logger.warning("model.cuda() before partitioning is ignored; local modules move after partitioning")
-        return self
+    def cuda(self, device=None):
+        return self.to(device=torch.device("cuda") if device is None else torch.device("cuda", device)
+                       if isinstance(device, int) else device)
 
     def to(self, *args, **kwargs):
+        """Reference `patches/moves.py:110-130` (``distributed_to``): before partitioning the
+        DEVICE part of the request is dropped with a warning (every module moves to its own
+        stage's GPU when the partition is known) and a dtype cast applies to the whole model;
+        after partitioning local modules already live on this rank's device and remote ones
+        hold no storage, so a device request is a no-op (warned when it names another
+        device), and a dtype cast is applied only when it changes nothing -- the local
+        parameters are views into flat data/gradient buffers the reducers and the optimizer
+        hold, so a real cast after partitioning raises instead of silently doing nothing
+        (configure ``bf16`` / ``fp16`` in ``smp.init`` or cast before ``DistributedModel``)."""
+        device, dtype, _non_blocking, _fmt = torch._C._nn._parse_to(*args, **kwargs)
         if not self.partitioned:
-            logger.warning("model.to() before partitioning is ignored; local modules move after partitioning")
+            if device is not None:
+                logger.warning("model.to(device) before partitioning is ignored: local modules move to this rank's "
+                               "device once the model is partitioned")
+            if dtype is not None:
+                self.module.to(dtype=dtype)
+            return self
+        if device is not None:
+            want = torch.device(device)
+            have = state.device
+            if want.type != have.type or (want.index is not None and want.index != have.index):
+                logger.warning(f"model.to({want}) after partitioning is ignored: this rank's modules stay on {have}")
+        if dtype is not None:
+            local = [p for _, p in self.local_named_parameters() if p.is_floating_point()]
+            if any(p.dtype != dtype for p in local):
+                from ..backend.exceptions import SMPUnsupportedError
+
+                raise SMPUnsupportedError(
+                    f"casting a partitioned model to {dtype}: its parameters live in flat data/gradient buffers "
+                    "owned by the reducers and the optimizer; set 'bf16' / 'fp16' in smp.init or cast the module "
+                    "before smp.DistributedModel")
         return self
+
+    def half(self):
+        return self.to(torch.float16)
+
+    def bfloat16(self):
+        return self.to(torch.bfloat16)
+
+    def float(self):
+        return self.to(torch.float32)
+
+    def double(self):
+        return self.to(torch.float64)
 
 
 @contextlib.contextmanager

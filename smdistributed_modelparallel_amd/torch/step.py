@@ -71,6 +71,7 @@ class StepFunction:
         self.splitter = PTTensorSplitter(func, non_split_inputs, input_split_axes)
         self.detach_outputs = detach_outputs
         self.memory_metrics = StepMemoryMetricsCollector()
+        self.calls = 0  # completed calls (fast mode records its consumer maps on the first)
         state.step_func[self.id] = self
 
     def __call__(self, *args, **kwargs):
@@ -100,6 +101,7 @@ class StepFunction:
             core.timeline_end_step()
         if core.pp_size() > 1 and state.model.partitioned:
             state.engine.after_step(self, time.perf_counter() - t0)
+            self.calls += 1
         state.step_count += 1
         if state.model.partitioned:
             self._upload_metrics_once()

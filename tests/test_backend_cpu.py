@@ -459,3 +459,56 @@ def test_dropped_model_is_freed(tmp_path):
     r = subprocess.run([sys.executable, "-c", _LEAK_CODE], cwd=tmp_path, env=env, capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 0 and "LEAK_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+_MOVES_CODE = r"""
+import logging, torch
+import smdistributed_modelparallel_amd.torch as smp
+from smdistributed_modelparallel_amd.backend.exceptions import SMPUnsupportedError
+from smdistributed_modelparallel_amd.models import build_gpt, gpt_inputs
+smp.init({"microbatches": 1})
+model = smp.DistributedModel(build_gpt("gpt2-tiny", dropout=0.0, num_layers=2))
+if not model.partitioned:
+    # before partitioning: the dtype part of to() applies, the device part is dropped
+    model.to("cuda:5", torch.float64)
+    assert all(p.dtype == torch.float64 for p in model.get_module().parameters())
+    model.to(torch.float32)
+opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=1e-3))
+
+@smp.step
+def train(model, ids, labels):
+    loss, _ = model((ids, None, None, None, labels))
+    model.backward(loss)
+    return loss
+
+ids, _, _, _, labels = gpt_inputs(2, 16, 512, smp.state.device)
+opt.zero_grad(); train(model, ids, labels); opt.step()
+assert model.partitioned
+# after partitioning: a device request is a no-op, a no-change dtype request too
+assert model.to("cuda:3") is model and model.cuda() is model and model.float() is model
+for bad in (lambda: model.to(torch.float16), lambda: model.half(), lambda: model.bfloat16()):
+    try:
+        bad()
+    except SMPUnsupportedError:
+        pass
+    else:
+        raise AssertionError("a real cast after partitioning must raise")
+assert all(p.dtype == torch.float32 for p in model.get_module().parameters() if p.numel())
+opt.zero_grad(); train(model, ids, labels); opt.step()
+print("MOVES_OK")
+"""
+
+
+def test_distributed_model_to_cuda_semantics(tmp_path):
+    """Reference `patches/moves.py:110-130`: device moves are dropped before partitioning (dtype
+    casts apply) and are no-ops after it; a dtype change after partitioning raises instead of
+    being silently ignored (the parameters live in flat buffers)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SMP_FORCE_CPU="1", PYTHONPATH=root, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29000 + (os.getpid() + 7) % 1000))
+    r = subprocess.run([sys.executable, "-c", _MOVES_CODE], cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "MOVES_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

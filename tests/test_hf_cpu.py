@@ -51,6 +51,24 @@ def test_gpt2_parity():
     _lm_parity(GPT2LMHeadModel(cfg), gpt2, 97)
 
 
+@pytest.mark.parametrize("scale_attn_weights,reorder_and_upcast_attn,by_layer", [
+    (False, False, False), (True, True, False), (True, True, True), (True, False, True)])
+def test_gpt2_attention_config_flags_parity(scale_attn_weights, reorder_and_upcast_attn, by_layer):
+    """Non-default score scaling / upcast fields of the HF GPT-2 config reach the smp modules
+    (reference `torch/nn/huggingface/gpt2.py:75-78`): same logits as HF."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import gpt2
+
+    cfg = GPT2Config(n_layer=2, n_embd=64, n_head=4, vocab_size=97, n_positions=32, bos_token_id=0, eos_token_id=0,
+                     scale_attn_weights=scale_attn_weights, reorder_and_upcast_attn=reorder_and_upcast_attn,
+                     scale_attn_by_inverse_layer_idx=by_layer)
+    kw = gpt2.config_to_kwargs(cfg)
+    assert kw["scale_attention_scores"] == scale_attn_weights
+    assert kw["attention_in_fp32"] == kw["query_key_layer_scaling"] == reorder_and_upcast_attn
+    _lm_parity(GPT2LMHeadModel(cfg), gpt2, 97)
+
+
 def test_gptj_parity():
     from transformers import GPTJConfig, GPTJForCausalLM
 

@@ -51,6 +51,12 @@ def test_tp2():
     _run(2, 1, 2, 1)
 
 
+def test_tp2_dx_allreduce_overlaps_weight_gradient():
+    """Speed-mode column-parallel layers (QKV, dense1): the input-gradient all-reduce is
+    issued asynchronously and waited for only after the weight-gradient GEMM."""
+    _run(2, 1, 2, 1, extra={"check_tp_overlap": True}, env={"SMP_TRACE_TP_OVERLAP": "1"})
+
+
 def test_tp2_uneven_heads():
     _run(2, 1, 2, 2, extra={"model": {"num_attention_heads": 3, "attention_head_size": 16, "hidden_size": 48,
                                       "intermediate_size": 96}})
@@ -249,3 +255,34 @@ def test_display_partition_truncated_tree():
                        timeout=200)
     assert all("OK" in o for o in outs)
     assert "DISPLAY main: 0" in outs[0]
+
+
+def _fast_bytes(outs, rank):
+    import re
+
+    m = re.search(rf"rank {rank} OK bytes_per_step=([\d,]+)", "\n".join(outs))
+    assert m, outs
+    return [int(x) for x in m.group(1).split(",")]
+
+
+def test_pp4_fast_mode_modulelist_matches_and_skips_the_parent():
+    """HF-style ModuleList stack at PP=4: with fast_mode the block outputs go stage to stage
+    (after the recording step) and pp_rank 0 no longer relays them; losses and parameters
+    match the unpartitioned model either way (reference serialization.py:365-473)."""
+    slow = run_workers("fast_mode", 4, [4, 2, 3, 0], timeout=300)
+    fast = run_workers("fast_mode", 4, [4, 2, 3, 1], timeout=300)
+    s0, f0 = _fast_bytes(slow, 0), _fast_bytes(fast, 0)
+    # step 0 records (same traffic); afterwards the parent only sends the embedding output
+    # and receives the last block's output
+    assert f0[0] == s0[0]
+    assert f0[-1] < 0.35 * s0[-1], (f0, s0)
+    # the stages now talk to each other directly
+    assert _fast_bytes(fast, 2)[-1] > 0
+
+
+@pytest.mark.parametrize("mode", ["change", "misuse"])
+def test_pp4_fast_mode_errors(mode):
+    outs = run_workers("fast_mode", 4, [4, 2, 3, 1, mode], timeout=300)
+    assert all("OK" in o for o in outs)
+    if mode == "change":
+        assert "graph_change=True" in "\n".join(outs)

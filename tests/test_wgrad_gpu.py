@@ -108,3 +108,27 @@ def test_wgrad_auto_choice_accumulates_once(monkeypatch):
     assert len(L._WGRAD_KERNEL_CHOICE) == 1
     err = (g.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
+
+
+def test_wgrad_static_pick_is_deterministic(monkeypatch):
+    """SMP_WGRAD_PICK=static: the measured per-shape winner without timing trials; two runs
+    give bitwise identical gradients (same split-K accumulation order)."""
+    monkeypatch.setattr(L, "_WGRAD_PICK", "static")
+    T, N, K = 16384, 1600, 1600  # table entry: kernel, 5 splits
+    g0 = torch.Generator(device="cuda").manual_seed(3)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    base = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    key = (T, N, K, torch.bfloat16, torch.bfloat16)
+    L._WGRAD_KERNEL_CHOICE.pop(key, None)
+    outs = []
+    for _ in range(2):
+        g = base.clone()
+        L._wgrad_accumulate(g, dy, x)
+        outs.append(g)
+    assert L._WGRAD_KERNEL_CHOICE[key] == 5
+    assert torch.equal(outs[0], outs[1])
+    ref = base.float() + dy.float().t() @ x.float()
+    err = (outs[0].float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err
+    L._WGRAD_KERNEL_CHOICE.pop(key, None)

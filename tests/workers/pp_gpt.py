@@ -178,6 +178,16 @@ def main():
         # a subtree held by one partition is not expanded: no layer internals are listed
         assert not any(".attention" in x or "/attention" in x for x in lines), lines
         print("\n".join("DISPLAY " + x for x in lines[1:]), flush=True)
+    if extra.get("check_tp_overlap"):
+        from smdistributed_modelparallel_amd.ops import linear as lin
+
+        tr = lin.TP_OVERLAP_TRACE
+        starts = [i for i, e in enumerate(tr) if e == "dx_allreduce_start"]
+        assert starts, tr[:20]
+        for i in starts:
+            # the weight gradient runs while the dX all-reduce is in flight, then the wait
+            assert tr[i + 1:i + 3] == ["wgrad", "dx_allreduce_wait"], (i, tr[i:i + 3])
+        print(f"rank {smp.rank()} tp overlap: {len(starts)} dX all-reduces overlapped with wgrad", flush=True)
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
 
