@@ -56,3 +56,10 @@ def test_pp4_ipc_selfcheck_forced_failure_falls_back_to_host():
     # fallback (host staging, the process groups being gloo) and still train exactly
     env = {"SMP_P2P": "", "SMP_P2P_SELFCHECK_FAIL": "2"}
     _run(4, 4, 4, extra={"expect_mode": "host", "model": {"num_layers": 4}}, env=env)
+
+
+def test_pp4_fast_mode_ipc():
+    """Fast mode with the IPC transport: block outputs of a ModuleList stack go stage to stage
+    (gated sends, comm-stream pulls) and match the unpartitioned model."""
+    outs = run_workers("fast_mode", 4, [4, 2, 3, 1], timeout=110, env_extra=dict(_ENV))
+    assert all("OK" in o for o in outs)

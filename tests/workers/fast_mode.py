@@ -62,8 +62,10 @@ def main():
     smp.init({"pipeline_parallel_degree": pp, "microbatches": mbs, "pipeline": "interleaved",
               "auto_partition": False, "default_partition": 0, "fast_mode": fast,
               "ddp": int(os.environ["WORLD_SIZE"]) > pp})
+    dev = smp.state.device
     net = ListModel()
     net.load_state_dict(ref.state_dict())
+    ref.to(dev)
     n = len(net.blocks)
     for i, blk in enumerate(net.blocks):  # embedding + head stay with the parent on stage 0
         smp.set_partition(blk, min(pp - 1, 1 + (i * (pp - 1)) // n) if pp > 1 else 0)
@@ -81,7 +83,7 @@ def main():
     g = torch.Generator().manual_seed(3)
     bytes_per_step = []
     for it in range(steps):
-        ids = torch.randint(0, 64, (2 * mbs, 12), generator=g)
+        ids = torch.randint(0, 64, (2 * mbs, 12), generator=g).to(dev)
         if it == 1 and mode == "change":
             model.get_module().skip = 5
         if it == 1 and mode == "misuse":
@@ -114,12 +116,12 @@ def main():
         ropt.step()
         if smp.pp_rank() == 0:
             mine = float(out.reduce_mean())
-            assert abs(mine - rl.item()) < 1e-5, (it, mine, rl.item())
+            assert abs(mine - rl.item()) < (1e-5 if dev.type == "cpu" else 2e-4), (it, mine, rl.item())
     assert mode == "ok", f"{mode}: nothing raised"
     rp = dict(ref.named_parameters())
     for name, p in model.local_named_parameters():
         d = (p.detach() - rp[name].detach()).abs().max().item()
-        assert d < 1e-5, (name, d)
+        assert d < (1e-5 if dev.type == "cpu" else 5e-4), (name, d)
     print(f"rank {smp.rank()} OK bytes_per_step={','.join(str(b) for b in bytes_per_step)}", flush=True)
     smp.barrier()
 

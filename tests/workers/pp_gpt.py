@@ -29,6 +29,8 @@ def main():
     kw.update(extra.get("model", {}))
     ref = build_gpt("gpt2-tiny", dropout=0.0, **kw)  # built before init: unsharded reference
     smp.init(cfg)
+    dev = smp.state.device  # GPU runs (tests/test_hybrid_gpu.py): every rank on the box's one GPU
+    ref.to(dev)
     delayed = bool(extra.get("delayed"))
     with smp.delay_param_initialization(enabled=delayed):
         with smp.model_creation(tensor_parallelism=tp > 1):
@@ -36,12 +38,12 @@ def main():
     if delayed:
         assert all(p.is_meta for p in net.parameters())
     elif tp == 1:
-        net.load_state_dict(ref.state_dict())
+        net.load_state_dict({k: v.cpu() for k, v in ref.state_dict().items()})
     else:
         from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
 
         # distributed modules created under TP: copy the sliced reference weights
-        rsd = ref.state_dict()
+        rsd = {k: v.cpu() for k, v in ref.state_dict().items()}
         with torch.no_grad():
             for n, p in net.named_parameters():
                 full = rsd[n]
@@ -92,7 +94,7 @@ def main():
     my_dp = smp.rdp_rank() if prescaled else smp.dp_rank()
     local_bs = 2 * mbs
     for it in range(steps):
-        ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, 16), generator=g)
+        ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, 16), generator=g).to(dev)
         ids = ids_all[my_dp * local_bs:(my_dp + 1) * local_bs]
         opt.zero_grad()
         out = train(model, ids, ids)
@@ -138,7 +140,7 @@ def main():
         # entries equally gives the mean over shards and RDP replicas (the objective above)
         if smp.pp_rank() == 0 or True:
             avg = sum(all_l) / len(all_l)
-            assert abs(avg - ref_loss.item()) < 1e-4, (it, avg, ref_loss.item())
+            assert abs(avg - ref_loss.item()) < float(extra.get("loss_tol", 1e-4)), (it, avg, ref_loss.item())
     # parameter check (local, TP-sliced)
     from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
 
@@ -148,16 +150,17 @@ def main():
         # parameters are sharded: compare the gathered full state dict
         sd = model.state_dict(gather_to_rank0=False)
         for n, full in rp.items():
-            worst = max(worst, (sd[n].float() - full.detach().float()).abs().max().item())
+            worst = max(worst, (sd[n].float().cpu() - full.detach().float().cpu()).abs().max().item())
     for n, p in model.local_named_parameters():
         if p.numel() == 0:
             continue
-        full = rp[n].detach()
+        full = rp[n].detach().to(p.device)
         t = slice_for_param(full, p, smp.tp_rank(), smp.tp_size())
         d = (p.detach().float() - t.float()).abs().max().item()
         if d > worst:
             worst, worst_name = d, n
-    assert worst < 2e-4, (worst, worst_name if worst > 0 else None)
+    ptol = float(extra.get("param_tol", 2e-4))
+    assert worst < ptol, (worst, worst_name if worst > 0 else None)
     if extra.get("expect_hier") is not None:
         sdp = smp.state.sdp
         assert sdp.hier == extra["expect_hier"], (sdp.hier, extra["expect_hier"])
