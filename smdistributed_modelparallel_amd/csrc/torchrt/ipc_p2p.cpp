@@ -262,10 +262,26 @@ void register_ipc_p2p(py::module& m) {
       .def("stats", &IpcP2P::stats);
 }
 
+// Page-locks the storage of an ordinary CPU tensor in place (hipHostRegister): exact-size
+// pinned host memory for large optimizer-state arrays -- the caching pinned allocator rounds
+// every block up to a power of two, which at hundreds of GB costs tens of GB of host RAM.
+void host_register(const at::Tensor& t) {
+  TORCH_CHECK(t.device().is_cpu() && t.is_contiguous(), "host_register: a contiguous CPU tensor is required");
+  const size_t bytes = static_cast<size_t>(t.numel()) * t.element_size();
+  if (bytes == 0) return;
+  hip_check(hipHostRegister(t.data_ptr(), bytes, hipHostRegisterDefault), "hipHostRegister");
+}
+
+void host_unregister_ptr(uint64_t ptr) {
+  if (ptr != 0) (void)hipHostUnregister(reinterpret_cast<void*>(static_cast<uintptr_t>(ptr)));
+}
+
 void register_grad_tracker(py::module& m);
 void register_ipc_allreduce(py::module& m);
 
 void register_bindings(py::module& m) {
+  m.def("host_register", &host_register);
+  m.def("host_unregister_ptr", &host_unregister_ptr);
   register_grad_tracker(m);
   register_ipc_p2p(m);
   register_ipc_allreduce(m);

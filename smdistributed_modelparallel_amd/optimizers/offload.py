@@ -21,7 +21,9 @@ class OptimizerStateOffload:
     def __init__(self, domains, device):
         self.device = device
         n = max((d.numel for d in domains), default=0)
-        fields = [k for k in ("master", "m", "v") if domains and getattr(domains[0], k) is not None]
+        # the host-resident fields (SMP_OFFLOAD_OPTIMIZER_FIELDS); the rest stay in HBM
+        fields = [k for k in ("master", "m", "v")
+                  if domains and getattr(domains[0], k) is not None and not getattr(domains[0], k).is_cuda]
         self.fields = fields
         self.slots = [{k: torch.empty(n, dtype=torch.float32, device=device) for k in fields} for _ in range(2)]
         self.h2d = torch.cuda.Stream(device=device)
@@ -53,7 +55,7 @@ class OptimizerStateOffload:
                 up[i + 1] = self._upload(domains[i + 1], 1 - slot)
             comp.wait_event(up.pop(i))
             st = self.slots[slot]
-            views = tuple(st[k][: d.numel] if k in st else None for k in ("master", "m", "v"))
+            views = tuple(st[k][: d.numel] if k in st else getattr(d, k) for k in ("master", "m", "v"))
             update(d, views)
             done = torch.cuda.Event()
             done.record(comp)

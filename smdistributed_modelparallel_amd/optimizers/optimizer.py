@@ -15,6 +15,8 @@ chunk of each bucket when sharded).  For Adam/AdamW/SGD/Adagrad/LAMB the whole u
 is ONE fused HIP kernel per domain.  Any other torch optimizer runs through the same
 domains as fp32 "virtual parameters" (the reference's name for sharded master slices).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -64,6 +66,20 @@ class _Staged:
         self.master, self.m, self.v, self.upd, self.vparam = master, m, v, None, None
 
 
+def _pinned_full(n, fill):
+    """fp32 host array of exactly n elements, page-locked in place (hipHostRegister) so the
+    offload streams copy at PCIe rate without the pinned allocator's power-of-two rounding."""
+    import weakref
+
+    from ..ops._ext import ext
+
+    t = torch.full((n,), float(fill), dtype=torch.float32)
+    if n:
+        ext().host_register(t)
+        weakref.finalize(t, ext().host_unregister_ptr, t.data_ptr())
+    return t
+
+
 class DistributedOptimizer:
     def __init__(self, optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None):
         if state.model is None:
@@ -95,6 +111,12 @@ class DistributedOptimizer:
         self.offload = bool(getattr(cfg, "amd_offload_optimizer_state", False)) and state.use_gpu
         if self.offload and self.kind not in ("adam", "adamw", "sgd", "adagrad"):
             raise SMPInvalidArgumentError("amd_offload_optimizer_state supports Adam/AdamW/SGD/Adagrad")
+        # which fp32 fields live in pinned host memory (SMP_OFFLOAD_OPTIMIZER_FIELDS, default
+        # all three): e.g. "m,v" keeps the master weights in HBM and moves 8 B/param to the host
+        fields = os.environ.get("SMP_OFFLOAD_OPTIMIZER_FIELDS", "master,m,v")
+        self._offload_fields = {f.strip() for f in fields.split(",") if f.strip()} if self.offload else set()
+        if not self._offload_fields <= {"master", "m", "v"}:
+            raise SMPInvalidArgumentError(f"SMP_OFFLOAD_OPTIMIZER_FIELDS: unknown field in {fields!r}")
         self._offload = None
         state.optimizer = self
         if model.partitioned:
@@ -155,25 +177,30 @@ class DistributedOptimizer:
                 else:
                     s, e = b.start, b.end
                 d = _Domain(key, s, e, gi, b.params)
-                dev = flat.data.device
-                if self.offload:
-                    # pinned host copies; the low-precision params stay in HBM
-                    dev = torch.device("cpu")
-                    d.master = torch.empty(e - s, dtype=torch.float32, pin_memory=True)
+                gdev = flat.data.device
+                cpu = torch.device("cpu")
+                off = self._offload_fields
+                if "master" in off:
+                    # pinned host copy; the low-precision params stay in HBM
+                    d.master = _pinned_full(e - s, 0.0)
                     d.master.copy_(flat.data[s:e].float())
                 elif lowp or flat.data.dtype != torch.float32:
                     d.master = flat.data[s:e].float().clone()
                 else:
                     d.master = flat.data[s:e]  # fp32 model: the parameters are the master copy
-                pin = self.offload
+
+                def state_buf(field, fill=0.0):
+                    if field in off:
+                        return _pinned_full(e - s, fill)
+                    return torch.full((e - s,), float(fill), dtype=torch.float32, device=gdev)
+
                 if self.kind in ("adam", "adamw", "lamb"):
-                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
-                    d.v = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
+                    d.m = state_buf("m")
+                    d.v = state_buf("v")
                 elif self.kind in ("sgd",):
-                    d.m = torch.zeros(e - s, dtype=torch.float32, device=dev, pin_memory=pin)
+                    d.m = state_buf("m")
                 elif self.kind == "adagrad":
-                    init = self.optimizer.param_groups[gi].get("initial_accumulator_value", 0.0)
-                    d.v = torch.full((e - s,), float(init), dtype=torch.float32, device=dev, pin_memory=pin)
+                    d.v = state_buf("v", self.optimizer.param_groups[gi].get("initial_accumulator_value", 0.0))
                 if self.kind == "lamb":
                     d.upd = torch.empty(e - s, dtype=torch.float32, device=dev)
                 self.domains.append(d)

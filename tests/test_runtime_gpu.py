@@ -65,14 +65,16 @@ _OFFLOAD_RUN = r"""
 import sys, torch
 import smdistributed_modelparallel_amd.torch as smp
 from smdistributed_modelparallel_amd.models import build_gpt, gpt_inputs
-off = sys.argv[1] == "1"
+off = sys.argv[1] != "0"
 smp.init({"bf16": True, "amd_offload_optimizer_state": off})
 torch.manual_seed(0)
 m = smp.DistributedModel(build_gpt("gpt2-tiny", dropout=0.0, num_layers=3))
 opt = smp.DistributedOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=0.1))
 assert (opt._offload is not None) == off
-if off:
+if sys.argv[1] == "1":
     assert all(d.master.device.type == "cpu" and d.master.is_pinned() for d in opt.domains)
+if sys.argv[1] == "mv":  # SMP_OFFLOAD_OPTIMIZER_FIELDS=m,v: master weights stay in HBM
+    assert all(d.master.is_cuda and d.m.device.type == "cpu" and d.m.is_pinned() for d in opt.domains)
 @smp.step
 def train(model, ids):
     loss, _ = model((ids, None, None, None, ids))
@@ -94,14 +96,18 @@ def test_optimizer_state_offload_matches_resident(tmp_path):
     """Optimizer state in pinned host memory, streamed through HBM staging per domain:
     bitwise the same training trajectory as the resident optimizer."""
     outs = []
-    for off in ("0", "1"):
+    for off in ("0", "1", "mv"):
         f = tmp_path / f"r{off}.pt"
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        if off == "mv":
+            env["SMP_OFFLOAD_OPTIMIZER_FIELDS"] = "m,v"
         r = subprocess.run([sys.executable, "-c", _OFFLOAD_RUN, off, str(f)], cwd=ROOT, capture_output=True,
-                           text=True, timeout=180, env=dict(os.environ, PYTHONPATH=ROOT))
+                           text=True, timeout=180, env=env)
         assert r.returncode == 0 and "RUN_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
         outs.append(torch.load(f, weights_only=True))
-    a, b = outs
-    assert a["losses"] == b["losses"]
-    for n in a["params"]:
-        assert torch.equal(a["params"][n], b["params"][n]), n
-    assert torch.equal(a["m0"], b["m0"])
+    a = outs[0]
+    for b in outs[1:]:
+        assert a["losses"] == b["losses"]
+        for n in a["params"]:
+            assert torch.equal(a["params"][n], b["params"][n]), n
+        assert torch.equal(a["m0"], b["m0"])

@@ -76,6 +76,72 @@ def probe(args):
     print("MAXPARAMS " + json.dumps(rec), flush=True)
 
 
+def _host_rss_gb():
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmHWM:"):
+                return int(line.split()[1]) / 1e6
+    return None
+
+
+def shard(args):
+    """BASELINE config 5 (GPT-3 175B shape, PP=4 x TP=2) -- ONE rank's shard on one GPU: the
+    heaviest stage (embedding + 24 of the 96 layers) with every tensor-parallel dimension
+    halved (48 of the 96 heads x 128, 4h / 2 = 24576 MLP channels, half the vocabulary), built
+    at tp=1 with those sliced shapes.  bf16 params / grads, AdamW with the fp32 state fields
+    named by SMP_OFFLOAD_OPTIMIZER_FIELDS in pinned host memory (amd_offload_optimizer_state),
+    activation checkpointing on every layer, micro-batch 1 x seq 2048, 3 full steps."""
+    import torch
+
+    import smdistributed_modelparallel_amd.torch as smp
+    from smdistributed_modelparallel_amd.models import build_gpt, gpt_inputs
+
+    smp.init({"bf16": True, "delayed_parameter_initialization": True, "amd_offload_optimizer_state": True})
+    h, tp = 12288, 2
+    vocab = (50257 + tp - 1) // tp
+    with smp.delay_param_initialization():
+        with smp.model_creation(dtype=torch.bfloat16):
+            net = build_gpt("gpt3-175b", dropout=0.0, num_layers=args.layers, hidden_size=h,
+                            num_attention_heads=96 // tp, attention_head_size=128, intermediate_size=4 * h // tp,
+                            vocab_size=vocab, num_positions=args.seq)
+    model = smp.DistributedModel(net)
+    for layer in model.get_module().transformer.seq_layers:
+        smp.set_activation_checkpointing(layer)
+    opt = smp.DistributedOptimizer(torch.optim.AdamW(model.parameters(), lr=1e-5, betas=(0.9, 0.95)))
+
+    @smp.step
+    def train(model, ids, mask, labels):
+        loss, _ = model((ids, mask, None, None, labels))
+        model.backward(loss)
+        return loss
+
+    dev = smp.state.device
+    ids, mask, _, _, labels = gpt_inputs(args.mbs, args.seq, vocab, dev)
+    losses, times = [], []
+    for i in range(3):
+        t0 = time.time()
+        opt.zero_grad()
+        out = train(model, ids, mask, labels)
+        opt.step()
+        losses.append(float(out.reduce_mean()))
+        torch.cuda.synchronize()
+        times.append(round(time.time() - t0, 2))
+        print(f"shard step {i}: loss {losses[-1]:.4f} {times[-1]} s", flush=True)
+    n = sum(p.numel() for p in model.get_module().parameters())
+    host_state = sum(t.numel() * t.element_size() for d in opt.domains for t in (d.master, d.m, d.v)
+                     if t is not None and not t.is_cuda)
+    rec = {"ok": all(l == l for l in losses), "config": "GPT-3 175B shape, PP=4 x TP=2: one rank's shard "
+           "(embedding + 24 layers, TP-sliced shapes at tp=1)", "layers": args.layers, "hidden": h,
+           "heads_local": 96 // tp, "intermediate_local": 4 * h // tp, "vocab_local": vocab, "params": n,
+           "offloaded_fields": sorted(opt._offload_fields), "host_state_gb": round(host_state / 1e9, 2),
+           "host_peak_rss_gb": round(_host_rss_gb() or 0.0, 2),
+           "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2),
+           "peak_reserved_gb": round(torch.cuda.max_memory_reserved() / 1e9, 2),
+           "hbm_gb": round(torch.cuda.get_device_properties(dev).total_memory / 1e9, 2),
+           "step_s": times, "losses": [round(l, 4) for l in losses]}
+    print("MAXPARAMS " + json.dumps(rec), flush=True)
+
+
 def run_probe(layers, args):
     cmd = [sys.executable, os.path.abspath(__file__), "probe", "--layers", str(layers), "--hidden", str(args.hidden),
            "--seq", str(args.seq), "--mbs", str(args.mbs)]
@@ -138,7 +204,7 @@ def search(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["probe", "search"])
+    ap.add_argument("mode", choices=["probe", "search", "shard"])
     ap.add_argument("--layers", type=int, default=24)
     ap.add_argument("--hidden", type=int, default=6144)
     ap.add_argument("--seq", type=int, default=2048)
@@ -150,6 +216,9 @@ def main():
     args = ap.parse_args()
     if args.mode == "probe":
         probe(args)
+        return 0
+    if args.mode == "shard":
+        shard(args)
         return 0
     return search(args)
 
