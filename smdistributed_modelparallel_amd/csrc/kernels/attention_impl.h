@@ -740,7 +740,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       }
       // dO^T / Q^T fragments of the dV / dK MFMAs now (independent of the exp / dS work below),
       // so those MFMAs issue back to back instead of each waiting on its own LDS reads
-      constexpr bool TPRE = D <= 128 && !BIAS;
+      constexpr bool TPRE = D <= 128 && !BIAS && !DROP && CAUSAL;  // (others: spills)
       typename MF<T>::e8 tdo[TPRE ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
       if constexpr (TPRE) {
         const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
@@ -757,10 +757,37 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
         for (int j = 0; j < 16; ++j) s[j] += kbias;
       }
+      // Dropout decisions of the lane's key for the 16 query registers.  The two lanes of a
+      // key PAIR (keys 2j, 2j+1 = lanes r, r^1: one 32-bit hash per (query, key pair)) share
+      // the work: the even lane hashes query registers 0-7, the odd one 8-15, and a DPP swap
+      // of adjacent lanes hands each the other half -- 8 hashes per lane instead of 16, the
+      // same random stream as the forward and the dQ kernel.
+      // (D = 256: registers are short there, so every lane hashes its own 16 pairs)
+      constexpr bool PAIRH = DROP && D <= 128;
+      uint32_t dkeep = 0;
+      if (PAIRH) {
+        const uint32_t odd = static_cast<uint32_t>(krow & 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t qq = static_cast<uint32_t>(qs + acc_row(j, hh)) + 16u * odd;
+          const uint32_t hv = mix32(dkey ^ (qq * npairs + kpair));
+          const uint32_t sw = static_cast<uint32_t>(
+              __builtin_amdgcn_mov_dpp(static_cast<int>(hv), 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, true));
+          const uint32_t lo = odd ? sw : hv;  // query register j
+          const uint32_t hi = odd ? hv : sw;  // query register j + 8
+          dkeep |= ((((lo >> kshift) & 0xffffu) >= thr) ? 1u : 0u) << j;
+          dkeep |= ((((hi >> kshift) & 0xffffu) >= thr) ? 1u : 0u) << (j + 8);
+        }
+      }
       auto finish = [&](float pv, int reg, int qq) {
         if (DROP) {
-          const uint32_t hsh = mix32(dkey ^ (static_cast<uint32_t>(qq) * npairs + kpair));
-          const float z = ((hsh >> kshift) & 0xffffu) >= thr ? rsd : 0.f;
+          float z;
+          if constexpr (PAIRH) {
+            z = ((dkeep >> reg) & 1u) ? rsd : 0.f;
+          } else {
+            const uint32_t hsh = mix32(dkey ^ (static_cast<uint32_t>(qq) * npairs + kpair));
+            z = ((hsh >> kshift) & 0xffffu) >= thr ? rsd : 0.f;
+          }
           s[reg] = pv * z;                             // (P o Z) for dV
           dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
         } else {
@@ -931,7 +958,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     // S / dP accumulators are live next to the 16 Q / dO fragments.
     constexpr bool SEQ = D >= 256;
     // K^T fragments of the dQ MFMAs (independent of the softmax work): read up front
-    constexpr bool KPRE = !SEQ && !BIAS;
+    constexpr bool KPRE = !SEQ && !BIAS && !DROP;
     typename MF<T>::e8 ktf[KPRE ? DO / 32 : 1][4];
     if constexpr (KPRE) {
 #pragma unroll

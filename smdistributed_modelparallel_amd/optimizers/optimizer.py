@@ -202,7 +202,7 @@ class DistributedOptimizer:
                 elif self.kind == "adagrad":
                     d.v = state_buf("v", self.optimizer.param_groups[gi].get("initial_accumulator_value", 0.0))
                 if self.kind == "lamb":
-                    d.upd = torch.empty(e - s, dtype=torch.float32, device=dev)
+                    d.upd = torch.empty(e - s, dtype=torch.float32, device=gdev)
                 self.domains.append(d)
         if self.offload:
             from .offload import OptimizerStateOffload

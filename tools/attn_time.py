@@ -39,7 +39,28 @@ o, lse = C.attention_fwd(q, k, v, 0.125, True, 0)
 do = torch.randn_like(o)
 dqkv = torch.empty_like(qkv)
 zb = torch.zeros(b, s, device="cuda")
+def drop_times():
+    """dropout 0.1: hash-regenerating backward, and (new builds) forward-stored keep bits."""
+    out = {}
+    args = (q, k, v, 0.125, True, 0, None, 0.1, 1234, 0)
+    o1, lse1 = C.attention_fwd(*args)[:2]
+    out["fwd_drop_us"] = round(t(lambda: C.attention_fwd(*args)), 1)
+    out["bwd_drop_hash_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, o1, lse1, dqkv[:, :, 0], dqkv[:, :, 1],
+                                                                   dqkv[:, :, 2], 0.125, True, 0, None, 0.1, 1234, 0)), 1)
+    try:
+        res = C.attention_fwd(*args, True)
+    except TypeError:
+        return out
+    mask = res[2]
+    out["fwd_drop_store_us"] = round(t(lambda: C.attention_fwd(*args, True)), 1)
+    out["bwd_drop_bits_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, res[0], res[1], dqkv[:, :, 0],
+                                                                   dqkv[:, :, 1], dqkv[:, :, 2], 0.125, True, 0, None,
+                                                                   0.1, 1234, 0, mask)), 1)
+    return out
+
+
 for _ in range(2):
+    print(path or "in-tree", drop_times(), flush=True)
     print(path or "in-tree", {
         "fwd_us": round(t(lambda: C.attention_fwd(q, k, v, 0.125, True, 0)), 1),
         "fwd_zero_bias_us": round(t(lambda: C.attention_fwd(q, k, v, 0.125, True, 0, zb)), 1),
