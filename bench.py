@@ -47,7 +47,9 @@ def parse():
     ap.add_argument("--head-cost", type=float, default=float(os.environ.get("SMP_BENCH_HEAD_COST", "2.4")),
                     help="PP layer split: cost of stage 0's tied embedding + LM head + loss in transformer-layer "
                          "units (2 h V vs 24 h^2 + attention FLOPs per token, plus the CE kernels)")
-    ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--dropout", type=float, default=0.1,
+                    help="attention / hidden / embedding dropout probability; default 0.1 = the GPT-2 XL and "
+                         "smp.nn DistributedTransformer default (the reference trains with it on)")
     ap.add_argument("--no-flash", action="store_true")
     ap.add_argument("--activation-checkpointing", action="store_true")
     ap.add_argument("--shard-optimizer-state", action="store_true")

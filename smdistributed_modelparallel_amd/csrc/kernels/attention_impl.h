@@ -73,8 +73,9 @@ struct LdsStride {
 };
 
 // ---------------------------------------------------------------- dropout hash
-// lowbias32 (a bijective 32-bit mixer): distinct (query, key-pair) inputs under one key give
-// distinct outputs; the two 16-bit halves are the uniforms of the pair's even / odd key.
+// lowbias32 (a bijective 32-bit mixer): distinct (query, key-quad) inputs under one key give
+// distinct outputs; byte i of mix32(key ^ (q * nquads + k / 4)) is the 8-bit uniform of key
+// 4 (k / 4) + i.  One hash serves four keys (FlashAttention-style 8-bit dropout decisions).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -82,6 +83,40 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x *= 0x846ca68bu;
   x ^= x >> 16;
   return x;
+}
+
+// Per-byte keep test without unpacking: bit 8i+7 of the result is set iff byte i of h is
+// >= drop_thr.  thr <= 128 (xr = 0, c = (128 - thr) x 0x01010101): a byte >= 128 is kept, a
+// smaller one carries into its bit 7 iff b + 128 - thr >= 128 (no carry leaves the byte).
+// thr > 128 (xr = ~0): the same test on the complemented bytes with 256 - thr, negated.
+__device__ __forceinline__ uint32_t keep_flags(uint32_t h, uint32_t xr, uint32_t c) {
+  const uint32_t hx = h ^ xr;
+  return (((hx & 0x7f7f7f7fu) + c) | hx) ^ xr;
+}
+
+// all-ones iff bit `bit` of f is set (v_bfe_i32)
+__device__ __forceinline__ uint32_t bit_mask(uint32_t f, uint32_t bit) {
+  return static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(f), bit, 1u));
+}
+
+// lane 4 (lane / 4) + j's v, for every lane of the quad (DPP quad_perm [j, j, j, j]); j is a
+// compile-time constant after unrolling
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int j) {
+  const int x = static_cast<int>(v);
+  switch (j) {
+    case 0:
+      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0x00, 0xF, 0xF, true));
+    case 1:
+      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0x55, 0xF, 0xF, true));
+    case 2:
+      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0xAA, 0xF, 0xF, true));
+    default:
+      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0xFF, 0xF, 0xF, true));
+  }
+}
+
+__device__ __forceinline__ float and_mask(float x, uint32_t m) {
+  return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m);
 }
 
 __device__ __forceinline__ uint32_t drop_key(const AttnParams& p, int64_t bh) {
@@ -315,17 +350,18 @@ __device__ __forceinline__ void publish_bias_flag(float bstage, int* sFlag) {
 }
 
 // Dropout for a transposed tile (query on the lane, 16 keys in registers starting at key
-// `kbase` (even)): register pairs (2j, 2j+1) are the key pairs kbase/2 + acc_row(2j)/2.
-__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t thr16,
-                                          float keepval_scale, bool scale_kept) {
+// `kbase` (a multiple of 32)): register group g (registers 4g..4g+3) holds keys
+// kbase + 8g + 4hh + 0..3 = key quad kbase/4 + 2g + hh, bytes 0..3 of its hash.  Dropped
+// entries become +0; kept ones keep their value (the 1 / keep-probability factor is applied
+// by the caller).
+__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t xr,
+                                          uint32_t c) {
 #pragma unroll
-  for (int reg = 0; reg < 16; reg += 2) {
-    const uint32_t kp = static_cast<uint32_t>(kbase >> 1) + static_cast<uint32_t>(acc_row(reg, hh) >> 1);
-    const uint32_t hsh = mix32(key ^ (qbase + kp));
-    const float k0 = scale_kept ? a[reg] * keepval_scale : a[reg];
-    const float k1 = scale_kept ? a[reg + 1] * keepval_scale : a[reg + 1];
-    a[reg] = (hsh << 16) >= thr16 ? k0 : 0.f;
-    a[reg + 1] = hsh >= thr16 ? k1 : 0.f;
+  for (int g = 0; g < 4; ++g) {
+    const uint32_t kq = static_cast<uint32_t>(kbase >> 2) + static_cast<uint32_t>(2 * g + hh);
+    const uint32_t f = keep_flags(mix32(key ^ (qbase + kq)), xr, c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[4 * g + i] = and_mask(a[4 * g + i], bit_mask(f, 8 * i + 7));
   }
 }
 
@@ -428,8 +464,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   const float sl2 = p.scale * kLog2e;
   const float inv_scale = 1.f / p.scale;
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 1) >> 1);
-  const uint32_t thr16 = p.drop_thr << 16;
+  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
   float m_i = -INFINITY, l_i = 0.f;
   f32x16 o[D / 32];
 #pragma unroll
@@ -549,8 +584,8 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
     }
     m_i = m_new;
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
-      drop_tile(s0, dkey, qbase, kv0, hh, thr16, 1.f, false);
-      drop_tile(s1, dkey, qbase, kv0 + 32, hh, thr16, 1.f, false);
+      drop_tile(s0, dkey, qbase, kv0, hh, p.drop_xr, p.drop_c);
+      drop_tile(s1, dkey, qbase, kv0 + 32, hh, p.drop_xr, p.drop_c);
     }
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
 #pragma unroll
@@ -659,11 +694,17 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   float kbias = 0.f;
   bool blk_bias = false;  // this wave's 32 keys carry a bias
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t npairs = static_cast<uint32_t>((sk + 1) >> 1);
-  const uint32_t kpair = static_cast<uint32_t>(krow >> 1);
-  const int kshift = (krow & 1) * 16;
-  const uint32_t thr = p.drop_thr;
-  const float rsd = p.drop_rs;
+  // dropout: the 4 lanes of a key quad (keys 4j..4j+3 = lanes with the same lane >> 2) share
+  // one hash per query; quad position qp hashes query registers 4 qp .. 4 qp + 3 (inputs
+  // q * nquads + key quad, the query part of each a per-lane constant plus qs * nquads)
+  const uint32_t nquads = static_cast<uint32_t>((sk + 3) >> 2);
+  const int qp = lane & 3;
+  uint32_t hin[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    hin[i] = static_cast<uint32_t>(acc_row(4 * qp + i, hh)) * nquads + static_cast<uint32_t>(krow >> 2);
+  const uint32_t kbit = 8u * static_cast<uint32_t>(qp) + 7u;  // this key's flag bit in a keep word
+  const uint32_t rsd_bits = __builtin_bit_cast(uint32_t, p.drop_rs);
   int q_start = 0, q_end = sq;
   if (CAUSAL) {
     q_start = kb * BKEYS - diag;
@@ -757,37 +798,21 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
         for (int j = 0; j < 16; ++j) s[j] += kbias;
       }
-      // Dropout decisions of the lane's key for the 16 query registers.  The two lanes of a
-      // key PAIR (keys 2j, 2j+1 = lanes r, r^1: one 32-bit hash per (query, key pair)) share
-      // the work: the even lane hashes query registers 0-7, the odd one 8-15, and a DPP swap
-      // of adjacent lanes hands each the other half -- 8 hashes per lane instead of 16, the
-      // same random stream as the forward and the dQ kernel.
-      // (D = 256: registers are short there, so every lane hashes its own 16 pairs)
-      constexpr bool PAIRH = DROP && D <= 128;
-      uint32_t dkeep = 0;
-      if (PAIRH) {
-        const uint32_t odd = static_cast<uint32_t>(krow & 1);
+      // Dropout decisions of the lane's key for the 16 query registers: this lane hashes
+      // query registers 4 qp + i (keep flags of the quad's 4 keys in one word each), and the
+      // word of register j comes from quad lane j / 4 by a DPP broadcast -- 4 hashes per lane
+      // instead of 16, the same random stream as the forward and the dQ kernel.
+      uint32_t kf4[4] = {0u, 0u, 0u, 0u};
+      if (DROP) {
+        const uint32_t qsn = static_cast<uint32_t>(qs) * nquads;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t qq = static_cast<uint32_t>(qs + acc_row(j, hh)) + 16u * odd;
-          const uint32_t hv = mix32(dkey ^ (qq * npairs + kpair));
-          const uint32_t sw = static_cast<uint32_t>(
-              __builtin_amdgcn_mov_dpp(static_cast<int>(hv), 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, true));
-          const uint32_t lo = odd ? sw : hv;  // query register j
-          const uint32_t hi = odd ? hv : sw;  // query register j + 8
-          dkeep |= ((((lo >> kshift) & 0xffffu) >= thr) ? 1u : 0u) << j;
-          dkeep |= ((((hi >> kshift) & 0xffffu) >= thr) ? 1u : 0u) << (j + 8);
-        }
+        for (int i = 0; i < 4; ++i) kf4[i] = keep_flags(mix32(dkey ^ (qsn + hin[i])), p.drop_xr, p.drop_c);
       }
-      auto finish = [&](float pv, int reg, int qq) {
+      auto finish = [&](float pv, int reg) {
         if (DROP) {
-          float z;
-          if constexpr (PAIRH) {
-            z = ((dkeep >> reg) & 1u) ? rsd : 0.f;
-          } else {
-            const uint32_t hsh = mix32(dkey ^ (static_cast<uint32_t>(qq) * npairs + kpair));
-            z = ((hsh >> kshift) & 0xffffu) >= thr ? rsd : 0.f;
-          }
+          // register reg = 4 j + i: word i of quad lane j (quad_perm [j, j, j, j])
+          const uint32_t w = quad_bcast(kf4[reg & 3], reg >> 2);
+          const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
           s[reg] = pv * z;                             // (P o Z) for dV
           dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
         } else {
@@ -797,7 +822,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       };
       if (interior) {
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) finish(fast_exp2(s[reg] * sl2), reg, qs + acc_row(reg, hh));
+        for (int reg = 0; reg < 16; ++reg) finish(fast_exp2(s[reg] * sl2), reg);
       } else {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
@@ -805,7 +830,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
           float pv = fast_exp2(s[reg] * sl2);
           if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win))
             pv = 0.f;
-          finish(pv, reg, qq);
+          finish(pv, reg);
         }
       }
       // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
@@ -910,8 +935,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
   }
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 1) >> 1);
-  const uint32_t thr16 = p.drop_thr << 16;
+  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
+  const float rsd = p.drop_rs;
   f32x16 dq[DO / 32];
 #pragma unroll
   for (int i = 0; i < DO / 32; ++i) dq[i] = f32x16{0};
@@ -981,14 +1006,14 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
       if (tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       if (DROP) {
-        // dp <- Z o dP (raw), then dS = P o (Z o dP - delta)
-        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, thr16, p.drop_rs, true);
+        // dp <- keep o dP (raw), then dS = P o (dP o keep / (1 - p) - delta)
+        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, p.drop_xr, p.drop_c);
       }
       if (interior) {
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
           const float pv = fast_exp2(s[u][reg] * sl2);
-          dp[u][reg] = DROP ? pv * (dp[u][reg] - dl) : dp[u][reg] * pv;  // dS^T
+          dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : dp[u][reg] * pv;  // dS^T
         }
       } else {
 #pragma unroll
@@ -997,7 +1022,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
           const int kk = kv0 + 32 * u + acc_row(reg, hh);
           if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win))
             pv = 0.f;
-          dp[u][reg] = DROP ? pv * (dp[u][reg] - dl) : dp[u][reg] * pv;
+          dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : dp[u][reg] * pv;
         }
       }
       if (SEQ) {

@@ -588,10 +588,16 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
   }
   TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention: dropout_p must be in [0, 1)");
   if (dropout_p > 0.0) {
-    // dropped iff the element's 16-bit uniform < thr: keep probability 1 - thr / 65536
-    uint32_t thr = static_cast<uint32_t>(dropout_p * 65536.0 + 0.5);
-    p.drop_thr = thr < 1 ? 1 : (thr > 65535 ? 65535 : thr);
-    p.drop_rs = static_cast<float>(1.0 / (1.0 - dropout_p));
+    // dropped iff the element's 8-bit uniform < thr: keep probability 1 - thr / 256 (the
+    // probability is quantised to 1/256, as with 8-bit dropout masks; kept values are scaled
+    // by the exact inverse keep probability, so the expectation is unchanged)
+    uint32_t thr = static_cast<uint32_t>(dropout_p * 256.0 + 0.5);
+    thr = thr < 1 ? 1 : (thr > 255 ? 255 : thr);
+    p.drop_thr = thr;
+    p.drop_rs = static_cast<float>(256.0 / (256.0 - thr));
+    const uint32_t t7 = thr <= 128 ? thr : 256 - thr;  // 1..128
+    p.drop_xr = thr <= 128 ? 0u : 0xffffffffu;
+    p.drop_c = (128u - t7) * 0x01010101u;
     p.seed = static_cast<uint64_t>(seed);
     p.offset = static_cast<uint64_t>(offset);
   }

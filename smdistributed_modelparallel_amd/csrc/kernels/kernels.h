@@ -146,8 +146,10 @@ struct AttnParams {
   int window;  // >0: local attention window (GPT-Neo)
   const float* kbias;  // optional additive key bias [b, sk] (padding mask); nullptr = none
   int64_t kbias_sb;    // its batch stride (0: one row shared by the batch)
-  uint32_t drop_thr;   // dropout: element dropped iff its 16-bit uniform < drop_thr (0 = off)
-  float drop_rs;       // 1 / (1 - p)
+  uint32_t drop_thr;   // dropout: element dropped iff its 8-bit uniform < drop_thr (0 = off)
+  float drop_rs;       // 1 / keep probability = 256 / (256 - drop_thr)
+  uint32_t drop_xr;    // per-byte keep test constants (attention_impl.h keep_flags):
+  uint32_t drop_c;     //   xr = 0 / ~0 for drop_thr <= / > 128, c = per-byte add constant
   uint64_t seed, offset;
 };
 struct AttnBwdParams {

@@ -85,21 +85,33 @@ def _mix32(x):
     return x ^ (x >> 16)
 
 
+def flash_dropout_threshold(dropout_p):
+    """8-bit drop threshold of the flash kernels: an element is dropped iff its 8-bit uniform is
+    below it, so the realised drop probability is ``thr / 256`` (``dropout_p`` quantised to
+    1/256) and kept values are scaled by ``256 / (256 - thr)``."""
+    return max(1, min(255, int(dropout_p * 256.0 + 0.5)))
+
+
+def flash_dropout_keep_prob(dropout_p):
+    return 1.0 - flash_dropout_threshold(dropout_p) / 256.0
+
+
 def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu"):
     """Host reconstruction of the kernel's dropout decisions ([b, h, sq, sk] bool, True =
-    kept): test oracle for the in-kernel hash (csrc/kernels/attention_impl.h drop_key/mix32)."""
+    kept): test oracle for the in-kernel hash (csrc/kernels/attention_impl.h drop_key/mix32):
+    byte ``k % 4`` of ``mix32(key ^ (q * ceil(sk / 4) + k // 4))`` is key k's 8-bit uniform."""
     M = 0xFFFFFFFF
-    thr = max(1, min(65535, int(dropout_p * 65536.0 + 0.5)))
+    thr = flash_dropout_threshold(dropout_p)
     s0, s1, o0, o1 = seed & M, (seed >> 32) & M, offset & M, (offset >> 32) & M
     bh = torch.arange(b * h, dtype=torch.int64, device=device)
     key = _mix32(torch.full_like(bh, s0) ^ _mix32((s1 + 0x9E3779B9 * (bh + 1)) & M) ^
                  _mix32(torch.full_like(bh, o0) ^ _mix32(torch.full_like(bh, (o1 + 0x85EBCA6B) & M))))
-    npairs = (sk + 1) // 2
+    nquads = (sk + 3) // 4
     q = torch.arange(sq, dtype=torch.int64, device=device).view(1, -1, 1)
     k = torch.arange(sk, dtype=torch.int64, device=device).view(1, 1, -1)
-    x = (key.view(-1, 1, 1) ^ ((q * npairs + (k >> 1)) & M)) & M
+    x = (key.view(-1, 1, 1) ^ ((q * nquads + (k >> 2)) & M)) & M
     hsh = _mix32(x)
-    u = torch.where((k & 1) == 1, hsh >> 16, hsh & 0xFFFF)
+    u = (hsh >> (8 * (k & 3))) & 0xFF
     return (u >= thr).view(b, h, sq, sk)
 
 

@@ -85,3 +85,26 @@ def test_materialised_gemm_layouts_avoid_faulting_nt_product():
             o = A.attention(q, k, v, causal=causal, use_flash=False)
             o.backward(torch.ones_like(o))
     assert not bad, bad
+
+
+def test_flash_dropout_byte_keep_test_swar():
+    """The flash kernels' per-byte keep test (attention_impl.h keep_flags, constants from
+    bindings.cpp attn_params): bit 8i+7 set iff byte i >= thr, for every threshold, in both
+    the thr <= 128 and the complemented thr > 128 form; realised keep probability 1 - thr/256."""
+    import random
+
+    M = 0xFFFFFFFF
+    rnd = random.Random(0)
+    words = [rnd.getrandbits(32) for _ in range(64)] + [0, M, 0x7F7F7F7F, 0x80808080, 0x807F0180]
+    for thr in range(1, 256):
+        t7 = thr if thr <= 128 else 256 - thr
+        xr = 0 if thr <= 128 else M
+        c = (128 - t7) * 0x01010101
+        for h in words:
+            hx = h ^ xr
+            f = ((((hx & 0x7F7F7F7F) + c) & M) | hx) ^ xr
+            for i in range(4):
+                assert bool((f >> (8 * i + 7)) & 1) == (((h >> (8 * i)) & 0xFF) >= thr), (thr, hex(h), i)
+    assert A.flash_dropout_threshold(0.1) == 26 and abs(A.flash_dropout_keep_prob(0.1) - (1 - 26 / 256)) < 1e-12
+    keep = A.flash_dropout_keep_mask(2, 3, 64, 64, 0.1, 1234, 7)
+    assert abs(keep.float().mean().item() - A.flash_dropout_keep_prob(0.1)) < 0.01

@@ -27,7 +27,9 @@ def _ref(q, k, v, scale, causal, window=None, kbias=None, keep=None, p=0.0):
     s = s.masked_fill(masked, float("-inf"))
     pr = torch.softmax(s, dim=-1)
     if keep is not None:
-        pr = pr * keep.float() / (1.0 - p)
+        from smdistributed_modelparallel_amd.ops.attention import flash_dropout_keep_prob
+
+        pr = pr * keep.float() / flash_dropout_keep_prob(p)
     return torch.matmul(pr, vf).transpose(1, 2)
 
 
@@ -65,15 +67,16 @@ def test_flash_fwd_bwd(dt, d, causal, s):
                  3e-2 if dt == torch.bfloat16 else 8e-3)
 
 
-@pytest.mark.parametrize("d", [64, 96, 128, 256])
-@pytest.mark.parametrize("causal", [True, False])
-def test_flash_dropout_matches_host_mask(d, causal):
+@pytest.mark.parametrize("d,causal,p", [(64, True, 0.2), (64, False, 0.2), (96, True, 0.2), (96, False, 0.2),
+                                         (128, True, 0.2), (128, False, 0.2), (256, True, 0.2), (256, False, 0.2),
+                                         (64, True, 0.75), (256, False, 0.6)])
+def test_flash_dropout_matches_host_mask(d, causal, p):
     """In-kernel dropout: forward and backward equal the fp32 reference that applies the
     keep mask rebuilt on the host from the same seed/offset (so fwd and bwd agree)."""
     from smdistributed_modelparallel_amd.ops.attention import _FlashAttention, flash_dropout_keep_mask
 
     torch.manual_seed(3)
-    b, s, h, p = 2, 192, 2, 0.2
+    b, s, h = 2, 192, 2
     q, k, v = (torch.randn(b, s, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
     scale = 1.0 / math.sqrt(d)
     gen = torch.cuda.default_generators[torch.cuda.current_device()]
@@ -84,7 +87,7 @@ def test_flash_dropout_matches_host_mask(d, causal):
     assert abs(rate - p) < 0.02, rate
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
     orf = _ref(qr, kr, vr, scale, causal, keep=keep, p=p)
-    assert (o.float() - orf).abs().max().item() < 3e-2
+    assert (o.float() - orf).abs().max().item() < 3e-2 * max(1.0, orf.abs().max().item())
     g = torch.randn_like(orf)
     o.backward(g.to(torch.bfloat16))
     orf.backward(g)
