@@ -43,6 +43,7 @@ namespace attn {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
 struct MF;
@@ -349,19 +350,51 @@ __device__ __forceinline__ void publish_bias_flag(float bstage, int* sFlag) {
   }
 }
 
-// Dropout for a transposed tile (query on the lane, 16 keys in registers starting at key
-// `kbase` (a multiple of 32)): register group g (registers 4g..4g+3) holds keys
-// kbase + 8g + 4hh + 0..3 = key quad kbase/4 + 2g + hh, bytes 0..3 of its hash.  Dropped
-// entries become +0; kept ones keep their value (the 1 / keep-probability factor is applied
-// by the caller).
-__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t xr,
-                                          uint32_t c) {
+// Dropout keep words of a transposed tile (query on the lane, 16 keys in registers starting
+// at key `kbase`, a multiple of 32): register group g (registers 4g..4g+3) holds keys
+// kbase + 8g + 4hh + 0..3 = key quad kbase/4 + 2g + hh, whose keep flags are bits 7, 15, 23,
+// 31 of f[g] (keep_flags of the quad's hash).
+__device__ __forceinline__ void drop_words(uint32_t (&f)[4], uint32_t key, uint32_t qbase, int kbase, int hh,
+                                           uint32_t xr, uint32_t c) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const uint32_t kq = static_cast<uint32_t>(kbase >> 2) + static_cast<uint32_t>(2 * g + hh);
-    const uint32_t f = keep_flags(mix32(key ^ (qbase + kq)), xr, c);
+    f[g] = keep_flags(mix32(key ^ (qbase + kq)), xr, c);
+  }
+}
+
+// Element i of a keep word as an all-ones / zero 32-bit mask, by v_perm_b32's sign-replicating
+// selectors (8: bit 15 of src1, 9: bit 31 of src1, 10: bit 15 of src0, 11: bit 31 of src0) on
+// (f, f << 8): flag bits 7 / 23 sit at 15 / 31 of the shifted word.
+__device__ __forceinline__ uint32_t elem_mask(uint32_t f, uint32_t sh, int i) {
+  constexpr uint32_t kSel[4] = {0x08080808u, 0x0A0A0A0Au, 0x09090909u, 0x0B0B0B0Bu};
+  return __builtin_amdgcn_perm(f, sh, kSel[i]);
+}
+
+// Zero the dropped entries of a packed MFMA operand (8 bf16/f16 = registers 8 half .. +7 =
+// groups 2 half, 2 half + 1): one v_perm mask per element pair, applied with one AND.
+template <typename E>
+__device__ __forceinline__ E drop_packed(E v, uint32_t f0, uint32_t f1) {
+  u32x4 w = __builtin_bit_cast(u32x4, v);
+  const uint32_t s0 = f0 << 8, s1 = f1 << 8;
+  w[0] &= __builtin_amdgcn_perm(f0, s0, 0x0A0A0808u);  // elements 0, 1 of group 2 half
+  w[1] &= __builtin_amdgcn_perm(f0, s0, 0x0B0B0909u);  // elements 2, 3
+  w[2] &= __builtin_amdgcn_perm(f1, s1, 0x0A0A0808u);  // group 2 half + 1
+  w[3] &= __builtin_amdgcn_perm(f1, s1, 0x0B0B0909u);
+  return __builtin_bit_cast(E, w);
+}
+
+// Dropped entries of a transposed fp32 tile become +0 (kept ones keep their value; the
+// 1 / keep-probability factor is applied by the caller).
+__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t xr,
+                                          uint32_t c) {
+  uint32_t f[4];
+  drop_words(f, key, qbase, kbase, hh, xr, c);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[4 * g + i] = and_mask(a[4 * g + i], bit_mask(f, 8 * i + 7));
+  for (int g = 0; g < 4; ++g) {
+    const uint32_t sh = f[g] << 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[4 * g + i] = and_mask(a[4 * g + i], elem_mask(f[g], sh, i));
   }
 }
 
@@ -583,11 +616,16 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
     }
     m_i = m_new;
-    if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
-      drop_tile(s0, dkey, qbase, kv0, hh, p.drop_xr, p.drop_c);
-      drop_tile(s1, dkey, qbase, kv0 + 32, hh, p.drop_xr, p.drop_c);
-    }
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
+    if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
+      uint32_t f0[4], f1[4];
+      drop_words(f0, dkey, qbase, kv0, hh, p.drop_xr, p.drop_c);
+      drop_words(f1, dkey, qbase, kv0 + 32, hh, p.drop_xr, p.drop_c);
+      pf[0] = drop_packed(pf[0], f0[0], f0[1]);
+      pf[1] = drop_packed(pf[1], f0[2], f0[3]);
+      pf[2] = drop_packed(pf[2], f1[0], f1[1]);
+      pf[3] = drop_packed(pf[3], f1[2], f1[3]);
+    }
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
 #pragma unroll
