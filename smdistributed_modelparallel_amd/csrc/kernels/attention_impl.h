@@ -34,6 +34,8 @@
 //    dS = P o (Z o dP - delta) with Z = keep / (1 - p); delta = rowsum(dO o O) is unchanged.
 //  * head dims 64, 96, 128, 256.  D = 96 uses a 128-element LDS row stride (swizzle needs a
 //    power-of-two chunk count) but runs 6 / 3 MFMA k-steps / tiles, not 8 / 4.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -640,6 +642,254 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   if (hh == 0) p.lse[bh * p.sq + qrow] = (l_i > 0.f) ? (m_i + log2f(l_i)) / kLog2e : -INFINITY;
 }
 
+// s_waitcnt vmcnt(N) from inline asm (the LDS-DMA it waits for is issued from inline asm too)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N == 0 || N == 2 || N == 4 || N == 8, "vm_wait: add the count");
+  if constexpr (N == 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+// ===================================================== software-pipelined forward
+// D = 64 / 128 without key bias or window (the others take attn_fwd_kernel).  Same block
+// and wave layout and LDS image, but each wave runs a two-stage pipeline over its key tiles
+// instead of QK^T -> softmax -> PV in turn (profiles/r3: the in-turn loop keeps a wave
+// waiting on its own MFMA results or LDS reads ~65 % of its cycles, MFMA busy 25 %):
+//   phase A of iteration t: the QK^T MFMAs of tile t + 1, each followed in program order by
+//     a slice of tile t's exp / row-sum VALU work (sched_group_barrier), so the VALU issues
+//     in the MFMA shadow;
+//   phase B: tile t's P is packed (and dropped) fragment by fragment, each fragment's PV
+//     MFMAs issued as soon as it is ready; then tile t + 1's row max, which needs its S.
+// K and V have separate two-slot rings filled by LDS-DMA: iteration t reads K(t + 1) and
+// V(t), and issues K(t + 2) and V(t + 1) right after its barrier.  The row sum stays a
+// per-lane partial (both half-waves see the same row maxima) and is combined once at the end.
+template <typename T, int D, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(kThreads, 2) attn_fwd_pipe_kernel(AttnParams p) {
+  static_assert(D == 64 || D == 128, "pipelined forward: D 64 / 128");
+  constexpr int BM = 128, BN = 64, TS = BN * D;
+  constexpr int L = (BN * D * 2 / 1024) / (kThreads / 64);  // DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[4 * TS];  // K slots 0, 1, V slots 0, 1
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
+  int tile;
+  int64_t bh;
+  xcd_map(nqb, p.b * p.h, tile, bh);
+  const int64_t b = bh / p.h, h = bh % p.h;
+  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;
+  const int q0 = qb * BM + wave * 32;
+  const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
+  const int diag = sk - sq;
+  const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
+  const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
+  const uint16_t* V = static_cast<const uint16_t*>(p.v) + b * p.v_sb + h * p.v_sh;
+
+  typename MF<T>::e8 qf[D / 16];
+  const int qrow = q0 + r;
+#pragma unroll
+  for (int t = 0; t < D / 16; ++t) {
+    if (qrow < sq) {
+      qf[t] = ld8<T>(Q + static_cast<int64_t>(qrow) * p.q_ss + 16 * t + 8 * hh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[t][j] = MF<T>::cvt(0.f);
+    }
+  }
+  const float sl2 = p.scale * kLog2e;
+  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
+  // block range (every wave takes part in every tile's barrier) and this wave's own range
+  int kv_end = sk;
+  if (CAUSAL) {
+    const int lim = (qb + 1) * BM + diag;
+    kv_end = lim < sk ? lim : sk;
+  }
+  const int nt = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  int wend = kv_end;
+  if (CAUSAL) wend = q0 + 32 + diag < kv_end ? q0 + 32 + diag : kv_end;
+  const int ntw = wend > 0 ? (wend + BN - 1) / BN : 0;
+  const int wave_last_q = q0 + 31;
+  auto interior = [&](int kv0) {
+    return kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag);
+  };
+  auto dmaK = [&](int t) { dma_tile<D, BN>(sKV + (t & 1) * TS, K, p.k_ss, t * BN, sk, wave, lane); };
+  auto dmaV = [&](int t) { dma_tile<D, BN>(sKV + (2 + (t & 1)) * TS, V, p.v_ss, t * BN, sk, wave, lane); };
+  const RowOff<D> ro(r, hh);
+  const TrOff<D> tro(lane);
+
+  // S of tile t (raw scores, masked), the exponent offset of tile t, the O / l rescale
+  float m_i = -INFINITY, l_i = 0.f, m_use = 0.f, alpha = 1.f;
+  bool rescale = false;
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) o[i] = f32x16{0};
+  f32x16 sc0 = f32x16{0}, sc1 = f32x16{0};
+
+  // masks a raw score tile (keys kv0 .. kv0 + 63) and folds its row max into the running max
+  auto stats = [&](f32x16& s0, f32x16& s1, int kv0) {
+    if (!interior(kv0)) {
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k0 = kv0 + acc_row(reg, hh);
+        const int k1 = k0 + 32;
+        if (k0 >= sk || (CAUSAL && k0 > qrow + diag)) s0[reg] = -INFINITY;
+        if (k1 >= sk || (CAUSAL && k1 > qrow + diag)) s1[reg] = -INFINITY;
+      }
+    }
+    float mx0 = max3(s0[0], s1[0], s0[1]), mx1 = max3(s1[1], s0[2], s1[2]);
+#pragma unroll
+    for (int reg = 3; reg < 15; reg += 2) {
+      mx0 = max3(mx0, s0[reg], s1[reg]);
+      mx1 = max3(mx1, s0[reg + 1], s1[reg + 1]);
+    }
+    float mx = max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2;
+    mx = fmaxf(mx, xor32(mx));
+    const float m_new = fmaxf(m_i, mx);
+    const float mu = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
+    alpha = fast_exp2(m_i - mu);
+    rescale = __any(m_new != m_i);
+    m_i = m_new;
+    m_use = mu;
+  };
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): Q loads retired (see attn_fwd_kernel)
+  if (nt > 0) {
+    dmaK(0);
+    dmaV(0);
+    if (nt > 1) {
+      dmaK(1);
+      vm_wait<2 * L>();  // K(0) landed (V(0), K(1) may fly)
+    } else {
+      vm_wait<L>();
+    }
+    __syncthreads();
+    if (ntw > 0) {
+#pragma unroll
+      for (int k = 0; k < D / 16; ++k) {
+        sc0 = MF<T>::mma(ld8<T>(sKV + ro.o[k]), qf[k], sc0);
+        sc1 = MF<T>::mma(ld8<T>(sKV + ro.o[k] + 32 * D), qf[k], sc1);
+      }
+      stats(sc0, sc1, 0);
+    }
+  }
+  // tile t's barrier: this wave's K(t + 1) and V(t) landed, everyone's too, and the slots
+  // of K(t) and V(t - 1) are free for K(t + 2) and V(t + 1)
+  auto sync_issue = [&](int t) {
+    vm_wait<0>();
+    __syncthreads();
+    if (t + 2 < nt) dmaK(t + 2);
+    if (t + 1 < nt) dmaV(t + 1);
+  };
+  auto rescale_o = [&]() {
+    if (rescale) {
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
+    }
+    l_i *= alpha;
+  };
+  // tile t: exponentials of c0 / c1 (its masked scores); with MORE, tile t + 1's scores into
+  // n0 / n1 (the caller alternates the two register sets, no copies)
+  auto step = [&](int t, auto more_c, f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1) {
+    const int kv0 = t * BN;
+    const uint16_t* sV = sKV + (2 + (t & 1)) * TS;
+    constexpr bool MORE = decltype(more_c)::value;
+    // phase A: QK^T of tile t + 1 beside tile t's exponentials
+    if constexpr (MORE) {
+      const uint16_t* sK = sKV + ((t + 1) & 1) * TS;
+      n0 = f32x16{0};
+      n1 = f32x16{0};
+#pragma unroll
+      for (int k = 0; k < D / 16; ++k) {
+        n0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qf[k], n0);
+        n1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * D), qf[k], n1);
+      }
+    }
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float e0 = fast_exp2(fmaf(c0[reg], sl2, -m_use));
+      const float e1 = fast_exp2(fmaf(c1[reg], sl2, -m_use));
+      c0[reg] = e0;
+      c1[reg] = e1;
+      rs0 += e0;
+      rs1 += e1;
+    }
+    if constexpr (MORE) {
+      // 2 K reads, then per MFMA a slice of the 96 exp / fma / add instructions
+#pragma unroll
+      for (int k = 0; k < D / 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 96 / (D / 8), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 96 / (D / 8), 0);
+      }
+    }
+    l_i += rs0 + rs1;
+    // phase B: tile t's P fragment by fragment, each fragment's PV MFMAs once it is ready
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      typename MF<T>::e8 pf = pack8<T>(s < 2 ? c0 : c1, s & 1);
+      if (DROP) {
+        uint32_t f[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const int gg = 2 * (s & 1) + g;
+          const uint32_t kq =
+              static_cast<uint32_t>((kv0 + 32 * (s >> 1)) >> 2) + static_cast<uint32_t>(2 * gg + hh);
+          f[g] = keep_flags(mix32(dkey ^ (qbase + kq)), p.drop_xr, p.drop_c);
+        }
+        pf = drop_packed(pf, f[0], f[1]);
+      }
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i)
+        o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * D, tro.hi[i] + 16 * s * D), pf, o[i]);
+    }
+    if constexpr (MORE) {
+      stats(n0, n1, kv0 + BN);
+    }
+  };
+  // the loop keeps its state in fixed registers (unrolled by two over the two score sets);
+  // the wave's last tiles (no next S) and the barriers of the block's remaining tiles
+  // (causal: later waves see more keys) come after it
+  f32x16 sn0 = f32x16{0}, sn1 = f32x16{0};
+  int t = 0;
+  for (; t + 2 < ntw; t += 2) {
+    sync_issue(t);
+    rescale_o();
+    step(t, std::true_type{}, sc0, sc1, sn0, sn1);
+    sync_issue(t + 1);
+    rescale_o();
+    step(t + 1, std::true_type{}, sn0, sn1, sc0, sc1);
+  }
+  if (t + 1 < ntw) {
+    sync_issue(t);
+    rescale_o();
+    step(t, std::true_type{}, sc0, sc1, sn0, sn1);
+    sync_issue(t + 1);
+    rescale_o();
+    step(t + 1, std::false_type{}, sn0, sn1, sc0, sc1);
+    t += 2;
+  } else if (t < ntw) {
+    sync_issue(t);
+    rescale_o();
+    step(t, std::false_type{}, sc0, sc1, sn0, sn1);
+    ++t;
+  }
+  for (; t < nt; ++t) sync_issue(t);
+  if (qrow >= sq) return;
+  const float lt = l_i + xor32(l_i);
+  const float inv = lt > 0.f ? (DROP ? p.drop_rs : 1.f) / lt : 0.f;
+  uint16_t* O = static_cast<uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh + static_cast<int64_t>(qrow) * p.o_ss;
+  store_rows<T, D>(O, o, inv, hh);
+  if (hh == 0) p.lse[bh * p.sq + qrow] = (lt > 0.f) ? (m_i + log2f(lt)) / kLog2e : -INFINITY;
+}
+
 // ============================================================= delta = rowsum(dO * O)
 template <typename T>
 __global__ void __launch_bounds__(kThreads) attn_delta_kernel(AttnBwdParams p) {
@@ -1100,10 +1350,27 @@ inline bool attn_dma_enabled() {
   return v;
 }
 
+// SMP_ATTN_FWD_PIPE=1 selects the software-pipelined forward for D = 64 / 128.  Opt-in: it
+// passes the same tests but measured SLOWER at GPT-2 XL b32 (tools/gpu_attn_pipe_ab.sh, same
+// box, interleaved: 831-845 vs 758-768 us, dropout 0.1 873-876 vs 807-811 us) -- its two
+// live score sets need 205 VGPRs (2 waves / SIMD) where the in-turn loop runs at 124 (4
+// waves / SIMD), and at 3 waves it spills; cross-wave overlap at 4 waves beats in-wave overlap.
+inline bool attn_fwd_pipe_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("SMP_ATTN_FWD_PIPE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
+}
+
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_fwd_v(const AttnParams& p, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
   if constexpr ((D == 64 || D == 128) && !BI) {
+    if (p.window <= 0 && attn_fwd_pipe_enabled()) {
+      attn_fwd_pipe_kernel<T, D, C, DR><<<grid, kThreads, 0, s>>>(p);
+      return static_cast<int>(hipGetLastError());
+    }
     if (attn_dma_enabled()) {
       attn_fwd_kernel<T, D, C, DR, BI, true><<<grid, kThreads, 0, s>>>(p);
       return static_cast<int>(hipGetLastError());

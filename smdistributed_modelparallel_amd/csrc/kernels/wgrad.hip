@@ -278,6 +278,22 @@ __device__ __forceinline__ void stage_glds(uint16_t* lds, const uint16_t* src, i
   }
 }
 
+// instruction i (< TKS / W / 2) of stage_glds: the two rows RPW w + 2 i + {0, 1}
+template <int W, int TKS>
+__device__ __forceinline__ void stage_glds_one(uint16_t* lds, const uint16_t* src, int64_t ld, int vc, int wave,
+                                               int lane, int i) {
+  constexpr int RPW = TKS / W;
+  const int pc = lane & 31, half = lane >> 5;
+  const int r = RPW * wave + 2 * i + half;
+  const int g = ((r & 3) << 2) | ((r >> 2) & 3);
+  int c = pc ^ g;
+  c = c < vc ? c : vc - 1;
+  if (ld < (1 << 24))
+    lds_dma16_sv(src, static_cast<uint32_t>((r * static_cast<int>(ld) + c * 8) * 2), lds + (RPW * wave + 2 * i) * RW);
+  else
+    glds16(src + static_cast<int64_t>(r) * ld + c * 8, lds + (RPW * wave + 2 * i) * RW);
+}
+
 // s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 encoding)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -289,7 +305,11 @@ __device__ __forceinline__ void wait_vm() {
 // two waves per SIMD, each with half the accumulators).  NS-stage ring of TKS-token tiles:
 // the DMA of tile t + NS - 1 is issued right after the barrier that opens tile t, so a load
 // has NS - 1 tiles of MFMA work to land; one barrier per tile.
-template <typename T, int WN, int TKS, int NS>
+// SPREAD: the next tile's DMA instructions are issued one A and one B piece per 16-token
+// k-step, between that step's LDS reads and its MFMAs, instead of as one burst after the
+// barrier (an LDS-DMA issue holds the wave ~60 cycles; in a burst both waves of a SIMD stall
+// their MFMAs at the same time).
+template <typename T, int WN, int TKS, int NS, bool SPREAD = false>
 __global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B, float* __restrict__ ws,
                                                              int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
@@ -333,6 +353,7 @@ __global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t*
   const uint16_t* pa = A + t_begin * lda + n0;
   const uint16_t* pb = B + t_begin * ldb + k0;
   constexpr int STAGE = 2 * TKS * RW;  // elements per stage (A then B)
+  const bool active = n0 + wm * 128 < N && k0 + wn * WCOLS < K;  // wave-uniform
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) {
     if (p < ntiles) {
@@ -347,9 +368,10 @@ __global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t*
     else
       wait_vm<0>();
     __syncthreads();  // ... everyone's, and every wave is done reading tile t - 1's slot
-    if (t + NS - 1 < ntiles) {
-      uint16_t* nxt = smem + load_slot * STAGE;
-      const int64_t tt = t + NS - 1;
+    const bool issue = t + NS - 1 < ntiles;
+    uint16_t* nxt = smem + load_slot * STAGE;
+    const int64_t tt = t + NS - 1;
+    if (!SPREAD && issue) {
       stage_glds<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane);
       stage_glds<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane);
     }
@@ -364,10 +386,25 @@ __global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t*
       for (int i = 0; i < 4; ++i) fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
 #pragma unroll
       for (int j = 0; j < NJ; ++j) fb[j] = ld_tr<T>(sB, bLo[j] + s * 16 * RW, bHi[j] + s * 16 * RW);
+      if constexpr (SPREAD) {
+        constexpr int PER = (TKS / W / 2) / (TKS / 16);  // pieces per operand per k-step
+        static_assert(PER >= 1 && PER * (TKS / 16) == TKS / W / 2, "pieces split evenly over the k-steps");
+        if (issue) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+          for (int q = 0; q < PER; ++q) {
+            stage_glds_one<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane, s * PER + q);
+            stage_glds_one<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane, s * PER + q);
+          }
+        }
+      }
+      // a wave whose whole output block lies past the matrix edge (e.g. 3 of the 4 column
+      // waves of the last 64 of 1600 columns) skips its MFMAs
+      if (active) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
+      }
     }
   }
   float* out = ws + static_cast<int64_t>(split) * N * K;
@@ -584,30 +621,207 @@ int launch_pp(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens,
   return 0;
 }
 
+// ------------------------------------------------------ 16x16x32 MFMA variant
+// Same staging (LDS-DMA ring, swizzled 512-B rows) and 8-wave 128 x 64 output blocks, but
+// v_mfma_f32_16x16x32: 16 cycles per instruction instead of 32, which on gfx950 delivers
+// ~1.12-1.15x the FLOP/s of 32x32x16 in MFMA loops (MI355X_MICROARCH.md).  A 16 x 32 operand
+// fragment is two ds_read_b64_tr_b16: the 16-lane group g takes tokens 8 g .. 8 g + 7 of the
+// 32-token k-step, lane 4 q + p supplying row q (+4), columns 4 p .. 4 p + 3 of its 16-column
+// block; lane l receives column l % 16.  Accumulator: lane l holds C[4 (l / 16) + r][l % 16].
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+struct WMF16;
+template <>
+struct WMF16<bf16> {
+  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x4 mma(e8 a, e8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct WMF16<f16> {
+  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ f32x4 mma(e8 a, e8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, int off_lo, int off_hi) {
+  s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_lo));
+  s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_hi));
+  s16x8 v = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+  return __builtin_bit_cast(typename WMF16<T>::e8, v);
+}
+
+template <typename T, int TKS, int NS, bool SPREAD>
+__global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
+                                                             const uint16_t* __restrict__ B, float* __restrict__ ws,
+                                                             int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
+                                                             int64_t t_split, int group) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  constexpr int W = 8, WCOLS = 64, NI = 8, NJ = 4;  // wave block 128 x 64 = 8 x 4 tiles of 16 x 16
+  constexpr int L = 2 * (TKS / W / 2);
+  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
+  int split, tn, tk;
+  wg_map(tiles_n, tiles_k, group, split, tn, tk);
+  const int n0 = tn * TM, k0 = tk * TN;
+  const int64_t t_begin = split * t_split;
+  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / 4, wn = wave % 4;
+  // transposed-read offsets for k-step 0: row 8 (l / 16) + q (+4), column block base + 4 p
+  int aLo[NI], aHi[NI], bLo[NJ], bHi[NJ];
+  {
+    const int row = 8 * (lane >> 4) + ((lane & 15) >> 2), pp = lane & 3;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int ca = wm * 128 + 16 * i + 4 * pp;
+      aLo[i] = swz(row, ca >> 3) + (ca & 7);
+      aHi[i] = swz(row + 4, ca >> 3) + (ca & 7);
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cb = wn * WCOLS + 16 * j + 4 * pp;
+      bLo[j] = swz(row, cb >> 3) + (cb & 7);
+      bHi[j] = swz(row + 4, cb >> 3) + (cb & 7);
+    }
+  }
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
+  const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
+  const int64_t ntiles = (t_end - t_begin) / TKS;
+  const uint16_t* pa = A + t_begin * lda + n0;
+  const uint16_t* pb = B + t_begin * ldb + k0;
+  constexpr int STAGE = 2 * TKS * RW;
+  const bool active = n0 + wm * 128 < N && k0 + wn * WCOLS < K;  // wave-uniform
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) {
+    if (p < ntiles) {
+      stage_glds<W, TKS>(smem + p * STAGE, pa + p * TKS * lda, lda, vcA, wave, lane);
+      stage_glds<W, TKS>(smem + p * STAGE + TKS * RW, pb + p * TKS * ldb, ldb, vcB, wave, lane);
+    }
+  }
+  int cur_slot = 0, load_slot = NS - 1;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    if (t + NS - 2 < ntiles)
+      wait_vm<(NS - 2) * L>();
+    else
+      wait_vm<0>();
+    __syncthreads();
+    const bool issue = t + NS - 1 < ntiles;
+    uint16_t* nxt = smem + load_slot * STAGE;
+    const int64_t tt = t + NS - 1;
+    if (!SPREAD && issue) {
+      stage_glds<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane);
+      stage_glds<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane);
+    }
+    load_slot = load_slot + 1 == NS ? 0 : load_slot + 1;
+    const uint16_t* sA = smem + cur_slot * STAGE;
+    const uint16_t* sB = sA + TKS * RW;
+    cur_slot = cur_slot + 1 == NS ? 0 : cur_slot + 1;
+#pragma unroll
+    for (int s = 0; s < TKS / 32; ++s) {
+      typename WMF16<T>::e8 fa[NI / 2], fb[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) fb[j] = ld_tr16<T>(sB, bLo[j] + s * 32 * RW, bHi[j] + s * 32 * RW);
+#pragma unroll
+      for (int i = 0; i < NI / 2; ++i) fa[i] = ld_tr16<T>(sA, aLo[i] + s * 32 * RW, aHi[i] + s * 32 * RW);
+      if constexpr (SPREAD) {
+        constexpr int PER = (TKS / W / 2) / (TKS / 32);
+        static_assert(PER >= 1 && PER * (TKS / 32) == TKS / W / 2, "pieces split evenly over the k-steps");
+        if (issue) {
+#pragma unroll
+          for (int q = 0; q < PER; ++q) {
+            stage_glds_one<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane, s * PER + q);
+            stage_glds_one<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane, s * PER + q);
+          }
+        }
+      }
+      // the A fragments in two halves of 4 (fewer live registers)
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NI / 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = WMF16<T>::mma(fa[i], fb[j], acc[i][j]);
+      }
+#pragma unroll
+      for (int i = 0; i < NI / 2; ++i)
+        fa[i] = ld_tr16<T>(sA, aLo[NI / 2 + i] + s * 32 * RW, aHi[NI / 2 + i] + s * 32 * RW);
+      if (active) {
+#pragma unroll
+        for (int i = 0; i < NI / 2; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[NI / 2 + i][j] = WMF16<T>::mma(fa[i], fb[j], acc[NI / 2 + i][j]);
+      }
+    }
+  }
+  float* out = ws + static_cast<int64_t>(split) * N * K;
+  const int col_l = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = k0 + wn * WCOLS + 16 * j + col_l;
+    if (k >= K) continue;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int nb = n0 + wm * 128 + 16 * i + rq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = nb + r;
+        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+template <typename T, int TKS, int NS, bool SPREAD>
+int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
+                  int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
+  constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t);
+  static_assert(lds <= 160 * 1024, "LDS per CU");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds16_kernel<T, TKS, NS, SPREAD>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    attr_set = true;
+  }
+  wgrad_glds16_kernel<T, TKS, NS, SPREAD><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
+                                                                 wgrad_group());
+  return 0;
+}
+
 // SMP_WGRAD_PIPE: 0 = 4 waves, 2 x 64-token stages; 1 = 8 waves, 2 x 64; 2 = 8 waves,
-// 4 x 32; 3 = 8 waves, 5 x 32 (all 160 KB of LDS); 4 = phased, lockstep; 5 = phased ping-pong
+// 4 x 32; 3 = 8 waves, 5 x 32 (all 160 KB of LDS); 4 = phased, lockstep; 5 = phased ping-pong;
+// 6 / 7 = 1 / 2 with the DMA spread over the k-steps; 8 / 9 = 1 / 6 on 16x16x32 MFMAs.
+// Default 8 (tools/gpu_wgrad_ab.sh, same box, interleaved, ms at T = 65536: 4800x1600 s8
+// 1.123 vs 1.163, 6400x1600 s4 1.359-1.364 vs 1.419, 1600x6400 s4 1.454-1.471 vs 1.498,
+// 1600x1600 s5 0.360-0.363 vs 0.370; spreading the DMA over the k-steps: no gain)
 inline int wgrad_pipe() {
   static const int v = [] {
     const char* e = getenv("SMP_WGRAD_PIPE");
-    if (e != nullptr && e[0] >= '0' && e[0] <= '5') return e[0] - '0';
+    if (e != nullptr && e[0] >= '0' && e[0] <= '9') return e[0] - '0';
     const char* w = getenv("SMP_WGRAD_WAVES");
-    return (w != nullptr && w[0] == '4') ? 0 : 1;
+    return (w != nullptr && w[0] == '4') ? 0 : 8;
   }();
   return v;
 }
 
-template <typename T, int WN, int TKS, int NS>
+template <typename T, int WN, int TKS, int NS, bool SPREAD = false>
 int launch_glds(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
                 int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
   constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t);
   static_assert(lds <= 160 * 1024, "LDS per CU");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<T, WN, TKS, NS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<T, WN, TKS, NS, SPREAD>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr_set = true;
   }
-  wgrad_glds_kernel<T, WN, TKS, NS><<<grid, 128 * WN, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
+  wgrad_glds_kernel<T, WN, TKS, NS, SPREAD><<<grid, 128 * WN, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
   return 0;
 }
 
@@ -625,6 +839,14 @@ int launch_glds_pipe(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t 
       return launch_pp<T, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
     case 5:
       return launch_pp<T, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 6:
+      return launch_glds<T, 4, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 7:
+      return launch_glds<T, 4, 32, 4, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 8:
+      return launch_glds16<T, 64, 2, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
+    case 9:
+      return launch_glds16<T, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
     default:
       return launch_glds<T, 4, 64, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
   }

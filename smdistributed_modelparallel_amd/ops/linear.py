@@ -215,7 +215,7 @@ def _wgrad_native_ok(g, dy2, x2):
 # per-shape winners measured on MI355X at T = 65536 (profiles/r2/session4_wgrad_pick_ab.md),
 # keyed by (N, K); other shapes use the library GEMM.  No timing trials, no host sync in the
 # backward, and the same split-K accumulation order in every run and on every rank.
-_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7}
+_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 8}
 _WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "time")
 
 
