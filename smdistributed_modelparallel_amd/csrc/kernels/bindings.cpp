@@ -347,7 +347,10 @@ at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> 
 // Weight gradient: c (+)= dy^T x with dy [tokens, n], x [tokens, k] (rows may be strided,
 // elements contiguous), c contiguous [n, k] (bf16/f16/f32 -- the bound .grad view or an fp32
 // main grad).  splits = 0: chosen for the device's CU count.
-void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t splits) {
+// dbias given (bf16 operands): dbias (+)= sum over tokens of dy from the same kernel pass
+// (dbias_accumulate: add into it, else overwrite).
+void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t splits,
+            c10::optional<at::Tensor> dbias_opt, bool dbias_accumulate) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_: GPU tensors required");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_: 2-D operands required");
   TORCH_CHECK(dy.size(0) == x.size(0), "wgrad_: token counts differ");
@@ -364,19 +367,31 @@ void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t 
   }
   // the kernel takes whole 64-token tiles; the remainder rows go through the library GEMM
   const int64_t main_t = tokens / 64 * 64, tail = tokens - main_t;
+  at::Tensor dbias;
+  if (dbias_opt.has_value() && dbias_opt->defined()) {
+    dbias = *dbias_opt;
+    TORCH_CHECK(dbias.is_cuda() && dbias.is_contiguous() && dbias.numel() == n, "wgrad_: dbias must be [n]");
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16, "wgrad_: fused bias gradient needs bf16 operands");
+    TORCH_CHECK(dbias.scalar_type() == at::kBFloat16 || dbias.scalar_type() == at::kFloat,
+                "wgrad_: dbias must be bf16 or fp32");
+  }
   if (main_t == 0) {
     if (!accumulate) c.zero_();
+    if (dbias.defined() && !dbias_accumulate) dbias.zero_();
   } else {
-    auto ws = at::empty({splits * n * k}, dy.options().dtype(at::kFloat));
+    auto ws = at::empty({splits * n * k + (dbias.defined() ? splits * n : 0)}, dy.options().dtype(at::kFloat));
+    float* cs = dbias.defined() ? ws.data_ptr<float>() + splits * n * k : nullptr;
     check(smpk::wgrad(dt_code(dy), dy.data_ptr(), x.data_ptr(), dt_code(c), c.data_ptr(), ws.data_ptr<float>(), main_t,
                       static_cast<int>(n), static_cast<int>(k), dy.stride(0), x.stride(0), static_cast<int>(splits),
-                      accumulate ? 1 : 0, stream()),
+                      accumulate ? 1 : 0, stream(), dbias.defined() ? dt_code(dbias) : 0,
+                      dbias.defined() ? dbias.data_ptr() : nullptr, cs, dbias_accumulate ? 1 : 0),
           "wgrad");
   }
   if (tail > 0) {
     // < 64 rows: fp32 (no bf16 rounding of the partial product)
     auto part = at::mm(dy.narrow(0, main_t, tail).to(at::kFloat).t(), x.narrow(0, main_t, tail).to(at::kFloat));
     c.add_(part.to(c.scalar_type()));
+    if (dbias.defined()) dbias.add_(dy.narrow(0, main_t, tail).to(at::kFloat).sum(0).to(dbias.scalar_type()));
   }
 }
 
@@ -683,7 +698,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_into", &transpose_into);
   m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
   m.def("wgrad_", &wgrad_, py::arg("c"), py::arg("dy"), py::arg("x"), py::arg("accumulate") = true,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("dbias") = py::none(), py::arg("dbias_accumulate") = true);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),

@@ -372,7 +372,59 @@ __global__ void __launch_bounds__(256) bias_gelu_fwd_flat(const T* __restrict__ 
   }
 }
 
-// Default for the forward (tools/membw_probe.py, MI355X, [65536, 6400] bf16: 341 us = 4.9 TB/s
+// ---------------------------------------------------------------- one-pass streaming
+// One 16-byte vector per lane, one pass (grid = vectors / 256, no grid-stride loop): each
+// block streams 4 KB of consecutive memory once.  tools/membw/stream_variants.hip on MI355X
+// ([65536, 6400] bf16 read + write): 6.18 TB/s for this shape of access against 4.4-4.6 TB/s
+// for grid-stride loops of 1024-4096 blocks (any unroll), which is what the flat / walker
+// kernels were.  The bias column comes from L1/L2 (a 12.8 KB row); 32-bit index math.
+template <typename T, int ACT, bool BWD>
+__global__ void __launch_bounds__(256) bias_gelu_once(const T* __restrict__ dy, const T* __restrict__ x,
+                                                      const T* __restrict__ bias, T* __restrict__ y, uint32_t nvec,
+                                                      uint32_t cv) {
+  constexpr int N = Vec16<T>::N;
+  const uint32_t v = blockIdx.x * 256u + threadIdx.x;
+  if (v >= nvec) return;
+  const Vec16<T> a = load16(x + static_cast<int64_t>(v) * N);
+  Vec16<T> bv;
+  if (bias != nullptr) {
+    bv = load16(bias + (v % cv) * N);
+  } else {
+    bv.raw = make_uint4(0, 0, 0, 0);
+  }
+  Vec16<T> o;
+  if constexpr (BWD) {
+    const Vec16<T> d = load16(dy + static_cast<int64_t>(v) * N);
+#pragma unroll
+    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(to_f32(d.v[j]) * act_grad<ACT>(to_f32(a.v[j]) + to_f32(bv.v[j])));
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a.v[j]) + to_f32(bv.v[j])));
+  }
+  store16(y + static_cast<int64_t>(v) * N, o);
+}
+
+// SMP_GELU_ONCE=0 restores the grid-stride kernels (forward: flat, backward: elementwise)
+inline bool gelu_once_enabled() {
+  const char* e = getenv("SMP_GELU_ONCE");
+  return e == nullptr || e[0] != '0';
+}
+
+template <typename T, bool BWD>
+void launch_once(const void* dy, const void* x, const void* bias, void* y, int64_t nvec, int64_t cv, bool exact,
+                 hipStream_t s) {
+  const unsigned g = static_cast<unsigned>((nvec + 255) / 256);
+  if (exact)
+    bias_gelu_once<T, 1, BWD><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                static_cast<const T*>(bias), static_cast<T*>(y),
+                                                static_cast<uint32_t>(nvec), static_cast<uint32_t>(cv));
+  else
+    bias_gelu_once<T, 0, BWD><<<g, 256, 0, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
+                                                static_cast<const T*>(bias), static_cast<T*>(y),
+                                                static_cast<uint32_t>(nvec), static_cast<uint32_t>(cv));
+}
+
+// Previous forward default (tools/membw_probe.py, MI355X, [65536, 6400] bf16: 341 us = 4.9 TB/s
 // vs 415 us for the column walker); SMP_GELU_FLAT=0 restores the walker.
 inline bool gelu_flat_enabled() {
   const char* e = getenv("SMP_GELU_FLAT");
@@ -628,7 +680,9 @@ int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
                                           reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
     const int vpl = vec ? rows_vpl<T>(rows, cols) : 0;
-    if (vec && bias != nullptr && gelu_flat_enabled()) {
+    if (vec && total / N < (int64_t{1} << 31) && gelu_once_enabled()) {
+      launch_once<T, false>(nullptr, x, bias, y, total / N, cols / N, exact, s);
+    } else if (vec && bias != nullptr && gelu_flat_enabled()) {
       const int64_t nvec = total / N;
       int64_t grid = nvec / (256 * 4);
       if (grid > 2048) grid = 2048;
@@ -682,7 +736,9 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                                           reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) &
                                          15) == 0;
-    if (vec && exact)
+    if (vec && total / N < (int64_t{1} << 31) && gelu_once_enabled())
+      launch_once<T, true>(dy, x, bias, dx, total / N, cols / N, exact, s);
+    else if (vec && exact)
       launch_gelu_bwd<T, true, 1>(dy, x, bias, dx, rows, cols, s);
     else if (vec)
       launch_gelu_bwd<T, true, 0>(dy, x, bias, dx, rows, cols, s);

@@ -654,20 +654,26 @@ __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, i
   return __builtin_bit_cast(typename WMF16<T>::e8, v);
 }
 
+// cs != nullptr: the blocks of the first K tile also sum their staged A (= dY) rows per
+// column -- the bias gradient of the layer, sum over tokens of dY, in the same pass over dY
+// (fp32, fixed order: rows of a tile per thread, 16 row groups through LDS, splits in order)
+// -- into cs[split][N]; no separate column-sum pass over dY.
+//
+// One SEGMENT = output tile (tn, tk) over `ntiles` 64-token tiles from token t_begin; the fp32
+// partial goes to out[(n - nb0) * ldo + (k - kb0)] and (colsum) the column sums to
+// cso[n - nb0].  Split mode: one segment per workgroup, out = the split's [N][K] slice.
+// (A stream-K style schedule -- equal runs of (tile, token-tile) items per workgroup, up to two
+// segments each, partial tiles summed in order -- was built on these segments and measured
+// 10-35 % SLOWER on every GPT-2 XL shape (profiles/r3/wgrad_variants.md): concurrent
+// workgroups then stream disjoint token ranges and stop sharing A / B strips in L2.)
 template <typename T, int TKS, int NS, bool SPREAD>
-__global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
-                                                             const uint16_t* __restrict__ B, float* __restrict__ ws,
-                                                             int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
-                                                             int64_t t_split, int group) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+__device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                               uint16_t* smem, int N, int K, int64_t lda, int64_t ldb, int tn, int tk,
+                                               int64_t t_begin, int64_t ntiles, float* __restrict__ out,
+                                               int64_t ldo, int nb0, int kb0, float* __restrict__ cso, bool colsum) {
   constexpr int W = 8, WCOLS = 64, NI = 8, NJ = 4;  // wave block 128 x 64 = 8 x 4 tiles of 16 x 16
   constexpr int L = 2 * (TKS / W / 2);
-  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
-  int split, tn, tk;
-  wg_map(tiles_n, tiles_k, group, split, tn, tk);
   const int n0 = tn * TM, k0 = tk * TN;
-  const int64_t t_begin = split * t_split;
-  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / 4, wn = wave % 4;
   // transposed-read offsets for k-step 0: row 8 (l / 16) + q (+4), column block base + 4 p
@@ -694,11 +700,18 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
   const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
-  const int64_t ntiles = (t_end - t_begin) / TKS;
   const uint16_t* pa = A + t_begin * lda + n0;
   const uint16_t* pb = B + t_begin * ldb + k0;
   constexpr int STAGE = 2 * TKS * RW;
   const bool active = n0 + wm * 128 < N && k0 + wn * WCOLS < K;  // wave-uniform
+  // column-sum accumulators in LDS after the operand ring (no registers held across the
+  // loop: the kernel is at its VGPR limit): thread (row group t >> 5, chunk t & 31) owns
+  // floats [(t >> 5) * 256 + (t & 31) * 8, +8)
+  float* csl = reinterpret_cast<float*>(smem + NS * STAGE) + (threadIdx.x >> 5) * 256 + (threadIdx.x & 31) * 8;
+  if (colsum) {
+    *reinterpret_cast<f32x4*>(csl) = f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(csl + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p) {
     if (p < ntiles) {
@@ -724,6 +737,25 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
     const uint16_t* sA = smem + cur_slot * STAGE;
     const uint16_t* sB = sA + TKS * RW;
     cur_slot = cur_slot + 1 == NS ? 0 : cur_slot + 1;
+    if (colsum) {
+      const int ch = threadIdx.x & 31;
+      f32x4 c0 = *reinterpret_cast<const f32x4*>(csl), c1 = *reinterpret_cast<const f32x4*>(csl + 4);
+#pragma unroll
+      for (int i = 0; i < TKS / 16; ++i) {
+        const int row = (threadIdx.x >> 5) + 16 * i;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(sA + swz(row, ch));
+        c0[0] += __uint_as_float(v[0] << 16);
+        c0[1] += __uint_as_float(v[0] & 0xffff0000u);
+        c0[2] += __uint_as_float(v[1] << 16);
+        c0[3] += __uint_as_float(v[1] & 0xffff0000u);
+        c1[0] += __uint_as_float(v[2] << 16);
+        c1[1] += __uint_as_float(v[2] & 0xffff0000u);
+        c1[2] += __uint_as_float(v[3] << 16);
+        c1[3] += __uint_as_float(v[3] & 0xffff0000u);
+      }
+      *reinterpret_cast<f32x4*>(csl) = c0;
+      *reinterpret_cast<f32x4*>(csl + 4) = c1;
+    }
 #pragma unroll
     for (int s = 0; s < TKS / 32; ++s) {
       typename WMF16<T>::e8 fa[NI / 2], fb[NJ];
@@ -760,7 +792,17 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
       }
     }
   }
-  float* out = ws + static_cast<int64_t>(split) * N * K;
+  if (colsum) {
+    // the 16 row groups' sums of each of the 256 columns
+    __syncthreads();
+    const float* red = reinterpret_cast<const float*>(smem + NS * STAGE);
+    if (threadIdx.x < 256 && n0 + static_cast<int>(threadIdx.x) < N) {
+      float a = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) a += red[g * 256 + threadIdx.x];
+      cso[n0 + threadIdx.x - nb0] = a;
+    }
+  }
   const int col_l = lane & 15, rq = 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
@@ -772,16 +814,34 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = nb + r;
-        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
+        if (n < N) out[static_cast<int64_t>(n - nb0) * ldo + (k - kb0)] = acc[i][j][r];
       }
     }
   }
 }
 
 template <typename T, int TKS, int NS, bool SPREAD>
+__global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
+                                                             const uint16_t* __restrict__ B, float* __restrict__ ws,
+                                                             int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
+                                                             int64_t t_split, int group, float* __restrict__ cs) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
+  int split, tn, tk;
+  wg_map(tiles_n, tiles_k, group, split, tn, tk);
+  const int64_t t_begin = split * t_split;
+  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  glds16_segment<T, TKS, NS, SPREAD>(A, B, smem, N, K, lda, ldb, tn, tk, t_begin, (t_end - t_begin) / TKS,
+                                     ws + static_cast<int64_t>(split) * N * K, K, 0, 0,
+                                     cs != nullptr ? cs + static_cast<int64_t>(split) * N : nullptr,
+                                     cs != nullptr && tk == 0);
+}
+
+template <typename T, int TKS, int NS, bool SPREAD>
 int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
-                  int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
-  constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t);
+                  int64_t ldb, int64_t t_split, int grid, hipStream_t s, float* cs = nullptr) {
+  // operand ring + the column-sum accumulators (16 row groups x 256 fp32)
+  constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t) + 16 * 256 * sizeof(float);
   static_assert(lds <= 160 * 1024, "LDS per CU");
   static bool attr_set = false;
   if (!attr_set) {
@@ -790,7 +850,7 @@ int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tok
     attr_set = true;
   }
   wgrad_glds16_kernel<T, TKS, NS, SPREAD><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
-                                                                 wgrad_group());
+                                                                 wgrad_group(), cs);
   return 0;
 }
 
@@ -883,6 +943,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   c[i + 3] = from_f32<TO>(s.w);
 }
 
+// bias (+)= sum over splits of cs[split][n]
+template <typename TO>
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ cs, TO* __restrict__ bias, int n,
+                                                            int splits, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a = accumulate ? to_f32(bias[i]) : 0.f;
+  for (int p = 0; p < splits; ++p) a += cs[static_cast<int64_t>(p) * n + i];
+  bias[i] = from_f32<TO>(a);
+}
+
 }  // namespace
 
 int wgrad_splits(int64_t tokens, int n, int k, int num_cus) {
@@ -904,14 +975,24 @@ int wgrad_splits(int64_t tokens, int n, int k, int num_cus) {
 }
 
 int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
-          int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s) {
+          int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s, int bias_dt, void* bias, float* cs,
+          int bias_accumulate) {
   // whole 64-token tiles only (the caller adds the token remainder)
   if (n % 8 != 0 || k % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || splits < 1 || tokens % TK != 0) return -1;
+  if (bias != nullptr && (dt != BF16 || cs == nullptr)) return -3;  // column sums: bf16 operands
   const int tiles = ((n + TM - 1) / TM) * ((k + TN - 1) / TN);
   int64_t t_split = (tokens + splits - 1) / splits;
   t_split = (t_split + TK - 1) / TK * TK;
   const int grid = tiles * splits;
-  if (wgrad_use_glds()) {
+  if (bias != nullptr) {
+    // the column-sum pass lives in the 16x16x32 kernel
+    const auto* pa = static_cast<const uint16_t*>(a);
+    const auto* pb = static_cast<const uint16_t*>(b);
+    if (wgrad_pipe() == 9)
+      launch_glds16<bf16, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
+    else
+      launch_glds16<bf16, 64, 2, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
+  } else if (wgrad_use_glds()) {
     const auto* pa = static_cast<const uint16_t*>(a);
     const auto* pb = static_cast<const uint16_t*>(b);
     if (dt == BF16)
@@ -940,6 +1021,15 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
     wgrad_reduce_kernel<f16><<<rgrid, 256, 0, s>>>(ws, static_cast<f16*>(c), nk, splits, accumulate);
   else
     return -2;
+  if (bias != nullptr) {
+    const unsigned g = static_cast<unsigned>((n + 255) / 256);
+    if (bias_dt == F32)
+      colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, splits, bias_accumulate);
+    else if (bias_dt == BF16)
+      colsum_reduce_kernel<bf16><<<g, 256, 0, s>>>(cs, static_cast<bf16*>(bias), n, splits, bias_accumulate);
+    else
+      return -2;
+  }
   return hipGetLastError();
 }
 

@@ -37,6 +37,7 @@ from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
 from ..ops.dropout import dropout_add as _dropout_add
+from ..ops import linear as _lin
 from ..ops.gelu import bias_gelu
 from ..ops import lm_head as lm_head_op
 from ..ops.linear import linear
@@ -245,14 +246,15 @@ def _normal_init(emb, std):
     state.param_initializers[emb] = init
 
 
-def _activation(x, kind, bias=None, tanh_gelu=False):
+def _activation(x, kind, bias=None, tanh_gelu=False, bias_grad=True):
     """"gelu" follows the reference (`smp/torch/nn/transformer.py:994,1096-1127`): the exact
     erf GeLU (F.gelu) unless fused_bias_gelu or SMP_USE_HF_GELU=1 select the tanh form
-    (HF "gelu_new"); "gelu_exact" is always erf.  Both run as one fused bias+GeLU kernel."""
+    (HF "gelu_new"); "gelu_exact" is always erf.  Both run as one fused bias+GeLU kernel;
+    ``bias_grad=False`` leaves the bias gradient to the producing linear (``dbias_of``)."""
     if kind == "gelu":
-        return bias_gelu(x, bias, exact=not tanh_gelu)
+        return bias_gelu(x, bias, exact=not tanh_gelu, bias_grad=bias_grad)
     if kind == "gelu_exact":
-        return bias_gelu(x, bias, exact=True)
+        return bias_gelu(x, bias, exact=True, bias_grad=bias_grad)
     if bias is not None:
         x = x + bias
     if kind == "relu":
@@ -543,9 +545,14 @@ class DistributedTransformerOutputLayer(DistributedModule):
             x = _activation(x, self.activation, None, self._tanh_gelu)
             out = linear(x, self.dense2_weight, self.dense2_bias)
             return reduce_scatter_for_tp(out, 2, get_merge_shapes(self.hidden_size))
-        # dense1's backward all-reduces dX asynchronously behind its weight-gradient GEMM
-        x = linear(m, self.dense1_weight, dx_allreduce=dx_allreduce_async if self._tp > 1 else None)
-        x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu)
+        # dense1's backward all-reduces dX asynchronously behind its weight-gradient GEMM; on
+        # GPU it also takes dense1_bias's gradient (summed by its weight-gradient kernel from
+        # the dY it reads anyway), so the bias-GeLU backward is a pure elementwise pass
+        fuse_db = (self.dense1_bias is not None and m.is_cuda and m.dtype == torch.bfloat16 and _lin._WGRAD_DBIAS
+                   and self.activation in ("gelu", "gelu_exact"))
+        x = linear(m, self.dense1_weight, dx_allreduce=dx_allreduce_async if self._tp > 1 else None,
+                   dbias_of=self.dense1_bias if fuse_db else None)
+        x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu, bias_grad=not fuse_db)
         out = linear(x, self.dense2_weight, self.dense2_bias)
         return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
 

@@ -200,6 +200,7 @@ def _wgrad_pick(g, dy2, x2):
 _WGRAD_KERNEL = os.environ.get("SMP_WGRAD_KERNEL", "auto")
 _WGRAD_KERNEL_MIN_T = int(os.environ.get("SMP_WGRAD_KERNEL_MIN_TOKENS", "4096"))
 _WGRAD_KERNEL_CHOICE = {}
+_WGRAD_KERNEL_SPLIT_BEST = {}  # (T, N, K) -> fastest kernel split count seen by the timing pick
 _WGRAD_PICK_ROUNDS = max(1, int(os.environ.get("SMP_WGRAD_PICK_ROUNDS", "2")))
 
 
@@ -216,6 +217,8 @@ def _wgrad_native_ok(g, dy2, x2):
 # keyed by (N, K); other shapes use the library GEMM.  No timing trials, no host sync in the
 # backward, and the same split-K accumulation order in every run and on every rank.
 _WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 8}
+# kernel split count for (1600, 6400) when the fused bias pass makes the kernel the choice
+_WGRAD_STATIC_KERNEL = {(1600, 6400): 4}
 _WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "time")
 
 
@@ -269,6 +272,9 @@ def _wgrad_kernel_splits(g, dy2, x2):
     del saved
     best = min(times, key=times.get)
     _WGRAD_KERNEL_CHOICE[key] = best
+    ks = {sp: t for sp, t in times.items() if sp != 0}
+    if ks:
+        _WGRAD_KERNEL_SPLIT_BEST[(key[0], key[1], key[2])] = min(ks, key=ks.get)
     if os.environ.get("SMP_WGRAD_LOG") == "1":
         print(f"wgrad T={key[0]} N={key[1]} K={key[2]}: "
               + ", ".join(f"{'library' if s == 0 else f'kernel s{s}'} {t / 3:.3f} ms" for s, t in times.items())
@@ -280,15 +286,35 @@ def _wgrad_kernel_wins(g, dy2, x2):
     return _wgrad_kernel_splits(g, dy2, x2) != 0
 
 
-def _wgrad_accumulate(g, dy2, x2):
-    """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape."""
+# Bias gradients from the weight-gradient kernel (SMP_WGRAD_DBIAS, default on): when a layer's
+# weight gradient runs on the MFMA kernel with bf16 operands, the kernel also sums dY over the
+# tokens (the bias gradient) from the dY tiles it stages anyway, so no separate column-sum
+# pass reads dY again -- and for the MLP's first projection, whose bias is added by the fused
+# bias-GeLU, that GeLU's backward becomes a pure elementwise pass (ops/gelu.py bias_grad).
+# Fused when dY is wide (>= SMP_WGRAD_DBIAS_MIN_N columns): the pass costs the kernel a roughly
+# fixed 0.01-0.07 ms while a column-sum kernel costs ~0.03 ms per 100 MB of dY (MI355X, T = 65536,
+# tools/wgrad_ab.py WG_DBIAS=1: QKV 4800 columns 0.126 ms -> +0.003-0.02, fc1 6400 0.163 ->
+# +0.065, but proj / fc2 1600 0.046 -> +0.05-0.075).
+_WGRAD_DBIAS = os.environ.get("SMP_WGRAD_DBIAS", "1") != "0"
+_WGRAD_DBIAS_MIN_N = int(os.environ.get("SMP_WGRAD_DBIAS_MIN_N", "4096"))
+
+
+def _wgrad_accumulate(g, dy2, x2, dbias=None):
+    """g += dy2^T x2 with the weight-gradient algorithm chosen for this shape.  ``dbias``: a
+    tensor to accumulate the column sums of dy2 into from the same kernel pass; returns True
+    when that happened (False: the caller computes them)."""
     if _wgrad_native_ok(g, dy2, x2):
         s = _wgrad_kernel_splits(g, dy2, x2)
+        fuse = (dbias is not None and _WGRAD_DBIAS and dy2.dtype == torch.bfloat16
+                and dy2.shape[1] >= _WGRAD_DBIAS_MIN_N)
+        if fuse and s == 0:
+            # the fused bias pass makes the kernel the cheaper choice (it saves a full read of dY)
+            s = _wgrad_dbias_splits(dy2, x2)
         if s != 0:
             from ._ext import ext
 
-            ext().wgrad_(g, dy2, x2, True, max(s, 0))
-            return
+            ext().wgrad_(g, dy2, x2, True, max(s, 0), dbias if fuse else None, True)
+            return fuse
     method = "nn"
     if _WGRAD_TUNE and g.is_cuda and dy2.shape[0] >= _WGRAD_MIN_T and dy2.is_contiguous() and x2.is_contiguous():
         key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype)
@@ -296,6 +322,18 @@ def _wgrad_accumulate(g, dy2, x2):
         if method is None:
             method = _WGRAD_CHOICE[key] = _wgrad_pick(g, dy2, x2)
     _wgrad_run(method, g, dy2, x2)
+    return False
+
+
+def _wgrad_dbias_splits(dy2, x2):
+    """Kernel split count for a shape whose timed pick was the library GEMM (the fused bias
+    pass is not part of that timing): the fastest kernel count measured, or the static table."""
+    key = (dy2.shape[0], dy2.shape[1], x2.shape[1])
+    hit = _WGRAD_KERNEL_SPLIT_BEST.get(key)
+    if hit:
+        return hit
+    k = (dy2.shape[1], x2.shape[1])
+    return _WGRAD_STATIC.get(k, 0) or _WGRAD_STATIC_KERNEL.get(k, -1)
 
 
 # Weight gradients on a side HIP stream (opt-in, SMP_WGRAD_STREAM=1): dW = dY^T X is off the
@@ -355,16 +393,19 @@ TP_OVERLAP_TRACE = []
 
 class _LinearWGradAccum(torch.autograd.Function):
     """y = x W^T + b with (a) the weight gradient accumulated by a GEMM straight into the
-    flat gradient buffer and (b) optionally the tensor-parallel all-reduce of the input
+    flat gradient buffer, (b) the bias gradient -- of ``b`` or of ``dbias_of``, a bias that a
+    fused activation adds downstream -- summed by the weight-gradient kernel in the same pass
+    over dY when that kernel runs, and (c) optionally the tensor-parallel all-reduce of the input
     gradient (column-parallel layer of the speed mode; reference `nn/utils.py:548-570`
     BackwardAllreduceForTP) issued asynchronously right after dX and waited for only after
     the weight-gradient GEMM, so the two overlap."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, dx_allreduce=None):
+    def forward(ctx, x, weight, bias, dx_allreduce=None, dbias_of=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias = bias
+        ctx.dbias_of = dbias_of
         ctx.dx_allreduce = dx_allreduce
         ctx.wt = _transposed(weight) if _use_transposed(weight) else None
         return F.linear(x, weight, bias)
@@ -372,7 +413,8 @@ class _LinearWGradAccum(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dx = db = dw = None
+        dx = dw = None
+        grads = {2: None, 4: None}  # input index -> gradient returned to autograd
         work = None
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.needs_input_grad[0]:
@@ -381,11 +423,16 @@ class _LinearWGradAccum(torch.autograd.Function):
                 work = ctx.dx_allreduce(dx)  # fresh tensor: reduced in place, async when large
                 if TRACE_TP_OVERLAP:
                     TP_OVERLAP_TRACE.append("dx_allreduce_start")
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            if _fusable(ctx.bias) and dy2.is_cuda:
-                _col_sum(dy2, ctx.bias.grad)  # into the bound flat-buffer view (no temp + add)
-            else:
-                db = _col_sum(dy2)
+        # the bias whose gradient is colsum(dY): this layer's own, or the downstream one
+        bidx = 2 if (ctx.has_bias and ctx.needs_input_grad[2]) else (
+            4 if (ctx.dbias_of is not None and ctx.needs_input_grad[4]) else None)
+        bparam = None if bidx is None else (ctx.bias if bidx == 2 else ctx.dbias_of)
+        # fused target: the bound flat-buffer view (accumulated in place), else a fresh fp32 sum
+        btarget = None
+        if bparam is not None and dy2.is_cuda:
+            btarget = bparam.grad if _fusable(bparam) else torch.zeros(bparam.shape, dtype=torch.float32,
+                                                                        device=dy2.device)
+        bdone = False
         if ctx.needs_input_grad[1]:
             if _fusable(w):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the
@@ -394,26 +441,38 @@ class _LinearWGradAccum(torch.autograd.Function):
                 if _WGRAD_STREAM and dy2.is_cuda:
                     _wgrad_async(w.grad, dy2, x.reshape(-1, x.shape[-1]))
                 else:
-                    _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]))
+                    bdone = _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]), dbias=btarget)
             else:
                 # grad slot re-bound/removed since forward: hand the gradient to autograd
                 dw = dy2.t().mm(x.reshape(-1, x.shape[-1]))
             if TRACE_TP_OVERLAP:
                 TP_OVERLAP_TRACE.append("wgrad")
+        if bparam is not None:
+            if not bdone:
+                if btarget is not None and btarget is bparam.grad:
+                    _col_sum(dy2, btarget)  # into the bound flat-buffer view (no temp + add)
+                else:
+                    btarget = _col_sum(dy2)
+            if btarget is not bparam.grad:
+                grads[bidx] = btarget.to(bparam.dtype)
         if work is not None:
             work.wait()
             if TRACE_TP_OVERLAP:
                 TP_OVERLAP_TRACE.append("dx_allreduce_wait")
-        return dx, dw, db, None
+        return dx, dw, grads[2], None, grads[4]
 
 
-def linear(x, weight, bias=None, dx_allreduce=None):
+def linear(x, weight, bias=None, dx_allreduce=None, dbias_of=None):
     """F.linear with GEMM-fused weight-gradient accumulation into the flat grad buffer.
     ``dx_allreduce(dx) -> work | None``: the column-parallel layer's input-gradient
     all-reduce, overlapped with the weight-gradient GEMM (the caller then applies no
-    separate backward all-reduce to x)."""
-    if torch.is_grad_enabled() and (weight.requires_grad or x.requires_grad) and dx_allreduce is not None:
-        return _LinearWGradAccum.apply(x, weight, bias, dx_allreduce)
+    separate backward all-reduce to x).  ``dbias_of``: a bias added to this layer's output
+    by a fused activation that leaves its gradient to this layer (``bias_gelu(...,
+    bias_grad=False)``): its gradient, the token sum of dY, is returned here -- from the
+    weight-gradient kernel's own pass over dY when that kernel runs."""
+    if torch.is_grad_enabled() and (dbias_of is not None or dx_allreduce is not None) and (
+            weight.requires_grad or x.requires_grad or (dbias_of is not None and dbias_of.requires_grad)):
+        return _LinearWGradAccum.apply(x, weight, bias, dx_allreduce, dbias_of)
     if torch.is_grad_enabled() and weight.requires_grad and _fusable(weight):
-        return _LinearWGradAccum.apply(x, weight, bias, None)
+        return _LinearWGradAccum.apply(x, weight, bias, None, None)
     return F.linear(x, weight, bias)

@@ -40,8 +40,15 @@ for (n, k), splits in (((4800, 1600), (7, 6, 8)), ((1600, 1600), (5, 4, 6)), ((6
     C.wgrad_(gg, dy[:ts], x[:ts], True, 2)
     err = float((gg - ref).abs().max() / ref.abs().max())
     r = {"pipe": pipe, "shape": f"{n}x{k}", "rel_err": round(err, 6)}
+    bias = torch.zeros(n, device="cuda", dtype=torch.bfloat16)
     for sp in splits:
         ms = timeit(lambda: C.wgrad_(g, dy, x, True, sp))
         r[f"s{sp}"] = [round(ms, 3), round(2.0 * T * n * k / ms / 1e9, 1)]
+        if os.environ.get("WG_DBIAS") == "1":
+            ms = timeit(lambda: C.wgrad_(g, dy, x, True, sp, bias, True))
+            r[f"s{sp}_dbias"] = round(ms, 3)
+    if os.environ.get("WG_DBIAS") == "1":
+        r["col_sum_ms"] = round(timeit(lambda: C.col_sum(dy, bias)), 3)
+        r["library_ms"] = round(timeit(lambda: g.addmm_(dy.t(), x)), 3)
     print(json.dumps(r), flush=True)
     del dy, x, g, gg, ref
