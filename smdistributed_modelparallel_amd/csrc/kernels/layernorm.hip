@@ -547,10 +547,22 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
 
 // Number of partial rows the backward will produce for (rows, cols): callers size
 // dw_part/db_part as [parts, cols] fp32.
+// SMP_LN_BWD_PARTS caps the partial rows (= backward workgroups) of the register paths; more
+// workgroups keep more rows in flight per CU (the block-per-rows kernel streams its rows one
+// at a time behind a barrier) at the price of a larger dgamma/dbeta partial reduction.
+static inline int64_t ln_bwd_parts_cap() {
+  static const int64_t v = [] {
+    const char* e = getenv("SMP_LN_BWD_PARTS");
+    const long p = e != nullptr ? atol(e) : 1024;
+    return static_cast<int64_t>(p >= 64 && p <= 65536 ? p : 1024);
+  }();
+  return v;
+}
+
 static inline int ln_bwd_parts(int64_t rows, int64_t cols, bool reg_path) {
   if (!reg_path) return static_cast<int>(rows);
   int64_t blocks = (rows + kRowsPerBlock - 1) / kRowsPerBlock;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > ln_bwd_parts_cap()) blocks = ln_bwd_parts_cap();
   return static_cast<int>(blocks);
 }
 
