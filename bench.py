@@ -106,11 +106,14 @@ def balanced_layer_split(num_layers, pp, head_cost):
 
 
 def tunableop_file(args):
+    """Per-shape GEMM selections; the GEMM shapes depend on the micro-batch, sequence and TP
+    degree but not on the pipeline degree, so a PP run falls back to the PP=1 file."""
     if os.environ.get("SMP_TUNABLEOP_FILE"):
         return os.environ["SMP_TUNABLEOP_FILE"]
-    root = os.path.dirname(os.path.abspath(__file__))
-    return os.path.join(root, "configs", "tunableop",
-                        f"{args.model}_mbs{args.mbs}_s{args.seq}_pp{args.pp}_tp{args.tp}.csv")
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "configs", "tunableop")
+    path = os.path.join(root, f"{args.model}_mbs{args.mbs}_s{args.seq}_pp{args.pp}_tp{args.tp}.csv")
+    pp1 = os.path.join(root, f"{args.model}_mbs{args.mbs}_s{args.seq}_pp1_tp{args.tp}.csv")
+    return path if (os.path.isfile(path) or not os.path.isfile(pp1) or args.tunableop == "tune") else pp1
 
 
 def setup_tunableop(args):
@@ -170,6 +173,8 @@ def main():
         "shard_optimizer_state": args.shard_optimizer_state,
         "amd_offload_optimizer_state": args.offload_optimizer_state,
     }
+    if os.environ.get("SMP_BENCH_ACTIVE_MB"):  # in-flight microbatches (default pp + 2)
+        cfg["active_microbatches"] = int(os.environ["SMP_BENCH_ACTIVE_MB"])
     split = None
     if args.pp > 1:
         cfg["pipeline"] = "interleaved"
