@@ -1039,9 +1039,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         d_stage = qq < sq ? DL[qq] : 0.f;
       }
     }
-    // D = 64 without dropout: both 32-query sub-steps in one unrolled body (the second one's S / dP MFMAs
-    // overlap the first one's exp / dS work)
-#pragma unroll(D == 64 && !DROP ? 2 : 1)
+    // D = 64 (except dropout + key bias): both 32-query sub-steps in one unrolled body (the second one's S / dP
+    // MFMAs overlap the first one's exp / dS / dropout work; with a key bias the unrolled body spills)
+#pragma unroll(D == 64 && (!DROP || !BIAS) ? 2 : 1)
     for (int sub = 0; sub < 2; ++sub) {
       const int qs = qt + 32 * sub;  // first query of this sub-step
       if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
