@@ -550,14 +550,14 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
 // SMP_LN_BWD_PARTS caps the partial rows (= backward workgroups) of the register paths; more
 // workgroups keep more rows in flight per CU (the block-per-rows kernel streams its rows one
 // at a time behind a barrier) at the price of a larger dgamma/dbeta partial reduction.
-// Default 1792 = 7 workgroups (the kernel's occupancy at hidden 1600) on each of 256 CUs:
-// GPT-2 XL bench, same box, 2 alternating rounds: 1024 -> 802.8 / 808.0 ms/step, 1792 ->
-// 785.5 / 794.8, 3584 -> 800.3 / 791.1.
+// Default 1024: in the GPT-2 XL step's kernel trace the block-per-rows kernel takes 176 us at
+// 1024 partial rows and 191 us at 1792 (bench-level A/B of 1024 / 1792 / 3584 was within the
+// box's +-1 % noise).
 static inline int64_t ln_bwd_parts_cap() {
   static const int64_t v = [] {
     const char* e = getenv("SMP_LN_BWD_PARTS");
-    const long p = e != nullptr ? atol(e) : 1792;
-    return static_cast<int64_t>(p >= 64 && p <= 65536 ? p : 1792);
+    const long p = e != nullptr ? atol(e) : 1024;
+    return static_cast<int64_t>(p >= 64 && p <= 65536 ? p : 1024);
   }();
   return v;
 }
