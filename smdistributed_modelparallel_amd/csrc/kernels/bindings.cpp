@@ -379,7 +379,8 @@ void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t 
     if (!accumulate) c.zero_();
     if (dbias.defined() && !dbias_accumulate) dbias.zero_();
   } else {
-    auto ws = at::empty({splits * n * k + (dbias.defined() ? splits * n : 0)}, dy.options().dtype(at::kFloat));
+    const int64_t cs_rows = splits * ((k + 255) / 256);  // column-sum partials (wgrad.hip)
+    auto ws = at::empty({splits * n * k + (dbias.defined() ? cs_rows * n : 0)}, dy.options().dtype(at::kFloat));
     float* cs = dbias.defined() ? ws.data_ptr<float>() + splits * n * k : nullptr;
     check(smpk::wgrad(dt_code(dy), dy.data_ptr(), x.data_ptr(), dt_code(c), c.data_ptr(), ws.data_ptr<float>(), main_t,
                       static_cast<int>(n), static_cast<int>(k), dy.stride(0), x.stride(0), static_cast<int>(splits),

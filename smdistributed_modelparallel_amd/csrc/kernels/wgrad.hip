@@ -654,10 +654,12 @@ __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, i
   return __builtin_bit_cast(typename WMF16<T>::e8, v);
 }
 
-// cs != nullptr: the blocks of the first K tile also sum their staged A (= dY) rows per
-// column -- the bias gradient of the layer, sum over tokens of dY, in the same pass over dY
-// (fp32, fixed order: rows of a tile per thread, 16 row groups through LDS, splits in order)
-// -- into cs[split][N]; no separate column-sum pass over dY.
+// cs != nullptr: the workgroups also sum their staged A (= dY) rows per column -- the bias
+// gradient of the layer, sum over tokens of dY, in the same pass over dY.  The tiles_k
+// workgroups that share an A strip split that work: workgroup tk sums the 64-token tiles t with
+// t % tiles_k == tk (all-blocks-balanced; letting only tk = 0 do it made those workgroups the
+// kernel's tail), into cs[split * tiles_k + tk][N] (fp32, fixed order: rows of a tile per
+// thread, 16 row groups through LDS, partials in order) -- no separate column-sum pass.
 //
 // One SEGMENT = output tile (tn, tk) over `ntiles` 64-token tiles from token t_begin; the fp32
 // partial goes to out[(n - nb0) * ldo + (k - kb0)] and (colsum) the column sums to
@@ -670,7 +672,8 @@ template <typename T, int TKS, int NS, bool SPREAD>
 __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                uint16_t* smem, int N, int K, int64_t lda, int64_t ldb, int tn, int tk,
                                                int64_t t_begin, int64_t ntiles, float* __restrict__ out,
-                                               int64_t ldo, int nb0, int kb0, float* __restrict__ cso, bool colsum) {
+                                               int64_t ldo, int nb0, int kb0, float* __restrict__ cso, bool colsum,
+                                               int cs_mod, int cs_rem) {
   constexpr int W = 8, WCOLS = 64, NI = 8, NJ = 4;  // wave block 128 x 64 = 8 x 4 tiles of 16 x 16
   constexpr int L = 2 * (TKS / W / 2);
   const int n0 = tn * TM, k0 = tk * TN;
@@ -737,7 +740,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
     const uint16_t* sA = smem + cur_slot * STAGE;
     const uint16_t* sB = sA + TKS * RW;
     cur_slot = cur_slot + 1 == NS ? 0 : cur_slot + 1;
-    if (colsum) {
+    if (colsum && static_cast<int>(t % cs_mod) == cs_rem) {
       const int ch = threadIdx.x & 31;
       f32x4 c0 = *reinterpret_cast<const f32x4*>(csl), c1 = *reinterpret_cast<const f32x4*>(csl + 4);
 #pragma unroll
@@ -833,8 +836,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
   glds16_segment<T, TKS, NS, SPREAD>(A, B, smem, N, K, lda, ldb, tn, tk, t_begin, (t_end - t_begin) / TKS,
                                      ws + static_cast<int64_t>(split) * N * K, K, 0, 0,
-                                     cs != nullptr ? cs + static_cast<int64_t>(split) * N : nullptr,
-                                     cs != nullptr && tk == 0);
+                                     cs != nullptr ? cs + (static_cast<int64_t>(split) * tiles_k + tk) * N : nullptr,
+                                     cs != nullptr, tiles_k, tk);
 }
 
 template <typename T, int TKS, int NS, bool SPREAD>
@@ -943,7 +946,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   c[i + 3] = from_f32<TO>(s.w);
 }
 
-// bias (+)= sum over splits of cs[split][n]
+// bias (+)= sum over the partial rows of cs[part][n], in order
 template <typename TO>
 __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ cs, TO* __restrict__ bias, int n,
                                                             int splits, int accumulate) {
@@ -1022,11 +1025,14 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   else
     return -2;
   if (bias != nullptr) {
+    const int tiles_k = (k + TN - 1) / TN;
     const unsigned g = static_cast<unsigned>((n + 255) / 256);
     if (bias_dt == F32)
-      colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, splits, bias_accumulate);
+      colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, splits * tiles_k,
+                                                    bias_accumulate);
     else if (bias_dt == BF16)
-      colsum_reduce_kernel<bf16><<<g, 256, 0, s>>>(cs, static_cast<bf16*>(bias), n, splits, bias_accumulate);
+      colsum_reduce_kernel<bf16><<<g, 256, 0, s>>>(cs, static_cast<bf16*>(bias), n, splits * tiles_k,
+                                                   bias_accumulate);
     else
       return -2;
   }

@@ -1,0 +1,22 @@
+"""Steady-state per-kernel table of the last full step in a rocprofv3 kernel trace (step
+boundaries: the LM-head cross-entropy forward kernel); weight-gradient kernels split by grid."""
+import collections
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "xent_fwd" in r["Kernel_Name"]]
+last = rows[idx[-2]:idx[-1]]
+t0, t1 = int(last[0]["Start_Timestamp"]), int(rows[idx[-1]]["Start_Timestamp"])
+agg = collections.defaultdict(lambda: [0.0, 0])
+for r in last:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    k = r["Kernel_Name"]
+    if "wgrad_glds" in k or "Cijk" in k:
+        k = k[:48] + f" grid={int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}"
+    agg[k[:95]][0] += d
+    agg[k[:95]][1] += 1
+tot = sum(v[0] for v in agg.values())
+print(f"step {(t1 - t0) / 1e6:.1f} ms wall, {tot / 1e3:.1f} ms kernels")
+for k, v in sorted(agg.items(), key=lambda x: -x[1][0])[:40]:
+    print(f"{v[0] / 1e3:8.2f} ms {v[1]:4d} {v[0] / v[1]:8.1f} us  {k}")
