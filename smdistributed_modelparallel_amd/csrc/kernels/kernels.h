@@ -186,7 +186,7 @@ int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row
 // workspace ws [splits][n][k], then reduced into C.  n, k, lda, ldb multiples of 8.
 int wgrad_splits(int64_t tokens, int n, int k, int num_cus);
 // bias != nullptr (bf16 operands): bias (+)= sum over tokens of A, computed by the same kernel
-// from its staged A tiles (cs: [splits * ceil(k / 256)][n] fp32 workspace).
+// from its staged A tiles (cs: [splits * ceil(k / 256)][n] fp32 workspace, wgrad.hip).
 int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
           int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s, int bias_dt = 0, void* bias = nullptr,
           float* cs = nullptr, int bias_accumulate = 1);

@@ -646,6 +646,9 @@ struct WMF16<f16> {
   }
 };
 
+// the idle-wave column-sum mode applies: the last 256-wide K tile leaves a 64-wide wave column free
+__host__ __device__ __forceinline__ bool wgrad_cs_idle(int K) { return K % 256 != 0 && K % 256 <= 192; }
+
 template <typename T>
 __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, int off_lo, int off_hi) {
   s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_lo));
@@ -654,12 +657,18 @@ __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, i
   return __builtin_bit_cast(typename WMF16<T>::e8, v);
 }
 
-// cs != nullptr: the workgroups also sum their staged A (= dY) rows per column -- the bias
-// gradient of the layer, sum over tokens of dY, in the same pass over dY.  The tiles_k
-// workgroups that share an A strip split that work: workgroup tk sums the 64-token tiles t with
-// t % tiles_k == tk (all-blocks-balanced; letting only tk = 0 do it made those workgroups the
-// kernel's tail), into cs[split * tiles_k + tk][N] (fp32, fixed order: rows of a tile per
-// thread, 16 row groups through LDS, partials in order) -- no separate column-sum pass.
+// cs != nullptr: the kernel also sums the staged A (= dY) rows per column -- the bias gradient
+// of the layer, sum over tokens of dY -- in the same pass over dY, one of two ways:
+//  * idle-wave MFMA (K % 256 in [1, 192]; every GPT-2 XL layer with K = 1600): in the last K
+//    tile the wave columns past K have no output; the first of them multiplies its A fragments
+//    by an all-ones B fragment instead (acc[n][c] = sum over tokens of A[t][n]), on a SIMD that
+//    would otherwise idle -- 8 extra MFMAs per k-step in one workgroup per (split, tn).  Output
+//    cs[split][N].
+//  * otherwise, through LDS: the tiles_k workgroups that share an A strip split the work
+//    (workgroup tk sums the 64-token tiles t with t % tiles_k == tk) into
+//    cs[split * tiles_k + tk][N] (fp32, fixed order: rows of a tile per thread, 16 row groups
+//    through LDS, partials in order).  Measured in-step (profiles/r3/wgrad_variants.md) this
+//    costs the MFMA loop about what a separate column-sum pass would.
 //
 // One SEGMENT = output tile (tn, tk) over `ntiles` 64-token tiles from token t_begin; the fp32
 // partial goes to out[(n - nb0) * ldo + (k - kb0)] and (colsum) the column sums to
@@ -673,7 +682,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
                                                uint16_t* smem, int N, int K, int64_t lda, int64_t ldb, int tn, int tk,
                                                int64_t t_begin, int64_t ntiles, float* __restrict__ out,
                                                int64_t ldo, int nb0, int kb0, float* __restrict__ cso, bool colsum,
-                                               int cs_mod, int cs_rem) {
+                                               int cs_mod, int cs_rem, bool cs_idle) {
   constexpr int W = 8, WCOLS = 64, NI = 8, NJ = 4;  // wave block 128 x 64 = 8 x 4 tiles of 16 x 16
   constexpr int L = 2 * (TKS / W / 2);
   const int n0 = tn * TM, k0 = tk * TN;
@@ -706,7 +715,13 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
   const uint16_t* pa = A + t_begin * lda + n0;
   const uint16_t* pb = B + t_begin * ldb + k0;
   constexpr int STAGE = 2 * TKS * RW;
-  const bool active = n0 + wm * 128 < N && k0 + wn * WCOLS < K;  // wave-uniform
+  // idle-wave column sums: the first wave column past K (only exists in the last K tile) runs
+  // the normal MFMA loop with its first B fragment replaced by ones (no extra live registers)
+  const bool cs_wave = cs_idle && n0 + wm * 128 < N && wn == (K - k0 + WCOLS - 1) / WCOLS;
+  const bool active = (n0 + wm * 128 < N && k0 + wn * WCOLS < K) || cs_wave;  // wave-uniform
+  typename WMF16<T>::e8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = 1.0f;
   // column-sum accumulators in LDS after the operand ring (no registers held across the
   // loop: the kernel is at its VGPR limit): thread (row group t >> 5, chunk t & 31) owns
   // floats [(t >> 5) * 256 + (t & 31) * 8, +8)
@@ -764,6 +779,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
       typename WMF16<T>::e8 fa[NI / 2], fb[NJ];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) fb[j] = ld_tr16<T>(sB, bLo[j] + s * 32 * RW, bHi[j] + s * 32 * RW);
+      if (cs_wave) fb[0] = ones;
 #pragma unroll
       for (int i = 0; i < NI / 2; ++i) fa[i] = ld_tr16<T>(sA, aLo[i] + s * 32 * RW, aHi[i] + s * 32 * RW);
       if constexpr (SPREAD) {
@@ -807,6 +823,15 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
     }
   }
   const int col_l = lane & 15, rq = 4 * (lane >> 4);
+  if (cs_wave && col_l == 0) {  // every column of acc[i][0] holds the row sums
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wm * 128 + 16 * i + rq + r;
+        if (n < N) cso[n - nb0] = acc[i][0][r];
+      }
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int k = k0 + wn * WCOLS + 16 * j + col_l;
@@ -834,10 +859,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
   wg_map(tiles_n, tiles_k, group, split, tn, tk);
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  glds16_segment<T, TKS, NS, SPREAD>(A, B, smem, N, K, lda, ldb, tn, tk, t_begin, (t_end - t_begin) / TKS,
-                                     ws + static_cast<int64_t>(split) * N * K, K, 0, 0,
-                                     cs != nullptr ? cs + (static_cast<int64_t>(split) * tiles_k + tk) * N : nullptr,
-                                     cs != nullptr, tiles_k, tk);
+  const bool idle = wgrad_cs_idle(K);
+  glds16_segment<T, TKS, NS, SPREAD>(
+      A, B, smem, N, K, lda, ldb, tn, tk, t_begin, (t_end - t_begin) / TKS, ws + static_cast<int64_t>(split) * N * K,
+      K, 0, 0, cs == nullptr ? nullptr : cs + (static_cast<int64_t>(split) * (idle ? 1 : tiles_k) + (idle ? 0 : tk)) * N,
+      cs != nullptr && !idle, tiles_k, tk, cs != nullptr && idle);
 }
 
 template <typename T, int TKS, int NS, bool SPREAD>
@@ -1025,14 +1051,12 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   else
     return -2;
   if (bias != nullptr) {
-    const int tiles_k = (k + TN - 1) / TN;
+    const int parts = splits * (wgrad_cs_idle(k) ? 1 : (k + TN - 1) / TN);
     const unsigned g = static_cast<unsigned>((n + 255) / 256);
     if (bias_dt == F32)
-      colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, splits * tiles_k,
-                                                    bias_accumulate);
+      colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, parts, bias_accumulate);
     else if (bias_dt == BF16)
-      colsum_reduce_kernel<bf16><<<g, 256, 0, s>>>(cs, static_cast<bf16*>(bias), n, splits * tiles_k,
-                                                   bias_accumulate);
+      colsum_reduce_kernel<bf16><<<g, 256, 0, s>>>(cs, static_cast<bf16*>(bias), n, parts, bias_accumulate);
     else
       return -2;
   }

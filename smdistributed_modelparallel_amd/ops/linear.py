@@ -291,12 +291,20 @@ def _wgrad_kernel_wins(g, dy2, x2):
 # tokens (the bias gradient) from the dY tiles it stages anyway, so no separate column-sum
 # pass reads dY again -- and for the MLP's first projection, whose bias is added by the fused
 # bias-GeLU, that GeLU's backward becomes a pure elementwise pass (ops/gelu.py bias_grad).
-# Fused when dY is wide (>= SMP_WGRAD_DBIAS_MIN_N columns): the pass costs the kernel a roughly
-# fixed 0.01-0.07 ms while a column-sum kernel costs ~0.03 ms per 100 MB of dY (MI355X, T = 65536,
-# tools/wgrad_ab.py WG_DBIAS=1: QKV 4800 columns 0.126 ms -> +0.003-0.02, fc1 6400 0.163 ->
-# +0.065, but proj / fc2 1600 0.046 -> +0.05-0.075).
+# Two kernel modes (csrc/kernels/wgrad.hip): when the input width K leaves a wave column of the
+# last 256-wide output tile idle (K % 256 in [1, 192] -- every GPT-2 XL layer but fc2, K = 1600)
+# that wave sums dY on the matrix core (B fragment = ones): no cost on the busy SIMDs, so it is
+# always fused.  Otherwise the sums go through LDS inside the MFMA loop, which in-step costs
+# about what a separate column-sum pass does (GPT-2 XL b32 kernel traces: fc1 wgrad +150 us
+# vs. bias-GeLU backward -148 us), so that mode is only used for wide dY (>=
+# SMP_WGRAD_DBIAS_MIN_N columns).
 _WGRAD_DBIAS = os.environ.get("SMP_WGRAD_DBIAS", "1") != "0"
 _WGRAD_DBIAS_MIN_N = int(os.environ.get("SMP_WGRAD_DBIAS_MIN_N", "4096"))
+
+
+def _wgrad_dbias_free(k):
+    """The kernel's idle-wave column-sum mode applies to input width ``k``."""
+    return 0 < k % 256 <= 192
 
 
 def _wgrad_accumulate(g, dy2, x2, dbias=None):
@@ -306,7 +314,7 @@ def _wgrad_accumulate(g, dy2, x2, dbias=None):
     if _wgrad_native_ok(g, dy2, x2):
         s = _wgrad_kernel_splits(g, dy2, x2)
         fuse = (dbias is not None and _WGRAD_DBIAS and dy2.dtype == torch.bfloat16
-                and dy2.shape[1] >= _WGRAD_DBIAS_MIN_N)
+                and (_wgrad_dbias_free(x2.shape[1]) or dy2.shape[1] >= _WGRAD_DBIAS_MIN_N))
         if fuse and s == 0:
             # the fused bias pass makes the kernel the cheaper choice (it saves a full read of dY)
             s = _wgrad_dbias_splits(dy2, x2)

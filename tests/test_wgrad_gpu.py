@@ -134,7 +134,9 @@ def test_wgrad_static_pick_is_deterministic(monkeypatch):
     L._WGRAD_KERNEL_CHOICE.pop(key, None)
 
 
-@pytest.mark.parametrize("shape", [(4096, 1600, 1600), (8200, 4800, 1600), (5000, 392, 1048), (16384, 1600, 6400)])
+# K 1600 / 1048: idle-wave MFMA column sums; K 6400 / 1000: LDS column sums
+@pytest.mark.parametrize("shape", [(4096, 1600, 1600), (8200, 4800, 1600), (5000, 392, 1048), (16384, 1600, 6400),
+                                   (4160, 1040, 1000)])
 @pytest.mark.parametrize("bdtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("accumulate", [True, False])
 def test_wgrad_kernel_fused_bias_colsum(shape, bdtype, accumulate):
