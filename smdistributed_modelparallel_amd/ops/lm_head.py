@@ -13,8 +13,9 @@ W^T copies of ``ops/linear.py``), so
   and every gradient equal the unpadded model's exactly (the padding rows never
   receive gradient and never influence the logits that are read);
 * the input gradient ``dlogits @ E`` runs as ``F.linear(dlogits, E_pad^T)`` (TN, aligned);
-* the weight gradient is one aligned GEMM into a [Vp, h] temporary whose first V rows are
-  added to the (flat-buffer) gradient.
+* the weight gradient is one aligned GEMM -- the split-K MFMA kernel of ``ops/linear.py``
+  for bf16 -- into a [Vp, h] temporary whose first V rows are added to the (flat-buffer)
+  gradient.
 
 The user still receives [.., V] logits (a view) and can backpropagate through them.
 
@@ -33,6 +34,9 @@ import torch.nn.functional as F
 
 from ._ext import ext
 from .linear import _WT_EPOCH, _fusable
+
+# LM-head weight gradient on the MFMA weight-gradient kernel (SMP_LM_HEAD_WGRAD_KERNEL, default on)
+_WGRAD_KERNEL = os.environ.get("SMP_LM_HEAD_WGRAD_KERNEL", "1") != "0"
 
 _ALIGN = 64
 _ENABLED = os.environ.get("SMP_PADDED_LM_HEAD", "0") == "1"
@@ -99,7 +103,15 @@ class _PaddedLMHeadCE(torch.autograd.Function):
         dx = F.linear(dl, ctx.wpt).view(ctx.hshape) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            gp = torch.mm(dl.t(), h2)  # [vp, h], aligned
+            if _WGRAD_KERNEL and dl.is_cuda and dl.dtype == torch.bfloat16 and h2.dtype == torch.bfloat16 \
+                    and h2.shape[1] % 8 == 0 and h2.is_contiguous():
+                # the split-K MFMA weight-gradient kernel (csrc/kernels/wgrad.hip): 9.99 vs
+                # 10.9-11.1 ms for hipBLASLt at GPT-2 XL's [50304, 1600] x 65536 tokens
+                # (profiles/r2/wgrad_kernel.md)
+                gp = torch.empty(dl.shape[1], h2.shape[1], dtype=h2.dtype, device=h2.device)
+                ext().wgrad_(gp, dl, h2, False, 0)
+            else:
+                gp = torch.mm(dl.t(), h2)  # [vp, h], aligned
             w = ctx.weight
             if _fusable(w):
                 w.grad.add_(gp[:V])  # flat-buffer view: accumulate in place (hooks still fire)
