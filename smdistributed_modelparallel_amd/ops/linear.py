@@ -216,10 +216,16 @@ def _wgrad_native_ok(g, dy2, x2):
 # per-shape winners measured on MI355X at T = 65536 (profiles/r2/session4_wgrad_pick_ab.md),
 # keyed by (N, K); other shapes use the library GEMM.  No timing trials, no host sync in the
 # backward, and the same split-K accumulation order in every run and on every rank.
-_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 8}
+# (4800, 1600): s7 in the GPT-2 XL b32 step with the fused bias sums (1092-1099 us vs s5 1131,
+# s8 1167 + a larger partial reduce; profiles/r3/wgrad_variants.md).
+_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7}
 # kernel split count for (1600, 6400) when the fused bias pass makes the kernel the choice
 _WGRAD_STATIC_KERNEL = {(1600, 6400): 4}
+# "time" (default): table shapes at >= _WGRAD_STATIC_MIN_T tokens take the table (timing trials
+# there flip between near-equal split counts from run to run: s5 / s7 for QKV), other shapes
+# are timed; "timed": always time; "static": always the table (library off-table).
 _WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "time")
+_WGRAD_STATIC_MIN_T = 32768
 
 
 def _wgrad_static_pick(dy2, x2):
@@ -238,7 +244,9 @@ def _wgrad_kernel_splits(g, dy2, x2):
     hit = _WGRAD_KERNEL_CHOICE.get(key)
     if hit is not None:
         return hit
-    if _WGRAD_PICK == "static" or torch.are_deterministic_algorithms_enabled():
+    if _WGRAD_PICK == "static" or torch.are_deterministic_algorithms_enabled() or (
+            _WGRAD_PICK == "time" and dy2.shape[0] >= _WGRAD_STATIC_MIN_T
+            and (dy2.shape[1], x2.shape[1]) in _WGRAD_STATIC):
         _WGRAD_KERNEL_CHOICE[key] = _wgrad_static_pick(dy2, x2)
         return _WGRAD_KERNEL_CHOICE[key]
     from ._ext import ext
