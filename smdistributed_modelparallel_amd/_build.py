@@ -108,6 +108,10 @@ def build_runtime(jobs=8, verbose=False):
     return out
 
 
+# per-translation-unit extra flags (measured per kernel: profiles/r3/s3_rehearsal.md)
+_TU_FLAGS = {"attention_d64_dq.hip": ["-fno-slp-vectorize"]}
+
+
 def build_kernels(jobs=8, verbose=False):
     src_dir = os.path.join(CSRC, "kernels")
     hip_srcs = sorted(glob.glob(os.path.join(src_dir, "*.hip")))
@@ -131,7 +135,7 @@ def build_kernels(jobs=8, verbose=False):
         # kernel TUs do not include torch headers: fast to build, reusable outside torch
         obj = os.path.join(BUILD_DIR, "kernels", os.path.basename(s) + ".o")
         objs.append(obj)
-        flags = common + ["-I" + src_dir]
+        flags = common + ["-I" + src_dir] + _TU_FLAGS.get(os.path.basename(s), [])
         tasks.append((s, obj, [HIPCC] + flags + ["-c", s, "-o", obj], hdrs, flags))
     for s in cpp_srcs:
         obj = os.path.join(BUILD_DIR, "kernels", os.path.basename(s) + ".o")

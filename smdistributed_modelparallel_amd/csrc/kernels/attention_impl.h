@@ -1389,20 +1389,37 @@ inline bool attn_fused_delta() {
   return v;
 }
 
+// dQ launch as its own function template: a head dim can instantiate it in a separate
+// translation unit built with other flags (D = 64: attention_d64_dq.hip, no SLP vectorisation
+// -- packed fp32 VALU beside the MFMAs costs the dQ kernel 4.5 %, profiles/r3/s3_rehearsal.md)
+template <typename T, int D, bool C, bool DR, bool BI, bool FD>
+void launch_dq(const AttnBwdParams& p, unsigned g, hipStream_t s) {
+  attn_bwd_dq_kernel<T, D, C, DR, BI, FD><<<g, kThreads, 0, s>>>(p);
+}
+
+// X(T, C, DR, BI) for every dtype x variant of one head dim
+#define SMPK_ATTN_VARIANTS(X)                                                                 \
+  X(bf16, false, false, false) X(bf16, false, false, true) X(bf16, false, true, false)         \
+  X(bf16, false, true, true) X(bf16, true, false, false) X(bf16, true, false, true)            \
+  X(bf16, true, true, false) X(bf16, true, true, true) X(f16, false, false, false)             \
+  X(f16, false, false, true) X(f16, false, true, false) X(f16, false, true, true)              \
+  X(f16, true, false, false) X(f16, true, false, true) X(f16, true, true, false)               \
+  X(f16, true, true, true)
+
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_bwd_v(const AttnBwdParams& p, hipStream_t s) {
   const unsigned gk = static_cast<unsigned>(((p.f.sk + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
   const unsigned gq = static_cast<unsigned>(((p.f.sq + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
   if (attn_fused_delta()) {
     // dQ first: it writes delta for the dK/dV kernel (same stream)
-    attn_bwd_dq_kernel<T, D, C, DR, BI, true><<<gq, kThreads, 0, s>>>(p);
+    launch_dq<T, D, C, DR, BI, true>(p, gq, s);
     attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
     return static_cast<int>(hipGetLastError());
   }
   const int64_t rows = p.f.b * p.f.h * p.f.sq;
   attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
   attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
-  attn_bwd_dq_kernel<T, D, C, DR, BI><<<gq, kThreads, 0, s>>>(p);
+  launch_dq<T, D, C, DR, BI, false>(p, gq, s);
   return static_cast<int>(hipGetLastError());
 }
 
