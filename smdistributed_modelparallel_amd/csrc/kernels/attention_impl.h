@@ -128,6 +128,33 @@ __device__ __forceinline__ uint32_t drop_key(const AttnParams& p, int64_t bh) {
   return mix32(s0 ^ mix32(s1 + 0x9e3779b9u * static_cast<uint32_t>(bh + 1)) ^ mix32(o0 ^ mix32(o1 + 0x85ebca6bu)));
 }
 
+// Exact drop rate from 8-bit uniforms: each 32-query x 32-key block of one (b, h) draws its
+// threshold from {thr, thr + 1} with P(thr + 1) = frac / 65536 (one hash per block, keyed by
+// mix32(key + C) so it is independent of the element hashes), so every element's drop
+// probability is (thr + frac / 65536) / 256 = dropout_p to 2^-24; elements sharing a block
+// are correlated by < 2e-4.  Block indices are wave-uniform in all three kernels (the fwd / dQ
+// wave owns one query block, the dK/dV wave one key block), so this runs on the scalar unit.
+struct DropThr {
+  uint32_t xr, c;
+};
+__device__ __forceinline__ uint32_t drop_block_key(uint32_t dkey) { return mix32(dkey + 0x632be5abu); }
+__device__ __forceinline__ DropThr drop_block_thr(const AttnParams& p, uint32_t bkey, uint32_t qb32, uint32_t kb32) {
+  const uint32_t nkb = static_cast<uint32_t>((p.sk + 31) >> 5);
+  const bool hi = (mix32(bkey ^ (qb32 * nkb + kb32)) & 0xffffu) < p.drop_frac;
+  return DropThr{hi ? p.drop_xr1 : p.drop_xr, hi ? p.drop_c1 : p.drop_c};
+}
+
+// floor(a / b) for b > 0 and any sign of a
+__device__ __forceinline__ int fdiv(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int imin(int a, int b) { return a < b ? a : b; }
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+
+// Lazy online softmax: the exponent offset (running row max) only moves when a tile's max
+// exceeds it by more than kTau (log2 units), so stored probabilities stay <= 2^kTau (fp32
+// sums, bf16 / fp16 PV operands: no overflow) and the O / l rescale runs on a few tiles per
+// row instead of on almost every tile.
+constexpr float kTau = 8.f;
+
 template <typename T>
 __device__ __forceinline__ typename MF<T>::e8 ld8(const uint16_t* p) {
   return __builtin_bit_cast(typename MF<T>::e8, *reinterpret_cast<const s16x8*>(p));
@@ -225,12 +252,17 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // padded by the compiler and read stale values on some waves -- non-deterministic maxima).
 __device__ __forceinline__ float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
-// value of lane ^ 32 (the other half-wave) without an LDS round trip
-__device__ __forceinline__ float xor32(float x) {
+// max / sum of x over the lane pair (lane, lane ^ 32): the swap leaves the lower half's x in
+// one result and the upper half's in the other on every lane, so no lane select is needed
+__device__ __forceinline__ float pair_max32(float x) {
   const unsigned u = __builtin_bit_cast(unsigned, x);
   auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  const int lane = threadIdx.x & 63;
-  return __builtin_bit_cast(float, lane < 32 ? r[1] : r[0]);
+  return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+}
+__device__ __forceinline__ float pair_sum32(float x) {
+  const unsigned u = __builtin_bit_cast(unsigned, x);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
 }
 
 // Register-staged tile copy (issue global loads early, write LDS late: the HBM/L2 latency
@@ -446,6 +478,12 @@ struct QInLds {
 
 // DMA: K/V tiles arrive by LDS-DMA into two buffers (no staging registers, no ds_write, one
 // barrier per tile); D = 64 / 128 without bias.
+//
+// Tile phases: every wave takes part in every tile's barrier (the block shares its K/V
+// tiles) but runs the score work only on its visible tiles, and the per-element masks only on
+// its edge tiles: the interior tiles run a separately compiled mask-free body.  (With one loop
+// and a per-tile `if (!interior)`, hipcc if-converted the masks into ~100 VALU + ~100 SALU
+// selects executed on every tile -- profiles/r4/attention_isa.md.)
 template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
 __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
@@ -499,8 +537,10 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   const float sl2 = p.scale * kLog2e;
   const float inv_scale = 1.f / p.scale;
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
   const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
-  float m_i = -INFINITY, l_i = 0.f;
+  // m_i: exponent offset (lazy running max, log2 units), l_i: this lane's partial row sum
+  float m_i = -INFINITY, m_use = 0.f, l_i = 0.f;
   f32x16 o[D / 32];
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) o[i] = f32x16{0};
@@ -514,6 +554,20 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
     const int lo = qb * BM + diag - win + 1;
     kv_begin = lo > 0 ? (lo / BN) * BN : 0;
   }
+  const int nt = kv_begin < kv_end ? (kv_end - kv_begin + BN - 1) / BN : 0;
+  // this wave's visible tiles [tv0, tv1) and mask-free tiles [ti0, ti1) (tile t = keys
+  // kv_begin + t BN ...)
+  const int wave_last_q = q0 + 31;
+  int tv0 = 0, tv1 = nt;
+  if (CAUSAL) tv1 = imin(nt, imax(0, fdiv(wave_last_q + diag - kv_begin, BN) + 1));
+  if (win > 0) tv0 = imax(0, -fdiv(kv_begin - (q0 + diag - win + 2 - BN), BN));
+  tv0 = imin(tv0, tv1);
+  int ti0 = tv0, ti1 = wave_last_q < sq ? fdiv(sk - BN - kv_begin, BN) + 1 : 0;
+  if (CAUSAL) ti1 = imin(ti1, fdiv(q0 + diag - BN + 1 - kv_begin, BN) + 1);
+  if (win > 0) ti0 = imax(ti0, -fdiv(kv_begin - (wave_last_q + diag - win + 1), BN));
+  ti0 = imin(ti0, tv1);
+  ti1 = imax(ti0, imin(ti1, tv1));
+
   Stage<D, BN> stK(p.k_ss), stV(p.v_ss);  // (unused by DMA)
   const RowOff<D> ro(r, hh);
   const TrOff<D> tro(lane);
@@ -523,7 +577,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
     // the loop and drains vmcnt(0) -- the in-flight K/V DMA included -- before the first MFMA
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
   }
-  if (kv_begin < kv_end) {
+  if (nt > 0) {
     if constexpr (DMA) {
       dma_tile<D, BN>(sKV, K, p.k_ss, kv_begin, sk, wave, lane);
       dma_tile<D, BN>(sKV + BN * DS, V, p.v_ss, kv_begin, sk, wave, lane);
@@ -533,16 +587,17 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
     }
   }
-  const int wave_last_q = q0 + 31;
   int buf = 0;
-  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
-    bool tile_bias = false;
+  bool tile_bias = false;
+  // tile t's barrier: its K/V landed in LDS for every wave; the next tile's copy is issued
+  auto sync = [&](int t) {
+    const int kv0 = kv_begin + t * BN;
     if constexpr (DMA) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of the tile landed
       __syncthreads();  // ... everyone's; and every wave is done with the other buffer
       sK = sKV + buf * 2 * BN * DS;
       sV = sK + BN * DS;
-      if (kv0 + BN < kv_end) {
+      if (t + 1 < nt) {
         uint16_t* nb = sKV + (buf ^ 1) * 2 * BN * DS;
         dma_tile<D, BN>(nb, K, p.k_ss, kv0 + BN, sk, wave, lane);
         dma_tile<D, BN>(nb + BN * DS, V, p.v_ss, kv0 + BN, sk, wave, lane);
@@ -558,28 +613,29 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       }
       __syncthreads();
       tile_bias = BIAS && sFlag != 0;
-      if (kv0 + BN < kv_end) {
+      if (t + 1 < nt) {
         stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
         stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
         if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
       }
     }
-    if (CAUSAL && kv0 > wave_last_q + diag) continue;
-    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
-    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
-                          (win <= 0 || kv0 > wave_last_q + diag - win);
+  };
+  // one visible tile: S^T = K Q^T, (edge masks), online softmax, (dropout), O^T += V^T P^T
+  auto body = [&](int t, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int kv0 = kv_begin + t * BN;
     f32x16 s0 = f32x16{0}, s1 = f32x16{0};
 #pragma unroll
-    for (int t = 0; t < D / 16; ++t) {
-      const typename MF<T>::e8 qt = QLDS ? ld8<T>(sQ + ro.o[t] + wave * 32 * DS) : qf[t];
-      s0 = MF<T>::mma(ld8<T>(sK + ro.o[t]), qt, s0);
-      s1 = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * DS), qt, s1);
+    for (int k = 0; k < D / 16; ++k) {
+      const typename MF<T>::e8 qt = QLDS ? ld8<T>(sQ + ro.o[k] + wave * 32 * DS) : qf[k];
+      s0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qt, s0);
+      s1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * DS), qt, s1);
     }
-    if (tile_bias) {
+    if (BIAS && tile_bias) {
       add_from_keys(s0, sB, hh);
       add_from_keys(s1, sB + 32, hh);
     }
-    if (!interior) {
+    if constexpr (MASK) {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int k0 = kv0 + acc_row(reg, hh);
@@ -595,11 +651,20 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       mx0 = max3(mx0, s0[reg], s1[reg]);
       mx1 = max3(mx1, s0[reg + 1], s1[reg + 1]);
     }
-    float mx = max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2;
-    mx = fmaxf(mx, xor32(mx));
-    const float m_new = fmaxf(m_i, mx);
-    const float m_use = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
-    const float alpha = fast_exp2(m_i - m_use);
+    const float mx = pair_max32(max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2);
+    if (__any(mx > m_i + kTau)) {  // first visible tile, or a max jump: move the offset
+      // (a side-effecting statement: keeps hipcc from if-converting the rescale into 16
+      // packed multiplies on every tile)
+      asm volatile("" ::: "memory");
+      const float m_new = fmaxf(m_i, mx);
+      const float mu = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
+      const float alpha = fast_exp2(m_i - mu);
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
+      l_i *= alpha;
+      m_i = m_new;
+      m_use = mu;
+    }
     float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -610,19 +675,14 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       rs0 += e0;
       rs1 += e1;
     }
-    float rs = rs0 + rs1;
-    rs += xor32(rs);
-    l_i = l_i * alpha + rs;
-    if (__any(m_new != m_i)) {  // rescale only when a row max moved
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
-    }
-    m_i = m_new;
+    l_i += rs0 + rs1;
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
+      const DropThr d0 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5));
+      const DropThr d1 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + 1);
       uint32_t f0[4], f1[4];
-      drop_words(f0, dkey, qbase, kv0, hh, p.drop_xr, p.drop_c);
-      drop_words(f1, dkey, qbase, kv0 + 32, hh, p.drop_xr, p.drop_c);
+      drop_words(f0, dkey, qbase, kv0, hh, d0.xr, d0.c);
+      drop_words(f1, dkey, qbase, kv0 + 32, hh, d1.xr, d1.c);
       pf[0] = drop_packed(pf[0], f0[0], f0[1]);
       pf[1] = drop_packed(pf[1], f0[2], f0[3]);
       pf[2] = drop_packed(pf[2], f1[0], f1[1]);
@@ -634,256 +694,24 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       for (int s = 0; s < 4; ++s)
         o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
     }
-  }
-  if (qrow >= sq) return;
-  const float inv = l_i > 0.f ? (DROP ? p.drop_rs : 1.f) / l_i : 0.f;
-  uint16_t* O = static_cast<uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh + static_cast<int64_t>(qrow) * p.o_ss;
-  store_rows<T, D>(O, o, inv, hh);
-  if (hh == 0) p.lse[bh * p.sq + qrow] = (l_i > 0.f) ? (m_i + log2f(l_i)) / kLog2e : -INFINITY;
-}
-
-// s_waitcnt vmcnt(N) from inline asm (the LDS-DMA it waits for is issued from inline asm too)
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N == 0 || N == 2 || N == 4 || N == 8, "vm_wait: add the count");
-  if constexpr (N == 0)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2)
-    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-}
-
-// ===================================================== software-pipelined forward
-// D = 64 / 128 without key bias or window (the others take attn_fwd_kernel).  Same block
-// and wave layout and LDS image, but each wave runs a two-stage pipeline over its key tiles
-// instead of QK^T -> softmax -> PV in turn (profiles/r3: the in-turn loop keeps a wave
-// waiting on its own MFMA results or LDS reads ~65 % of its cycles, MFMA busy 25 %):
-//   phase A of iteration t: the QK^T MFMAs of tile t + 1, each followed in program order by
-//     a slice of tile t's exp / row-sum VALU work (sched_group_barrier), so the VALU issues
-//     in the MFMA shadow;
-//   phase B: tile t's P is packed (and dropped) fragment by fragment, each fragment's PV
-//     MFMAs issued as soon as it is ready; then tile t + 1's row max, which needs its S.
-// K and V have separate two-slot rings filled by LDS-DMA: iteration t reads K(t + 1) and
-// V(t), and issues K(t + 2) and V(t + 1) right after its barrier.  The row sum stays a
-// per-lane partial (both half-waves see the same row maxima) and is combined once at the end.
-template <typename T, int D, bool CAUSAL, bool DROP>
-__global__ void __launch_bounds__(kThreads, 2) attn_fwd_pipe_kernel(AttnParams p) {
-  static_assert(D == 64 || D == 128, "pipelined forward: D 64 / 128");
-  constexpr int BM = 128, BN = 64, TS = BN * D;
-  constexpr int L = (BN * D * 2 / 1024) / (kThreads / 64);  // DMA instructions per wave per tile
-  __shared__ __attribute__((aligned(16))) uint16_t sKV[4 * TS];  // K slots 0, 1, V slots 0, 1
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  const int nqb = static_cast<int>((p.sq + BM - 1) / BM);
-  int tile;
-  int64_t bh;
-  xcd_map(nqb, p.b * p.h, tile, bh);
-  const int64_t b = bh / p.h, h = bh % p.h;
-  const int qb = CAUSAL ? (nqb - 1 - tile) : tile;
-  const int q0 = qb * BM + wave * 32;
-  const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
-  const int diag = sk - sq;
-  const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
-  const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
-  const uint16_t* V = static_cast<const uint16_t*>(p.v) + b * p.v_sb + h * p.v_sh;
-
-  typename MF<T>::e8 qf[D / 16];
-  const int qrow = q0 + r;
-#pragma unroll
-  for (int t = 0; t < D / 16; ++t) {
-    if (qrow < sq) {
-      qf[t] = ld8<T>(Q + static_cast<int64_t>(qrow) * p.q_ss + 16 * t + 8 * hh);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[t][j] = MF<T>::cvt(0.f);
-    }
-  }
-  const float sl2 = p.scale * kLog2e;
-  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
-  // block range (every wave takes part in every tile's barrier) and this wave's own range
-  int kv_end = sk;
-  if (CAUSAL) {
-    const int lim = (qb + 1) * BM + diag;
-    kv_end = lim < sk ? lim : sk;
-  }
-  const int nt = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
-  int wend = kv_end;
-  if (CAUSAL) wend = q0 + 32 + diag < kv_end ? q0 + 32 + diag : kv_end;
-  const int ntw = wend > 0 ? (wend + BN - 1) / BN : 0;
-  const int wave_last_q = q0 + 31;
-  auto interior = [&](int kv0) {
-    return kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag);
   };
-  auto dmaK = [&](int t) { dma_tile<D, BN>(sKV + (t & 1) * TS, K, p.k_ss, t * BN, sk, wave, lane); };
-  auto dmaV = [&](int t) { dma_tile<D, BN>(sKV + (2 + (t & 1)) * TS, V, p.v_ss, t * BN, sk, wave, lane); };
-  const RowOff<D> ro(r, hh);
-  const TrOff<D> tro(lane);
-
-  // S of tile t (raw scores, masked), the exponent offset of tile t, the O / l rescale
-  float m_i = -INFINITY, l_i = 0.f, m_use = 0.f, alpha = 1.f;
-  bool rescale = false;
-  f32x16 o[D / 32];
-#pragma unroll
-  for (int i = 0; i < D / 32; ++i) o[i] = f32x16{0};
-  f32x16 sc0 = f32x16{0}, sc1 = f32x16{0};
-
-  // masks a raw score tile (keys kv0 .. kv0 + 63) and folds its row max into the running max
-  auto stats = [&](f32x16& s0, f32x16& s1, int kv0) {
-    if (!interior(kv0)) {
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int k0 = kv0 + acc_row(reg, hh);
-        const int k1 = k0 + 32;
-        if (k0 >= sk || (CAUSAL && k0 > qrow + diag)) s0[reg] = -INFINITY;
-        if (k1 >= sk || (CAUSAL && k1 > qrow + diag)) s1[reg] = -INFINITY;
-      }
-    }
-    float mx0 = max3(s0[0], s1[0], s0[1]), mx1 = max3(s1[1], s0[2], s1[2]);
-#pragma unroll
-    for (int reg = 3; reg < 15; reg += 2) {
-      mx0 = max3(mx0, s0[reg], s1[reg]);
-      mx1 = max3(mx1, s0[reg + 1], s1[reg + 1]);
-    }
-    float mx = max3(mx0, mx1, max3(s0[15], s1[15], s0[15])) * sl2;
-    mx = fmaxf(mx, xor32(mx));
-    const float m_new = fmaxf(m_i, mx);
-    const float mu = m_new == -INFINITY ? 0.f : m_new;  // fully masked so far: keep p = 0
-    alpha = fast_exp2(m_i - mu);
-    rescale = __any(m_new != m_i);
-    m_i = m_new;
-    m_use = mu;
-  };
-  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0): Q loads retired (see attn_fwd_kernel)
-  if (nt > 0) {
-    dmaK(0);
-    dmaV(0);
-    if (nt > 1) {
-      dmaK(1);
-      vm_wait<2 * L>();  // K(0) landed (V(0), K(1) may fly)
-    } else {
-      vm_wait<L>();
-    }
-    __syncthreads();
-    if (ntw > 0) {
-#pragma unroll
-      for (int k = 0; k < D / 16; ++k) {
-        sc0 = MF<T>::mma(ld8<T>(sKV + ro.o[k]), qf[k], sc0);
-        sc1 = MF<T>::mma(ld8<T>(sKV + ro.o[k] + 32 * D), qf[k], sc1);
-      }
-      stats(sc0, sc1, 0);
-    }
-  }
-  // tile t's barrier: this wave's K(t + 1) and V(t) landed, everyone's too, and the slots
-  // of K(t) and V(t - 1) are free for K(t + 2) and V(t + 1)
-  auto sync_issue = [&](int t) {
-    vm_wait<0>();
-    __syncthreads();
-    if (t + 2 < nt) dmaK(t + 2);
-    if (t + 1 < nt) dmaV(t + 1);
-  };
-  auto rescale_o = [&]() {
-    if (rescale) {
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i) o[i] *= alpha;
-    }
-    l_i *= alpha;
-  };
-  // tile t: exponentials of c0 / c1 (its masked scores); with MORE, tile t + 1's scores into
-  // n0 / n1 (the caller alternates the two register sets, no copies)
-  auto step = [&](int t, auto more_c, f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1) {
-    const int kv0 = t * BN;
-    const uint16_t* sV = sKV + (2 + (t & 1)) * TS;
-    constexpr bool MORE = decltype(more_c)::value;
-    // phase A: QK^T of tile t + 1 beside tile t's exponentials
-    if constexpr (MORE) {
-      const uint16_t* sK = sKV + ((t + 1) & 1) * TS;
-      n0 = f32x16{0};
-      n1 = f32x16{0};
-#pragma unroll
-      for (int k = 0; k < D / 16; ++k) {
-        n0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qf[k], n0);
-        n1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * D), qf[k], n1);
-      }
-    }
-    float rs0 = 0.f, rs1 = 0.f;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const float e0 = fast_exp2(fmaf(c0[reg], sl2, -m_use));
-      const float e1 = fast_exp2(fmaf(c1[reg], sl2, -m_use));
-      c0[reg] = e0;
-      c1[reg] = e1;
-      rs0 += e0;
-      rs1 += e1;
-    }
-    if constexpr (MORE) {
-      // 2 K reads, then per MFMA a slice of the 96 exp / fma / add instructions
-#pragma unroll
-      for (int k = 0; k < D / 16; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 96 / (D / 8), 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 96 / (D / 8), 0);
-      }
-    }
-    l_i += rs0 + rs1;
-    // phase B: tile t's P fragment by fragment, each fragment's PV MFMAs once it is ready
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      typename MF<T>::e8 pf = pack8<T>(s < 2 ? c0 : c1, s & 1);
-      if (DROP) {
-        uint32_t f[2];
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const int gg = 2 * (s & 1) + g;
-          const uint32_t kq =
-              static_cast<uint32_t>((kv0 + 32 * (s >> 1)) >> 2) + static_cast<uint32_t>(2 * gg + hh);
-          f[g] = keep_flags(mix32(dkey ^ (qbase + kq)), p.drop_xr, p.drop_c);
-        }
-        pf = drop_packed(pf, f[0], f[1]);
-      }
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i)
-        o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * D, tro.hi[i] + 16 * s * D), pf, o[i]);
-    }
-    if constexpr (MORE) {
-      stats(n0, n1, kv0 + BN);
-    }
-  };
-  // the loop keeps its state in fixed registers (unrolled by two over the two score sets);
-  // the wave's last tiles (no next S) and the barriers of the block's remaining tiles
-  // (causal: later waves see more keys) come after it
-  f32x16 sn0 = f32x16{0}, sn1 = f32x16{0};
   int t = 0;
-  for (; t + 2 < ntw; t += 2) {
-    sync_issue(t);
-    rescale_o();
-    step(t, std::true_type{}, sc0, sc1, sn0, sn1);
-    sync_issue(t + 1);
-    rescale_o();
-    step(t + 1, std::true_type{}, sn0, sn1, sc0, sc1);
+  for (; t < tv0; ++t) sync(t);
+  for (; t < ti0; ++t) {
+    sync(t);
+    body(t, std::true_type{});
   }
-  if (t + 1 < ntw) {
-    sync_issue(t);
-    rescale_o();
-    step(t, std::true_type{}, sc0, sc1, sn0, sn1);
-    sync_issue(t + 1);
-    rescale_o();
-    step(t + 1, std::false_type{}, sn0, sn1, sc0, sc1);
-    t += 2;
-  } else if (t < ntw) {
-    sync_issue(t);
-    rescale_o();
-    step(t, std::false_type{}, sc0, sc1, sn0, sn1);
-    ++t;
+  for (; t < ti1; ++t) {
+    sync(t);
+    body(t, std::false_type{});
   }
-  for (; t < nt; ++t) sync_issue(t);
+  for (; t < tv1; ++t) {
+    sync(t);
+    body(t, std::true_type{});
+  }
+  for (; t < nt; ++t) sync(t);
+  const float lt = pair_sum32(l_i);  // the two half-waves' partial row sums
   if (qrow >= sq) return;
-  const float lt = l_i + xor32(l_i);
   const float inv = lt > 0.f ? (DROP ? p.drop_rs : 1.f) / lt : 0.f;
   uint16_t* O = static_cast<uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh + static_cast<int64_t>(qrow) * p.o_ss;
   store_rows<T, D>(O, o, inv, hh);
@@ -982,6 +810,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   float kbias = 0.f;
   bool blk_bias = false;  // this wave's 32 keys carry a bias
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
   // dropout: the 4 lanes of a key quad (keys 4j..4j+3 = lanes with the same lane >> 2) share
   // one hash per query; quad position qp hashes query registers 4 qp .. 4 qp + 3 (inputs
   // q * nquads + key quad, the query part of each a per-lane constant plus qs * nquads)
@@ -1016,7 +845,20 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     }
   }
   const int klast = k0w + 31;
-  for (int qt = q_start; qt < q_end; qt += BQ) {
+  // 64-query tiles: this wave's visible tiles [tv0, tv1) and mask-free tiles [ti0, ti1) (tile
+  // t = queries q_start + 64 t ...; edge tiles run the masked sub-step body)
+  const int nt = q_start < q_end ? (q_end - q_start + BQ - 1) / BQ : 0;
+  int tv0 = 0, tv1 = nt;
+  if (CAUSAL) tv0 = imax(0, -fdiv(q_start - (k0w - diag - (BQ - 1)), BQ));
+  if (win > 0) tv1 = imin(nt, imax(0, fdiv(klast - diag + win - 1 - q_start, BQ) + 1));
+  tv0 = imin(tv0, tv1);
+  int ti0 = tv0, ti1 = klast < sk ? fdiv(sq - BQ - q_start, BQ) + 1 : 0;
+  if (CAUSAL) ti0 = imax(ti0, -fdiv(q_start - (klast - diag), BQ));
+  if (win > 0) ti1 = imin(ti1, fdiv(k0w - BQ - diag + win - q_start, BQ) + 1);
+  ti0 = imin(ti0, tv1);
+  ti1 = imax(ti0, imin(ti1, tv1));
+  auto sync = [&](int t) {
+    const int qt = q_start + t * BQ;
     __syncthreads();
     stQ.store(sQ);
     stO.store(sdO);
@@ -1030,7 +872,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       kbias = kbias_raw * (1.f / p.scale);
       blk_bias = __any(kbias != 0.f);
     }
-    if (qt + BQ < q_end) {
+    if (t + 1 < nt) {
       stQ.load(Q + static_cast<int64_t>(qt + BQ) * p.q_ss, sq - qt - BQ);
       stO.load(dO + static_cast<int64_t>(qt + BQ) * P.do_ss, sq - qt - BQ);
       if (threadIdx.x < BQ) {
@@ -1039,108 +881,126 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         d_stage = qq < sq ? DL[qq] : 0.f;
       }
     }
-    // D = 64 (except dropout + key bias): both 32-query sub-steps in one unrolled body (the second one's S / dP
-    // MFMAs overlap the first one's exp / dS / dropout work; with a key bias the unrolled body spills)
-#pragma unroll(D == 64 && (!DROP || !BIAS) ? 2 : 1)
-    for (int sub = 0; sub < 2; ++sub) {
-      const int qs = qt + 32 * sub;  // first query of this sub-step
-      if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
-      if (win > 0 && qs + diag - win + 1 > klast) continue;  // all keys left the window
-      const bool interior = qs + 31 < sq && klast < sk && (!CAUSAL || klast <= qs + diag) &&
-                            (win <= 0 || k0w > qs + 31 + diag - win);
-      // S' = Q K^T - lse/scale [+ bias/scale], dP' = dO V^T - delta (query rows in regs, key on lane)
-      f32x16 s, dp, ndl;
+  };
+  // one 32-query sub-step (queries qs .. qs + 31 = LDS rows 32 sub ..)
+  auto step = [&](int qs, int sub, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    // S' = Q K^T - lse/scale [+ bias/scale], dP' = dO V^T - delta (query rows in regs, key on lane)
+    f32x16 s, dp, ndl;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 lv = *reinterpret_cast<const float4*>(&sL[32 * sub + 8 * g + 4 * hh]);
-        const float4 dv4 = *reinterpret_cast<const float4*>(&sDl[32 * sub + 8 * g + 4 * hh]);
-        s[4 * g + 0] = lv.x; s[4 * g + 1] = lv.y; s[4 * g + 2] = lv.z; s[4 * g + 3] = lv.w;
-        if (DROP) {
-          ndl[4 * g + 0] = dv4.x; ndl[4 * g + 1] = dv4.y; ndl[4 * g + 2] = dv4.z; ndl[4 * g + 3] = dv4.w;
-          dp[4 * g + 0] = dp[4 * g + 1] = dp[4 * g + 2] = dp[4 * g + 3] = 0.f;
-        } else {
-          dp[4 * g + 0] = dv4.x; dp[4 * g + 1] = dv4.y; dp[4 * g + 2] = dv4.z; dp[4 * g + 3] = dv4.w;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < D / 16; ++t) {
-        s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * DS), kf[t], s);
-        dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * DS), vf[t], dp);
-      }
-      // dO^T / Q^T fragments of the dV / dK MFMAs now (independent of the exp / dS work below),
-      // so those MFMAs issue back to back instead of each waiting on its own LDS reads
-      constexpr bool TPRE = D <= 128 && !BIAS && !DROP && CAUSAL;  // (others: spills)
-      typename MF<T>::e8 tdo[TPRE ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
-      if constexpr (TPRE) {
-        const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
-#pragma unroll
-        for (int i = 0; i < DO / 32; ++i) {
-          tdo[i][0] = ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0);
-          tdo[i][1] = ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1);
-          tq[i][0] = ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0);
-          tq[i][1] = ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (blk_bias) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) s[j] += kbias;
-      }
-      // Dropout decisions of the lane's key for the 16 query registers: this lane hashes
-      // query registers 4 qp + i (keep flags of the quad's 4 keys in one word each), and the
-      // word of register j comes from quad lane j / 4 by a DPP broadcast -- 4 hashes per lane
-      // instead of 16, the same random stream as the forward and the dQ kernel.
-      uint32_t kf4[4] = {0u, 0u, 0u, 0u};
+    for (int g = 0; g < 4; ++g) {
+      const float4 lv = *reinterpret_cast<const float4*>(&sL[32 * sub + 8 * g + 4 * hh]);
+      const float4 dv4 = *reinterpret_cast<const float4*>(&sDl[32 * sub + 8 * g + 4 * hh]);
+      s[4 * g + 0] = lv.x; s[4 * g + 1] = lv.y; s[4 * g + 2] = lv.z; s[4 * g + 3] = lv.w;
       if (DROP) {
-        const uint32_t qsn = static_cast<uint32_t>(qs) * nquads;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) kf4[i] = keep_flags(mix32(dkey ^ (qsn + hin[i])), p.drop_xr, p.drop_c);
-      }
-      auto finish = [&](float pv, int reg) {
-        if (DROP) {
-          // register reg = 4 j + i: word i of quad lane j (quad_perm [j, j, j, j])
-          const uint32_t w = quad_bcast(kf4[reg & 3], reg >> 2);
-          const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
-          s[reg] = pv * z;                             // (P o Z) for dV
-          dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
-        } else {
-          s[reg] = pv;
-          dp[reg] *= pv;
-        }
-      };
-      if (interior) {
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) finish(fast_exp2(s[reg] * sl2), reg);
+        ndl[4 * g + 0] = dv4.x; ndl[4 * g + 1] = dv4.y; ndl[4 * g + 2] = dv4.z; ndl[4 * g + 3] = dv4.w;
+        dp[4 * g + 0] = dp[4 * g + 1] = dp[4 * g + 2] = dp[4 * g + 3] = 0.f;
       } else {
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int qq = qs + acc_row(reg, hh);
-          float pv = fast_exp2(s[reg] * sl2);
-          if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win))
-            pv = 0.f;
-          finish(pv, reg);
-        }
-      }
-      // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
-      typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
-      typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
-#pragma unroll
-      for (int i = 0; i < DO / 32; ++i) {
-        const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
-        if constexpr (TPRE) {
-          dv[i] = MF<T>::mma(tdo[i][0], pf0, dv[i]);
-          dv[i] = MF<T>::mma(tdo[i][1], pf1, dv[i]);
-          dk[i] = MF<T>::mma(tq[i][0], sf0, dk[i]);
-          dk[i] = MF<T>::mma(tq[i][1], sf1, dk[i]);
-        } else {
-          dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
-          dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
-          dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
-          dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
-        }
+        dp[4 * g + 0] = dv4.x; dp[4 * g + 1] = dv4.y; dp[4 * g + 2] = dv4.z; dp[4 * g + 3] = dv4.w;
       }
     }
+#pragma unroll
+    for (int t = 0; t < D / 16; ++t) {
+      s = MF<T>::mma(ld8<T>(sQ + ro.o[t] + 32 * sub * DS), kf[t], s);
+      dp = MF<T>::mma(ld8<T>(sdO + ro.o[t] + 32 * sub * DS), vf[t], dp);
+    }
+    // dO^T / Q^T fragments of the dV / dK MFMAs now (independent of the exp / dS work below),
+    // so those MFMAs issue back to back instead of each waiting on its own LDS reads
+    constexpr bool TPRE = D <= 128 && !BIAS && !DROP && CAUSAL;  // (others: spills)
+    typename MF<T>::e8 tdo[TPRE ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
+    if constexpr (TPRE) {
+      const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
+#pragma unroll
+      for (int i = 0; i < DO / 32; ++i) {
+        tdo[i][0] = ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0);
+        tdo[i][1] = ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1);
+        tq[i][0] = ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0);
+        tq[i][1] = ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (blk_bias) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s[j] += kbias;
+    }
+    // Dropout decisions of the lane's key for the 16 query registers: this lane hashes
+    // query registers 4 qp + i (keep flags of the quad's 4 keys in one word each), and the
+    // word of register j comes from quad lane j / 4 by a DPP broadcast -- 4 hashes per lane
+    // instead of 16, the same random stream as the forward and the dQ kernel.
+    uint32_t kf4[4] = {0u, 0u, 0u, 0u};
+    if (DROP) {
+      const DropThr dt = drop_block_thr(p, bkey, static_cast<uint32_t>(qs >> 5), static_cast<uint32_t>(k0w >> 5));
+      const uint32_t qsn = static_cast<uint32_t>(qs) * nquads;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) kf4[i] = keep_flags(mix32(dkey ^ (qsn + hin[i])), dt.xr, dt.c);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      float pv = fast_exp2(s[reg] * sl2);
+      if constexpr (MASK) {
+        const int qq = qs + acc_row(reg, hh);
+        if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win)) pv = 0.f;
+      }
+      if (DROP) {
+        // register reg = 4 j + i: word i of quad lane j (quad_perm [j, j, j, j])
+        const uint32_t w = quad_bcast(kf4[reg & 3], reg >> 2);
+        const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
+        s[reg] = pv * z;                             // (P o Z) for dV
+        dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
+      } else {
+        s[reg] = pv;
+        dp[reg] *= pv;
+      }
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
+    typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
+    typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
+#pragma unroll
+    for (int i = 0; i < DO / 32; ++i) {
+      const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
+      if constexpr (TPRE) {
+        dv[i] = MF<T>::mma(tdo[i][0], pf0, dv[i]);
+        dv[i] = MF<T>::mma(tdo[i][1], pf1, dv[i]);
+        dk[i] = MF<T>::mma(tq[i][0], sf0, dk[i]);
+        dk[i] = MF<T>::mma(tq[i][1], sf1, dk[i]);
+      } else {
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
+        dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
+      }
+    }
+  };
+  // edge tile: each visible sub-step with the per-element masks
+  auto edge = [&](int t) {
+    const int qt = q_start + t * BQ;
+#pragma unroll 1
+    for (int sub = 0; sub < 2; ++sub) {
+      const int qs = qt + 32 * sub;
+      if (CAUSAL && qs + 31 + diag < k0w) continue;          // no query sees these keys
+      if (win > 0 && qs + diag - win + 1 > klast) continue;  // all keys left the window
+      step(qs, sub, std::true_type{});
+    }
+  };
+  int t = 0;
+  for (; t < tv0; ++t) sync(t);
+  for (; t < ti0; ++t) {
+    sync(t);
+    edge(t);
   }
+  for (; t < ti1; ++t) {
+    sync(t);
+    // D = 64 (except dropout + key bias): both sub-steps in one unrolled body (the second one's
+    // S / dP MFMAs overlap the first one's exp / dS / dropout work; with a key bias the
+    // unrolled body spills)
+#pragma unroll(D == 64 && (!DROP || !BIAS) ? 2 : 1)
+    for (int sub = 0; sub < 2; ++sub) step(q_start + t * BQ + 32 * sub, sub, std::false_type{});
+  }
+  for (; t < tv1; ++t) {
+    sync(t);
+    edge(t);
+  }
+  for (; t < nt; ++t) sync(t);
   if (krow >= sk) return;
   uint16_t* dK = static_cast<uint16_t*>(P.dk) + b * P.dk_sb + h * P.dk_sh + static_cast<int64_t>(krow) * P.dk_ss;
   uint16_t* dV = static_cast<uint16_t*>(P.dv) + b * P.dv_sb + h * P.dv_sh + static_cast<int64_t>(krow) * P.dv_ss;
@@ -1150,7 +1010,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 
 // ========================================================================= dQ
 // Block = 4 waves x 32 queries (query on the lane: S^T = K Q^T, dP^T = V dO^T); K/V tiles
-// of 64 keys; dQ^T += K^T dS^T with K^T from transposed LDS reads.
+// of 64 keys; dQ^T += K^T dS^T with K^T from transposed LDS reads.  Tile phases as in the
+// forward (edge masks only on edge tiles).  Accumulators start at zero (an inline-constant
+// operand of the first MFMA) and the row constants enter the exponent's fma / the dS
+// subtraction instead of 64 register moves per tile.
 // FD (fused delta): the block computes delta = rowsum(dO o O) of its own query rows from the dO
 // fragments it holds anyway plus one read of the O rows, and publishes it for the dK/dV kernel
 // launched after it -- no separate delta pass over O and dO.
@@ -1202,7 +1065,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   if (lse == -INFINITY) lse = 0.f;  // fully masked row: every p is masked to 0 below
   const float sl2 = p.scale * kLog2e;
   const float inv_scale = 1.f / p.scale;
-  const float s_init = -lse * kLog2e / sl2;
+  const float lse2 = lse * kLog2e;  // p = exp2(S sl2 - lse2)
   float dl;
   if constexpr (FD) {
     // lane (r, hh) holds elements [16 t + 8 hh, +8) of dO row qrow: the matching O elements,
@@ -1217,12 +1080,13 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
         for (int j = 0; j < 8; ++j) part = fmaf(static_cast<float>(df[t][j]), static_cast<float>(o8[j]), part);
       }
     }
-    dl = part + xor32(part);
+    dl = pair_sum32(part);
     if (col0 == 0 && hh == 0 && qrow < sq) P.delta[bh * p.sq + qrow] = dl;
   } else {
     dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
   }
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
+  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
   const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
   const float rsd = p.drop_rs;
   f32x16 dq[DO / 32];
@@ -1237,17 +1101,31 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     const int lo = qb * BM + diag - win + 1;
     kv_begin = lo > 0 ? (lo / BN) * BN : 0;
   }
+  const int nt = kv_begin < kv_end ? (kv_end - kv_begin + BN - 1) / BN : 0;
+  // visible tiles [tv0, tv1), mask-free tiles [ti0, ti1) of this wave (as in the forward)
+  const int wave_last_q = q0 + 31;
+  int tv0 = 0, tv1 = nt;
+  if (CAUSAL) tv1 = imin(nt, imax(0, fdiv(wave_last_q + diag - kv_begin, BN) + 1));
+  if (win > 0) tv0 = imax(0, -fdiv(kv_begin - (q0 + diag - win + 2 - BN), BN));
+  tv0 = imin(tv0, tv1);
+  int ti0 = tv0, ti1 = wave_last_q < sq ? fdiv(sk - BN - kv_begin, BN) + 1 : 0;
+  if (CAUSAL) ti1 = imin(ti1, fdiv(q0 + diag - BN + 1 - kv_begin, BN) + 1);
+  if (win > 0) ti0 = imax(ti0, -fdiv(kv_begin - (wave_last_q + diag - win + 1), BN));
+  ti0 = imin(ti0, tv1);
+  ti1 = imax(ti0, imin(ti1, tv1));
+
   Stage<D, BN> stK(p.k_ss), stV(p.v_ss);
   const RowOff<D> ro(r, hh);
   const TrOff<D, DO / 32> tro(lane, col0);
   float bstage = 0.f;
-  if (kv_begin < kv_end) {
+  if (nt > 0) {
     stK.load(K + static_cast<int64_t>(kv_begin) * p.k_ss, sk - kv_begin);
     stV.load(V + static_cast<int64_t>(kv_begin) * p.v_ss, sk - kv_begin);
     if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
   }
-  const int wave_last_q = q0 + 31;
-  for (int kv0 = kv_begin; kv0 < kv_end; kv0 += BN) {
+  bool tile_bias = false;
+  auto sync = [&](int t) {
+    const int kv0 = kv_begin + t * BN;
     __syncthreads();
     stK.store(sK);
     stV.store(sV);
@@ -1256,16 +1134,16 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       publish_bias_flag(bstage, &sFlag);
     }
     __syncthreads();
-    const bool tile_bias = BIAS && sFlag != 0;
-    if (kv0 + BN < kv_end) {
+    tile_bias = BIAS && sFlag != 0;
+    if (t + 1 < nt) {
       stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
       stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
       if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
     }
-    if (CAUSAL && kv0 > wave_last_q + diag) continue;
-    if (win > 0 && kv0 + BN - 1 < q0 + diag - win + 1) continue;
-    const bool interior = kv0 + BN <= sk && wave_last_q < sq && (!CAUSAL || kv0 + BN - 1 <= q0 + diag) &&
-                          (win <= 0 || kv0 > wave_last_q + diag - win);
+  };
+  auto body = [&](int t, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int kv0 = kv_begin + t * BN;
     // D <= 128: both 32-key halves' dS^T, then the dQ MFMAs (the two halves' MFMA chains
     // overlap each other's softmax VALU work).  D = 256: half by half, so only one half's
     // S / dP accumulators are live next to the 16 Q / dO fragments.
@@ -1282,36 +1160,27 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     f32x16 s[2], dp[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      s[u] = f32x16{0};
+      dp[u] = f32x16{0};
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        s[u][j] = s_init;
-        dp[u][j] = DROP ? 0.f : -dl;
+      for (int k = 0; k < D / 16; ++k) {
+        s[u] = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * u * DS), qf[k], s[u]);
+        dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[k] + 32 * u * DS), df[k], dp[u]);
       }
-#pragma unroll
-      for (int t = 0; t < D / 16; ++t) {
-        s[u] = MF<T>::mma(ld8<T>(sK + ro.o[t] + 32 * u * DS), qf[t], s[u]);
-        dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[t] + 32 * u * DS), df[t], dp[u]);
-      }
-      if (tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
+      if (BIAS && tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       if (DROP) {
         // dp <- keep o dP (raw), then dS = P o (dP o keep / (1 - p) - delta)
-        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, p.drop_xr, p.drop_c);
+        const DropThr dt = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + u);
+        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, dt.xr, dt.c);
       }
-      if (interior) {
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const float pv = fast_exp2(s[u][reg] * sl2);
-          dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : dp[u][reg] * pv;  // dS^T
-        }
-      } else {
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          float pv = fast_exp2(s[u][reg] * sl2);
+      for (int reg = 0; reg < 16; ++reg) {
+        float pv = fast_exp2(fmaf(s[u][reg], sl2, -lse2));
+        if constexpr (MASK) {
           const int kk = kv0 + 32 * u + acc_row(reg, hh);
-          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win))
-            pv = 0.f;
-          dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : dp[u][reg] * pv;
+          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win)) pv = 0.f;
         }
+        dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : pv * (dp[u][reg] - dl);  // dS^T
       }
       if (SEQ) {
         const typename MF<T>::e8 sf0 = pack8<T>(dp[u], 0), sf1 = pack8<T>(dp[u], 1);
@@ -1333,7 +1202,22 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
                              sf[st], dq[i]);
       }
     }
+  };
+  int t = 0;
+  for (; t < tv0; ++t) sync(t);
+  for (; t < ti0; ++t) {
+    sync(t);
+    body(t, std::true_type{});
   }
+  for (; t < ti1; ++t) {
+    sync(t);
+    body(t, std::false_type{});
+  }
+  for (; t < tv1; ++t) {
+    sync(t);
+    body(t, std::true_type{});
+  }
+  for (; t < nt; ++t) sync(t);
   if (qrow >= sq) return;
   uint16_t* dQ = static_cast<uint16_t*>(P.dq) + b * P.dq_sb + h * P.dq_sh + static_cast<int64_t>(qrow) * P.dq_ss;
   store_rows<T, D, DO / 32>(dQ + col0, dq, p.scale, hh);
@@ -1350,27 +1234,10 @@ inline bool attn_dma_enabled() {
   return v;
 }
 
-// SMP_ATTN_FWD_PIPE=1 selects the software-pipelined forward for D = 64 / 128.  Opt-in: it
-// passes the same tests but measured SLOWER at GPT-2 XL b32 (tools/gpu_attn_pipe_ab.sh, same
-// box, interleaved: 831-845 vs 758-768 us, dropout 0.1 873-876 vs 807-811 us) -- its two
-// live score sets need 205 VGPRs (2 waves / SIMD) where the in-turn loop runs at 124 (4
-// waves / SIMD), and at 3 waves it spills; cross-wave overlap at 4 waves beats in-wave overlap.
-inline bool attn_fwd_pipe_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("SMP_ATTN_FWD_PIPE");
-    return e != nullptr && e[0] == '1';
-  }();
-  return v;
-}
-
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_fwd_v(const AttnParams& p, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
   if constexpr ((D == 64 || D == 128) && !BI) {
-    if (p.window <= 0 && attn_fwd_pipe_enabled()) {
-      attn_fwd_pipe_kernel<T, D, C, DR><<<grid, kThreads, 0, s>>>(p);
-      return static_cast<int>(hipGetLastError());
-    }
     if (attn_dma_enabled()) {
       attn_fwd_kernel<T, D, C, DR, BI, true><<<grid, kThreads, 0, s>>>(p);
       return static_cast<int>(hipGetLastError());
@@ -1426,7 +1293,7 @@ int launch_bwd_v(const AttnBwdParams& p, hipStream_t s) {
 // runtime flags -> template variant
 template <typename T, int D>
 int launch_fwd(const AttnParams& p, hipStream_t s) {
-  const bool dr = p.drop_thr > 0, bi = p.kbias != nullptr;
+  const bool dr = p.drop_on != 0, bi = p.kbias != nullptr;
   const int v = (p.causal ? 4 : 0) | (dr ? 2 : 0) | (bi ? 1 : 0);
   switch (v) {
     case 0: return launch_fwd_v<T, D, false, false, false>(p, s);
@@ -1442,7 +1309,7 @@ int launch_fwd(const AttnParams& p, hipStream_t s) {
 
 template <typename T, int D>
 int launch_bwd(const AttnBwdParams& p, hipStream_t s) {
-  const bool dr = p.f.drop_thr > 0, bi = p.f.kbias != nullptr;
+  const bool dr = p.f.drop_on != 0, bi = p.f.kbias != nullptr;
   const int v = (p.f.causal ? 4 : 0) | (dr ? 2 : 0) | (bi ? 1 : 0);
   switch (v) {
     case 0: return launch_bwd_v<T, D, false, false, false>(p, s);

@@ -604,16 +604,26 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
   }
   TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention: dropout_p must be in [0, 1)");
   if (dropout_p > 0.0) {
-    // dropped iff the element's 8-bit uniform < thr: keep probability 1 - thr / 256 (the
-    // probability is quantised to 1/256, as with 8-bit dropout masks; kept values are scaled
-    // by the exact inverse keep probability, so the expectation is unchanged)
-    uint32_t thr = static_cast<uint32_t>(dropout_p * 256.0 + 0.5);
-    thr = thr < 1 ? 1 : (thr > 255 ? 255 : thr);
-    p.drop_thr = thr;
-    p.drop_rs = static_cast<float>(256.0 / (256.0 - thr));
-    const uint32_t t7 = thr <= 128 ? thr : 256 - thr;  // 1..128
-    p.drop_xr = thr <= 128 ? 0u : 0xffffffffu;
-    p.drop_c = (128u - t7) * 0x01010101u;
+    // dropped iff the element's 8-bit uniform < thr, where each 32x32 block draws thr from
+    // {lo, lo + 1} with P(lo + 1) = frac / 65536 (attention_impl.h drop_block_thr): the drop
+    // probability of every element is (lo + frac / 65536) / 256 = dropout_p to 2^-24, and kept
+    // values are scaled by 1 / (1 - dropout_p)
+    const double x = dropout_p * 256.0;
+    uint32_t lo = static_cast<uint32_t>(x);
+    uint32_t frac = static_cast<uint32_t>((x - lo) * 65536.0 + 0.5);
+    if (frac >= 65536u) lo += 1, frac = 0;
+    const double p_eff = (lo + frac / 65536.0) / 256.0;
+    auto consts = [](uint32_t thr, uint32_t& xr, uint32_t& c) {
+      const uint32_t t7 = thr <= 128 ? thr : 256 - thr;  // 0..128
+      xr = thr <= 128 ? 0u : 0xffffffffu;
+      c = (128u - t7) * 0x01010101u;
+    };
+    p.drop_on = 1;
+    p.drop_thr = lo;
+    p.drop_frac = frac;
+    p.drop_rs = static_cast<float>(1.0 / (1.0 - p_eff));
+    consts(lo, p.drop_xr, p.drop_c);
+    consts(lo + 1, p.drop_xr1, p.drop_c1);
     p.seed = static_cast<uint64_t>(seed);
     p.offset = static_cast<uint64_t>(offset);
   }

@@ -146,10 +146,14 @@ struct AttnParams {
   int window;  // >0: local attention window (GPT-Neo)
   const float* kbias;  // optional additive key bias [b, sk] (padding mask); nullptr = none
   int64_t kbias_sb;    // its batch stride (0: one row shared by the batch)
-  uint32_t drop_thr;   // dropout: element dropped iff its 8-bit uniform < drop_thr (0 = off)
-  float drop_rs;       // 1 / keep probability = 256 / (256 - drop_thr)
-  uint32_t drop_xr;    // per-byte keep test constants (attention_impl.h keep_flags):
-  uint32_t drop_c;     //   xr = 0 / ~0 for drop_thr <= / > 128, c = per-byte add constant
+  uint32_t drop_on;    // dropout enabled
+  uint32_t drop_thr;   // element dropped iff its 8-bit uniform < thr, thr = drop_thr or drop_thr + 1
+  uint32_t drop_frac;  //   per 32x32 block, thr = drop_thr + 1 with probability drop_frac / 65536
+  float drop_rs;       // 1 / keep probability = 1 / (1 - dropout_p)
+  uint32_t drop_xr;    // per-byte keep test constants for thr = drop_thr (attention_impl.h keep_flags):
+  uint32_t drop_c;     //   xr = 0 / ~0 for thr <= / > 128, c = per-byte add constant
+  uint32_t drop_xr1;   // ... and for thr = drop_thr + 1
+  uint32_t drop_c1;
   uint64_t seed, offset;
 };
 struct AttnBwdParams {

@@ -86,32 +86,45 @@ def _mix32(x):
 
 
 def flash_dropout_threshold(dropout_p):
-    """8-bit drop threshold of the flash kernels: an element is dropped iff its 8-bit uniform is
-    below it, so the realised drop probability is ``thr / 256`` (``dropout_p`` quantised to
-    1/256) and kept values are scaled by ``256 / (256 - thr)``."""
-    return max(1, min(255, int(dropout_p * 256.0 + 0.5)))
+    """(lo, frac) of the flash kernels' dropout: an element is dropped iff its 8-bit uniform is
+    below a threshold that each 32-query x 32-key block draws from {lo, lo + 1}, lo + 1 with
+    probability frac / 65536 -- so every element is dropped with probability
+    (lo + frac / 65536) / 256 = dropout_p to 2^-24 (``bindings.cpp`` attn_params)."""
+    x = dropout_p * 256.0
+    lo = int(x)
+    frac = int((x - lo) * 65536.0 + 0.5)
+    if frac >= 65536:
+        lo, frac = lo + 1, 0
+    return lo, frac
 
 
 def flash_dropout_keep_prob(dropout_p):
-    return 1.0 - flash_dropout_threshold(dropout_p) / 256.0
+    lo, frac = flash_dropout_threshold(dropout_p)
+    return 1.0 - (lo + frac / 65536.0) / 256.0
 
 
 def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu"):
     """Host reconstruction of the kernel's dropout decisions ([b, h, sq, sk] bool, True =
-    kept): test oracle for the in-kernel hash (csrc/kernels/attention_impl.h drop_key/mix32):
-    byte ``k % 4`` of ``mix32(key ^ (q * ceil(sk / 4) + k // 4))`` is key k's 8-bit uniform."""
+    kept): test oracle for the in-kernel hash (csrc/kernels/attention_impl.h drop_key / mix32 /
+    drop_block_thr): byte ``k % 4`` of ``mix32(key ^ (q * ceil(sk / 4) + k // 4))`` is key k's
+    8-bit uniform; the threshold of block (q // 32, k // 32) is lo + 1 iff the low 16 bits of
+    ``mix32(mix32(key + 0x632be5ab) ^ (q // 32 * ceil(sk / 32) + k // 32))`` are below frac."""
     M = 0xFFFFFFFF
-    thr = flash_dropout_threshold(dropout_p)
+    lo, frac = flash_dropout_threshold(dropout_p)
     s0, s1, o0, o1 = seed & M, (seed >> 32) & M, offset & M, (offset >> 32) & M
     bh = torch.arange(b * h, dtype=torch.int64, device=device)
     key = _mix32(torch.full_like(bh, s0) ^ _mix32((s1 + 0x9E3779B9 * (bh + 1)) & M) ^
                  _mix32(torch.full_like(bh, o0) ^ _mix32(torch.full_like(bh, (o1 + 0x85EBCA6B) & M))))
+    bkey = _mix32((key + 0x632BE5AB) & M)
     nquads = (sk + 3) // 4
+    nkb = (sk + 31) // 32
     q = torch.arange(sq, dtype=torch.int64, device=device).view(1, -1, 1)
     k = torch.arange(sk, dtype=torch.int64, device=device).view(1, 1, -1)
     x = (key.view(-1, 1, 1) ^ ((q * nquads + (k >> 2)) & M)) & M
     hsh = _mix32(x)
     u = (hsh >> (8 * (k & 3))) & 0xFF
+    g = _mix32((bkey.view(-1, 1, 1) ^ (((q >> 5) * nkb + (k >> 5)) & M)) & M)
+    thr = lo + ((g & 0xFFFF) < frac).to(torch.int64)
     return (u >= thr).view(b, h, sq, sk)
 
 

@@ -92,8 +92,43 @@ class RemoteOutput(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *grads):
         if any(g is not None for g in grads):
-            ctx.engine._send_bwd(ctx.holder, ("out", ctx.key), ctx.mb, list(grads))
+            ctx.engine._entry_grads(ctx.mb, ("rout", ctx.key), ctx.holder, ("out", ctx.key), grads)
         return (None, None, None, None) + (None,) * len(grads)
+
+
+class _Entry:
+    """Tensors whose gradients go to another stage (a request's input leaves, a fast-mode
+    consumer leaf, or a RemoteOutput).  Their gradients are sent ONCE per microbatch: after
+    every backward wave that can reach them has run (``pending`` = number of registered
+    wave sources whose graph reaches them).  So every saved segment on the peer receives
+    exactly one backward message per microbatch -- which is what the GradTracker counts
+    (reference: the aggregated backward of `worker.py:382-418` + `ops.py:131`).  Sending per
+    wave instead broke DDP finality when an output fanned out to several consumers: the
+    peer's segment then ran once per consumer, beyond its registered count, and a bucket was
+    scaled and reduced before the last accumulation.  An entry that ends up with no gradient
+    still sends one (empty) message: the peer's segment then knows no wave will come, and the
+    entries IT holds are released in turn (an unused path must not block the used ones)."""
+
+    __slots__ = ("targets", "pending", "grads", "dst", "key", "leaf", "flushed")
+
+    def __init__(self, targets, dst, key, leaf):
+        self.targets = targets
+        self.pending = 0
+        self.grads = None
+        self.dst, self.key, self.leaf = dst, key, leaf
+        self.flushed = False
+
+    def take(self):
+        """The accumulated gradients (None: nothing arrived), reset."""
+        if self.leaf:
+            gs = [t.grad for t in self.targets]
+            if all(g is None for g in gs):
+                return None
+            for t in self.targets:
+                t.grad = None
+            return gs
+        gs, self.grads = self.grads, None
+        return gs
 
 
 class _Token:
@@ -119,7 +154,7 @@ class _Worker:
 
 
 class _MbState:
-    __slots__ = ("sent", "leaves", "out", "out_direct", "dleaves")
+    __slots__ = ("sent", "leaves", "out", "out_direct", "dleaves", "entries", "reach")
 
     def __init__(self):
         self.sent = {}
@@ -127,6 +162,8 @@ class _MbState:
         self.out = {}
         self.out_direct = {}  # (rid, mi) -> output tensor sent child-to-child   [fast mode producer]
         self.dleaves = {}  # rid -> [(leaf, producer rank, ("dout", prid, mi))]  [fast mode consumer]
+        self.entries = {}  # entry id -> _Entry (gradients owed to another stage)
+        self.reach = {}  # wave source key -> [entries its backward reaches]
 
 
 class _FastMode:
@@ -693,7 +730,7 @@ class PipelineEngine:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
                 self._mb(mb).sent[rid] = sent
-                st.model._track_segment(sent)
+                self._register_source(mb, ("in", rid), sent)
         mi_base = (target, count) if fm is not None else None
         st.transport.send(owner, ("fwd", rid, mb, target, stubbed, self.core.rank(), rid, grad_enabled, mi_base),
                           tensors)
@@ -720,6 +757,7 @@ class PipelineEngine:
                 t.requires_grad_(True)
                 ins.append(t)
             wrapped = RemoteOutput.apply(self, holder, out_key, mb, *ins)
+            self._mb(mb).entries[("rout", out_key)] = _Entry(list(wrapped), holder, ("out", out_key), False)
             for i, w in zip(rg_idx, wrapped):
                 tensors[i] = w
             if self._cur_worker is not None:
@@ -750,6 +788,7 @@ class PipelineEngine:
                     leaf_idx.append(s.index)
             if leaves:
                 self._mb(mb).leaves[rid] = (leaves, src)
+                self._mb(mb).entries[("in", rid)] = _Entry(leaves, src, ("in", rid), True)
         args, kwargs = unstubify(stubbed, tensors, dvals)
         mm = st.module_manager
         if target[0] == "module":
@@ -783,6 +822,7 @@ class PipelineEngine:
                 leaf = t.detach()
                 leaf.requires_grad_(True)
                 self._mb(mb).dleaves.setdefault(rid, []).append((leaf, prod, ("dout", prid, d.mi)))
+                self._mb(mb).entries[("dout", rid, d.mi)] = _Entry([leaf], prod, ("dout", prid, d.mi), True)
                 t = leaf
             out[d.mi] = t
         return out
@@ -845,7 +885,7 @@ class PipelineEngine:
             sent = [t for t in tensors if t.requires_grad]
             if sent:
                 self._mb(mb).sent[rid2] = sent
-                self.state.model._track_segment(sent)
+                self._register_source(mb, ("in", rid2), sent)
         self.state.transport.send(
             nxt,
             ("fwd", rid2, mb, ("chain", mm.get_module_name(seq), j), stubbed, reply_to, result_id, grad_enabled,
@@ -863,7 +903,7 @@ class PipelineEngine:
             rg = [t for t in tensors if t.requires_grad]
             if rg:
                 self._mb(mb).out[rid] = rg
-                self.state.model._track_segment(rg)
+                self._register_source(mb, ("out", rid), rg)
         msg = ("res", result_id, mb, stubbed, self.core.rank(), rid, grad_enabled)
         if reply_to == self.core.rank():
             # local delivery (a chain came back to its requester's stage): queue it for the
@@ -882,11 +922,16 @@ class PipelineEngine:
         direct_to = {}
         if using:
             parent_pp = self.core.ranker.get_pp_rank(reply_to)
+            my_pp = self.core.pp_rank()
             for t in iter_tensors(out):
                 mi = (mi_base, order[id(t)])
                 cons = fm.map.get(mi)
                 if cons and all(c[0] != parent_pp for c in cons):
-                    direct_to[id(t)] = (mi, sorted({c[0] for c in cons}))
+                    # every consuming call on another stage detaches its own leaf and sends
+                    # one "dout" backward; a call on this stage uses the tensor itself, so
+                    # its gradient flows inside that call's own segment
+                    n_remote = sum(1 for c in cons if c[0] != my_pp)
+                    direct_to[id(t)] = (mi, sorted({c[0] for c in cons}), n_remote)
 
         def direct(t):
             d = direct_to.get(id(t))
@@ -903,10 +948,13 @@ class PipelineEngine:
                 d = direct_to.get(id(t))
                 if d is None:
                     continue
-                mi, pps = d
+                mi, pps, n_remote = d
                 if grad_enabled and t.requires_grad:
                     s.out_direct[(rid, mi)] = [t]
-                    self.state.model._track_segment([t])
+                    # one expected backward segment per remote consuming call (ADVICE r3:
+                    # one per tensor let PP+DDP launch a bucket after the first of two douts,
+                    # and a same-stage consumer's count was never reached)
+                    self._register_source(mb, ("dout", rid, mi), [t], n_remote)
                 for pp in pps:
                     dst = self._pp_peer(pp)
                     if dst == me:
@@ -922,11 +970,11 @@ class PipelineEngine:
         mb = self.state.microbatch
         # register the loss segment before the scheduler marks this microbatch's forward
         # done: the last microbatch's mark must never see an incomplete expected count
-        self.state.model._track_segment([t for t in tensors if t.requires_grad])
+        self._register_source(mb, ("root",), [t for t in tensors if t.requires_grad])
         self._suspend(("bwd_start", mb))
         tid = self._new_token(None, None, mb)
         self._root_tokens[mb] = tid
-        self._run_backward(tid, mb, tensors, grads)
+        self._run_backward(tid, mb, tensors, grads, ("root",))
         self._maybe_finish(tid)
         if not self.tokens.get(tid, _DONE).done:
             self._suspend(("bwd_done", mb))
@@ -943,7 +991,62 @@ class PipelineEngine:
         self.tokens[parent].pending += 1
         self._send(holder, ("bwd", key, mb, grads, parent))
 
-    def _run_backward(self, tid, mb, tensors, grads):
+    def _register_source(self, mb, skey, tensors, waves=1):
+        """A saved segment whose backward will run `waves` times this microbatch (one per
+        gradient message, or the loss): the GradTracker expects the accumulations it
+        reaches, and every gradient entry it reaches waits for those waves."""
+        if not tensors:
+            return
+        for _ in range(waves):
+            self.state.model._track_segment(tensors)
+        s = self._mb(mb)
+        targets, owners = [], []
+        for e in s.entries.values():
+            for t in e.targets:
+                targets.append(t)
+                owners.append(e)
+        reached = []
+        if targets:
+            from ..ops._ext import ext
+
+            hit = ext().graph_reaches(list(tensors), targets, [])
+            seen = set()
+            for h, e in zip(hit, owners):
+                if h and id(e) not in seen:
+                    seen.add(id(e))
+                    reached.append(e)
+                    e.pending += waves
+        s.reach[skey] = reached
+
+    def _entry_grads(self, mb, eid, dst, key, grads):
+        """RemoteOutput backward: accumulate the output gradients of one wave (sent at the
+        end of the last wave that reaches the entry)."""
+        e = self._mb(mb).entries.get(eid)
+        if e is None:  # not tracked (should not happen): send right away
+            self._send_bwd(dst, key, mb, list(grads))
+            return
+        if e.grads is None:
+            e.grads = list(grads)
+        else:
+            e.grads = [a if b is None else (b if a is None else a + b) for a, b in zip(e.grads, grads)]
+
+    def _wave_done(self, mb, skey):
+        s = self.mbstate.get(mb)
+        if s is None:
+            return
+        for e in s.reach.get(skey, ()):
+            e.pending -= 1
+        for e in s.entries.values():
+            if e.pending > 0:
+                continue
+            gs = e.take()
+            if not e.flushed:
+                e.flushed = True
+                self._send_bwd(e.dst, e.key, mb, gs if gs is not None else [None] * len(e.targets))
+            elif gs is not None:  # a wave the counts did not foresee: never drop gradients
+                self._send_bwd(e.dst, e.key, mb, gs)
+
+    def _run_backward(self, tid, mb, tensors, grads, skey):
         pairs = [(t, g) for t, g in zip(tensors, grads) if g is not None and t.requires_grad]
         prev = self._cur_token
         self._cur_token = tid
@@ -951,25 +1054,9 @@ class PipelineEngine:
             if pairs:
                 with torch.enable_grad():
                     torch.autograd.backward([t for t, _ in pairs], [g for _, g in pairs], retain_graph=True)
-            self._flush_leaf_grads(mb)
+            self._wave_done(mb, skey)
         finally:
             self._cur_token = prev
-
-    def _flush_leaf_grads(self, mb):
-        s = self.mbstate.get(mb)
-        if s is None:
-            return
-        for rid, (leaves, provider) in s.leaves.items():
-            gs = [l.grad for l in leaves]
-            if any(g is not None for g in gs):
-                for l in leaves:
-                    l.grad = None
-                self._send_bwd(provider, ("in", rid), mb, gs)
-        for lst in s.dleaves.values():
-            for leaf, producer, key in lst:
-                if leaf.grad is not None:
-                    g, leaf.grad = leaf.grad, None
-                    self._send_bwd(producer, key, mb, [g])
 
     def _process_bwd(self, src, key, mb, grads, remote_token):
         s = self._mb(mb)
@@ -983,7 +1070,7 @@ class PipelineEngine:
         tid = self._new_token(src, remote_token, mb)
         self.state.microbatch = mb
         self.state.model._step_had_backward = True
-        self._run_backward(tid, mb, saved, grads)
+        self._run_backward(tid, mb, saved, grads, tuple(key))
         self._maybe_finish(tid)
 
     def _ack(self, tid):

@@ -96,7 +96,7 @@ def test_flash_dropout_byte_keep_test_swar():
     M = 0xFFFFFFFF
     rnd = random.Random(0)
     words = [rnd.getrandbits(32) for _ in range(64)] + [0, M, 0x7F7F7F7F, 0x80808080, 0x807F0180]
-    for thr in range(1, 256):
+    for thr in range(0, 257):
         t7 = thr if thr <= 128 else 256 - thr
         xr = 0 if thr <= 128 else M
         c = (128 - t7) * 0x01010101
@@ -105,6 +105,13 @@ def test_flash_dropout_byte_keep_test_swar():
             f = ((((hx & 0x7F7F7F7F) + c) & M) | hx) ^ xr
             for i in range(4):
                 assert bool((f >> (8 * i + 7)) & 1) == (((h >> (8 * i)) & 0xFF) >= thr), (thr, hex(h), i)
-    assert A.flash_dropout_threshold(0.1) == 26 and abs(A.flash_dropout_keep_prob(0.1) - (1 - 26 / 256)) < 1e-12
-    keep = A.flash_dropout_keep_mask(2, 3, 64, 64, 0.1, 1234, 7)
-    assert abs(keep.float().mean().item() - A.flash_dropout_keep_prob(0.1)) < 0.01
+    # exact rate (the plain 8-bit threshold turned p = 0.001 into 0.0039): the
+    # per-block {lo, lo + 1} threshold mixture keeps every element at dropout_p to 2^-24
+    for p in (0.001, 0.01, 0.1, 0.37, 0.999):
+        lo, frac = A.flash_dropout_threshold(p)
+        assert abs((lo + frac / 65536.0) / 256.0 - p) < 2 ** -24
+        assert abs(A.flash_dropout_keep_prob(p) - (1 - p)) < 2 ** -24
+    keep = A.flash_dropout_keep_mask(2, 3, 256, 256, 0.1, 1234, 7)
+    assert abs(keep.float().mean().item() - 0.9) < 0.005
+    keep = A.flash_dropout_keep_mask(4, 4, 256, 256, 0.01, 99, 3)
+    assert abs((1 - keep.float().mean().item()) - 0.01) < 0.002

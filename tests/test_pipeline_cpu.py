@@ -280,6 +280,15 @@ def test_pp4_fast_mode_modulelist_matches_and_skips_the_parent():
     assert _fast_bytes(fast, 2)[-1] > 0
 
 
+def test_pp3_dp2_fast_mode_fanout_matches():
+    """Fast mode under PP x DDP: a block output consumed by two calls on the next stage (two
+    "dout" backward segments) and one consumed by two calls on its own stage (no dout): the
+    gradient tracker must expect exactly the remote count, or a DDP bucket is all-reduced
+    before the second dout's gradient lands (engine._stubify_result)."""
+    outs = run_workers("fast_mode", 6, [3, 2, 3, 1, "fanout"], timeout=300)
+    assert all("OK" in o for o in outs), outs
+
+
 @pytest.mark.parametrize("mode", ["change", "misuse"])
 def test_pp4_fast_mode_errors(mode):
     outs = run_workers("fast_mode", 4, [4, 2, 3, 1, mode], timeout=300)

@@ -4,6 +4,9 @@ unpartitioned reference trained in the same process.
 
 argv: pp microbatches steps fast(0|1) [mode]
 mode: "ok"       -- train, check loss/params every step, report the transport byte counters
+      "fanout"   -- as "ok", but one block output feeds two calls on the NEXT stage and another
+                    two calls on its OWN stage (the producer's backward-segment count for DDP,
+                    ADVICE r3: run at PP3 x DP2)
       "misuse"   -- the parent reads a block's output itself (outside any module call) after
                     the recording step: must raise NotSupportedByFastModeError
       "change"   -- the graph changes after the recording step (a block is skipped): must raise
@@ -34,22 +37,34 @@ class Block(nn.Module):
 class ListModel(nn.Module):
     """GPT-shaped: embedding -> ModuleList of blocks (python loop) -> head -> CE loss."""
 
-    def __init__(self, vocab=64, h=32, n=8):
+    def __init__(self, vocab=64, h=32, n=8, fan=False):
         super().__init__()
         self.emb = nn.Embedding(vocab, h)
         self.blocks = nn.ModuleList([Block(h) for _ in range(n)])
         self.head = nn.Linear(h, vocab)
+        self.fan = fan
+        if fan:
+            self.mix = nn.Linear(h, h)   # consumes block 3's output (on the stage after it)
+            self.mix2 = nn.Linear(h, h)  # consumes block 2's output (on block 2's own stage)
         self.skip = None  # "change" mode: index of a block to skip
         self.peek = False  # "misuse" mode: the parent reads a block output itself
 
     def forward(self, ids):
         h = self.emb(ids)
+        keep = {}
         for i, blk in enumerate(self.blocks):
             if i == self.skip:
                 continue
             h = blk(h)
+            keep[i] = h
             if self.peek and i == 2:
                 h = h * 1.0  # parent-side arithmetic on a child's output
+        if self.fan:
+            which = os.environ.get("FAN", "23")
+            if "3" in which:
+                h = h + self.mix(keep[3])
+            if "2" in which:
+                h = h + self.mix2(keep[2])
         logits = self.head(h)
         return nn.functional.cross_entropy(logits.reshape(-1, logits.size(-1)), ids.reshape(-1))
 
@@ -58,17 +73,21 @@ def main():
     pp, mbs, steps, fast = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), bool(int(sys.argv[4]))
     mode = sys.argv[5] if len(sys.argv) > 5 else "ok"
     torch.manual_seed(0)
-    ref = ListModel()
+    fan = mode == "fanout"
+    ref = ListModel(fan=fan)
     smp.init({"pipeline_parallel_degree": pp, "microbatches": mbs, "pipeline": "interleaved",
               "auto_partition": False, "default_partition": 0, "fast_mode": fast,
               "ddp": int(os.environ["WORLD_SIZE"]) > pp})
     dev = smp.state.device
-    net = ListModel()
+    net = ListModel(fan=fan)
     net.load_state_dict(ref.state_dict())
     ref.to(dev)
     n = len(net.blocks)
     for i, blk in enumerate(net.blocks):  # embedding + head stay with the parent on stage 0
         smp.set_partition(blk, min(pp - 1, 1 + (i * (pp - 1)) // n) if pp > 1 else 0)
+    if fan:
+        smp.set_partition(net.mix, min(pp - 1, 1 + (4 * (pp - 1)) // n))
+        smp.set_partition(net.mix2, min(pp - 1, 1 + (2 * (pp - 1)) // n))
     model = smp.DistributedModel(net)
     lr = 0.1
     opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=lr))
@@ -120,7 +139,7 @@ def main():
         if smp.pp_rank() == 0:
             mine = float(out.reduce_mean())
             assert abs(mine - rl.item()) < (1e-5 if dev.type == "cpu" else 2e-4), (it, mine, rl.item())
-    assert mode == "ok", f"{mode}: nothing raised"
+    assert mode in ("ok", "fanout"), f"{mode}: nothing raised"
     rp = dict(ref.named_parameters())
     for name, p in model.local_named_parameters():
         d = (p.detach() - rp[name].detach()).abs().max().item()
