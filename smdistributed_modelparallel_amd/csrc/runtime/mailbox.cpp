@@ -280,10 +280,21 @@ void Mailbox::send_loop(int peer) {
         stats_.gated_sent++;
         stats_.gate_wait_us += static_cast<uint64_t>(us.count());
       }
-      if (r < 0) {
-        std::lock_guard<std::mutex> g(in_mu_);
-        if (error_.empty()) error_ = "mailbox: readiness gate of a message to rank " + std::to_string(peer) + " failed";
-        in_cv_.notify_all();
+      if (r <= 0) {
+        // the gate failed (r < 0), or shutdown gave up waiting for it (r == 0): the receiver could
+        // pull bytes the producer's kernels have not finished writing, so the message is
+        // dropped and the failure recorded instead of sending an ungated handle
+        {
+          std::lock_guard<std::mutex> g(in_mu_);
+          if (error_.empty())
+            error_ = std::string("mailbox: readiness gate of a message to rank ") + std::to_string(peer) +
+                     (r < 0 ? " failed" : " still pending at shutdown (message dropped)");
+          in_cv_.notify_all();
+        }
+        std::lock_guard<std::mutex> g(p.mu);
+        p.writing = false;
+        p.cv.notify_all();
+        continue;
       }
     }
     const std::shared_ptr<const std::string>& f = m.frame;

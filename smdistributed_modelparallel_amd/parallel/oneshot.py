@@ -25,9 +25,9 @@ Failures after set-up are never silent: a kernel that waits longer than
 peer -- a rank skipped a call, died, or drifted away -- writes NaN instead of reducing stale
 slots, raises the instance's host-mapped error word and pushes an abort into every peer's
 flag array, so the peers' kernels fail too.  ``check_errors()`` (called by
-``DistributedModel`` at the end of every step: a host read, no synchronisation) raises
-``OneShotAllReduceError`` on every rank of the group, and the failed instance refuses all
-later calls.
+``DistributedModel`` at the end of every step, before the optimizer update: waits for the
+step's kernels, then the TP ranks agree on the verdict) raises ``OneShotAllReduceError`` on
+every rank of the group in the same step, and the failed instance refuses all later calls.
 """
 import os
 import socket
@@ -177,14 +177,31 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None, async_op=False):
     return x
 
 
-def check_errors():
+def check_errors(group=None):
     """Raise ``OneShotAllReduceError`` if a one-shot all-reduce of any group failed (own
-    timeout, or a peer's abort).  Non-blocking: reads the host-mapped error words; a kernel
-    still waiting is caught by a later call.  The failed instance stays disabled."""
-    for k, inst in _instances.items():
-        if inst is not None and (k in _failed or inst.error(False)):
+    timeout, or a peer's abort) -- on every rank of `group` (the TP group's gloo twin) in the
+    SAME step, before the optimizer update: the step's kernels are waited for before the
+    host-mapped error words are read, and the ranks agree on the verdict (a MAX over
+    `group`).  Without the wait and the agreement, a peer whose poisoned kernel was still
+    running passed the check and applied NaN gradients.  Costs one stream
+    synchronisation and one 4-byte gloo all-reduce per step, only while one-shot instances
+    exist.  The failed instance stays disabled."""
+    active = [(k, inst) for k, inst in _instances.items() if inst is not None]
+    if not active and not _failed:
+        return
+    if torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize()
+    for k, inst in active:
+        if k in _failed or inst.error(False):
             _failed.add(k)
-    if _failed:
+    failed = bool(_failed)
+    if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        flag = torch.tensor([1 if failed else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()) and not failed:
+            _failed.add("peer")
+            failed = True
+    if failed:
         raise OneShotAllReduceError(f"one-shot all-reduce failed on {len(_failed)} TP group(s): a kernel timed out "
                                     f"waiting for a peer rank (or a peer aborted); outputs were poisoned with NaN")
 

@@ -1,12 +1,21 @@
-"""``smp.amp.GradScaler`` (reference `smp/torch/amp/scaler.py:22-91`).
+"""``smp.amp.GradScaler`` (reference `smp/torch/amp/scaler.py:22-194`).
 
-torch's GradScaler, except that the inf/nan decision is shared across every rank that
-holds a different slice of the model (pipeline and tensor parallel ranks), so all stages
-skip the same steps.  One MAX all-reduce of the found-inf flag on the device replaces the
-reference's CPU object all-gather.
+torch's GradScaler, except that the inf/nan decision is shared by every rank that holds a
+different slice of the model (pipeline and tensor parallel ranks), so all stages skip the
+same steps and keep the same scale:
+
+* a stage that never calls ``scale()`` (every pp_rank but the loss stage) initialises its
+  scale lazily at ``unscale_``/``step`` (reference `:164-165`);
+* a stage without local parameters records a zero found-inf instead of torch's "No inf
+  checks were recorded" error (reference `:169-183`), and skips ``optimizer.step()``;
+* the collective count is fixed -- exactly one MAX all-reduce of a one-element device tensor
+  per ``step()`` and one per ``update()``, whatever number of devices or optimizers recorded
+  checks -- so ranks with different local state never issue mismatched collectives (the
+  reference all-gathers a CPU object over the PP group at the same two points).
 """
 import torch
 import torch.distributed as dist
+from torch.amp.grad_scaler import OptState
 
 from .state_mod import state
 
@@ -18,19 +27,66 @@ class GradScaler(torch.amp.GradScaler):
         super().__init__(device, init_scale=init_scale, growth_factor=growth_factor,
                          backoff_factor=backoff_factor, growth_interval=growth_interval, enabled=enabled)
 
-    def _maybe_opt_step(self, optimizer, optimizer_state, *args, **kwargs):
-        flags = list(optimizer_state["found_inf_per_device"].values())
-        found = sum(v.item() for v in flags)
-        t = torch.tensor([float(found)], device=state.device if state.initialized else "cpu")
+    def _dev(self):
+        if state.initialized and state.device is not None:
+            return state.device
+        return torch.device(self._device)
+
+    def _lazy_scale(self):
+        if self._enabled and self._scale is None:
+            self._lazy_init_scale_growth_tracker(self._dev())
+
+    def _combine(self, flag):
+        """MAX of a one-element float flag over the model-parallel group (one collective)."""
+        flag = flag.reshape(1).to(device=self._dev(), dtype=torch.float32)
         if state.initialized and state.core.mp_size() > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=state.pgs.mp)
-        if t.item() == 0:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=state.pgs.mp)
+        return flag
+
+    @staticmethod
+    def _has_local_params():
+        model = state.model if state.initialized else None
+        return model is None or any(True for _ in model.local_parameters())
+
+    def unscale_(self, optimizer):
+        if not self._enabled:
+            return
+        self._lazy_scale()
+        super().unscale_(optimizer)
+        st = self._per_optimizer_states[id(optimizer)]
+        if not st["found_inf_per_device"]:  # no local gradients on this rank
+            st["found_inf_per_device"] = {self._dev(): torch.zeros(1, device=self._dev())}
+
+    def step(self, optimizer, *args, **kwargs):
+        if not self._enabled:
             return optimizer.step(*args, **kwargs)
-        return None
+        if "closure" in kwargs:
+            raise RuntimeError("Closure use is not currently supported if GradScaler is enabled.")
+        self._lazy_scale()
+        st = self._per_optimizer_states[id(optimizer)]
+        if st["stage"] is OptState.STEPPED:
+            raise RuntimeError("step() has already been called since the last update().")
+        if st["stage"] is OptState.READY:
+            self.unscale_(optimizer)
+        local = sum(v.to(self._dev()).float().sum() for v in st["found_inf_per_device"].values())
+        found = self._combine(torch.as_tensor(local))
+        retval = None
+        if found.item() == 0 and self._has_local_params():
+            retval = optimizer.step(*args, **kwargs)
+        st["stage"] = OptState.STEPPED
+        return retval
 
     def update(self, new_scale=None):
-        if state.initialized and state.core.mp_size() > 1 and self._enabled:
-            for st in self._per_optimizer_states.values():
-                for dev, v in st["found_inf_per_device"].items():
-                    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=state.pgs.mp)
+        if not self._enabled:
+            return
+        self._lazy_scale()
+        if new_scale is None:
+            states = list(self._per_optimizer_states.values())
+            flags = [v for st in states for v in st["found_inf_per_device"].values()]
+            if not flags:
+                raise RuntimeError("No inf checks were recorded prior to update.")
+            combined = self._combine(sum(v.to(self._dev()).float().sum() for v in flags))
+            zero = torch.zeros(1, device=self._dev())
+            for i, st in enumerate(states):
+                st["found_inf_per_device"] = {self._dev(): combined if i == 0 else zero}
         return super().update(new_scale)

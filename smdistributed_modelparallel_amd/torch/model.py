@@ -396,6 +396,39 @@ class DistributedModel(nn.Module):
                     if b is not None and b.numel() > 0 and b.is_floating_point():
                         dist.broadcast(b, src_dp, group=state.pgs.dp)
 
+    def _sync_buffers(self):
+        """Per-step buffer broadcast (reference `ddp_model.py:518-540`, `_pre_ddp_step` at
+        `:605-607`): module buffers (BatchNorm running statistics, ...) follow the
+        authoritative replica -- DP group rank 0; buffers of TP-sliced modules over the RDP
+        group -- before every step, coalesced into one broadcast per (group, dtype).  Under
+        ``model.join()`` the replicas are re-synchronised from the longest-running rank when
+        the join ends instead (`_join_shadow`)."""
+        core = state.core
+        if not (self.broadcast_buffers and state.cfg is not None and state.cfg.ddp) or core.dp_size() < 2:
+            return
+        groups = {}
+        for b in self.local_buffers():
+            if b is None or b.numel() == 0:
+                continue
+            scaled = self.is_distributed_buffer(b) and core.tp_size() > 1
+            if scaled and core.rdp_size() < 2:
+                continue
+            groups.setdefault((scaled, b.dtype, b.device), []).append(b)
+        if not groups:
+            return
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+        with torch.no_grad():
+            for (scaled, _, _), bufs in sorted(groups.items(), key=lambda kv: (kv[0][0], str(kv[0][1]))):
+                if scaled:
+                    src, grp = core.ranker.translate(core.pp_rank(), core.tp_rank(), 0), state.pgs.rdp
+                else:
+                    src, grp = core.ranker.translate(core.pp_rank(), 0, 0), state.pgs.dp
+                flat = _flatten_dense_tensors(bufs)
+                dist.broadcast(flat, src, group=grp)
+                for b, v in zip(bufs, _unflatten_dense_tensors(flat, bufs)):
+                    b.copy_(v)
+
     # ============================================================ step hooks
     def _begin_microbatch(self, mb, num_mb):
         final = mb == num_mb - 1 and state.core.pp_size() == 1
@@ -430,6 +463,8 @@ class DistributedModel(nn.Module):
         joining = self.partitioned and getattr(self, "_join", None) is not None
         if joining:
             self._join_begin_step(sync)
+        elif self.partitioned and torch.is_grad_enabled():
+            self._sync_buffers()
         yield
         if not self.partitioned:
             return
@@ -450,10 +485,10 @@ class DistributedModel(nn.Module):
                 self._post_step_hooks_run.add(name)
                 hook(self, state.optimizer)
         # a one-shot TP all-reduce that timed out (or whose peer aborted) poisoned its output:
-        # surface it on every rank of the group now (a host read, no device synchronisation)
+        # surface it on every rank of the TP group in this step, before the optimizer update
         from ..parallel import oneshot
 
-        oneshot.check_errors()
+        oneshot.check_errors(state.pgs.cpu_tp if state.pgs is not None else None)
         if state.core.pp_size() > 1:
             state.comm.barrier(CommGroup.PP_GROUP)
 

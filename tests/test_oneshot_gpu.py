@@ -42,3 +42,8 @@ def test_oneshot_skipped_call_raises_on_every_rank():
     outs = run_workers("oneshot_gpu", 2, ["skip"], timeout=110,
                        env_extra=dict(_ENV, SMP_ONESHOT_ALLREDUCE_TIMEOUT_S="3"))
     assert all("OK raised" in o for o in outs)
+
+
+def test_oneshot_failure_agreed_in_the_same_step():
+    outs = run_workers("oneshot_gpu", 2, ["agree"], timeout=110, env_extra=_ENV)
+    assert all("OK raised in the same step" in o for o in outs), outs

@@ -280,6 +280,21 @@ def test_pp4_fast_mode_modulelist_matches_and_skips_the_parent():
     assert _fast_bytes(fast, 2)[-1] > 0
 
 
+def test_amp_grad_scaler_pp2_stage_without_params():
+    """smp.amp.GradScaler: overflow skips the step on every stage (one without parameters
+    included) and the scale trajectory matches torch's GradScaler (reference amp/scaler.py)."""
+    outs = run_workers("amp_scaler", 2, [], timeout=200)
+    assert all("OK" in o for o in outs), outs
+    assert "local_params=0" in outs[1]
+
+
+@pytest.mark.parametrize("pp", [1, 2])
+def test_ddp_buffers_follow_rank0_every_step(pp):
+    """Per-step buffer broadcast from DP rank 0 (reference ddp_model.py:518-540,605-607)."""
+    outs = run_workers("ddp_buffers", 2 * pp, [pp], timeout=200)
+    assert all("OK" in o for o in outs), outs
+
+
 def test_pp3_dp2_fast_mode_fanout_matches():
     """Fast mode under PP x DDP: a block output consumed by two calls on the next stage (two
     "dout" backward segments) and one consumed by two calls on its own stage (no dout): the

@@ -87,6 +87,29 @@ def skip():
     dist.barrier()
 
 
+def agree():
+    """Rank 0's instance fails (injected) while rank 1's kernels all succeeded: the end-of-step
+    check must raise on BOTH ranks in the same call (rank 1 used to pass and apply
+    its update, raising only a step later)."""
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    from smdistributed_modelparallel_amd.parallel import oneshot
+
+    r = dist.get_rank()
+    x = torch.ones(4096, device="cuda")
+    oneshot.all_reduce(x)
+    oneshot.check_errors(dist.group.WORLD)  # healthy: no raise on either rank
+    if r == 0:
+        oneshot.inject_failure()
+    try:
+        oneshot.check_errors(dist.group.WORLD)
+    except oneshot.OneShotAllReduceError as e:
+        print(f"rank {r} OK raised in the same step: {str(e)[:40]}", flush=True)
+    else:
+        raise AssertionError(f"rank {r}: check_errors did not raise")
+    dist.barrier()
+
+
 def tp(steps):
     import smdistributed_modelparallel_amd.torch as smp
     from smdistributed_modelparallel_amd.models import build_gpt
@@ -127,5 +150,7 @@ if __name__ == "__main__":
         kernel()
     elif sys.argv[1] == "skip":
         skip()
+    elif sys.argv[1] == "agree":
+        agree()
     else:
         tp(int(sys.argv[2]))
