@@ -73,6 +73,61 @@ void fused_adagrad(c10::optional<at::Tensor> param, at::Tensor grad, at::Tensor 
         "fused_adagrad");
 }
 
+// ---------------------------------------------------------- multi-tensor apply
+// meta: int64 GPU tensor = 6 x nt role pointers + nchunks x 3 chunk ranges (ops/multi_tensor.py
+// MTMeta); g0 / p0: first grad / param of the list (their dtypes select the kernel)
+const int64_t* mt_meta(const at::Tensor& meta, int64_t nt, int64_t nchunks) {
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kLong && meta.is_contiguous(), "mt: meta must be int64 GPU");
+  TORCH_CHECK(meta.numel() == 6 * nt + 3 * nchunks, "mt: meta size mismatch");
+  return meta.data_ptr<int64_t>();
+}
+
+void mt_adam(at::Tensor meta, int64_t nt, int64_t nchunks, at::Tensor g0, at::Tensor p0, bool master, double lr,
+             double b1, double b2, double eps, double wd, double bc1, double bc2, double gscale, bool adamw) {
+  check(smpk::mt_adam(mt_meta(meta, nt, nchunks), nt, nchunks, dt_code(p0), dt_code(g0), master ? 1 : 0, lr, b1, b2,
+                      eps, wd, bc1, bc2, gscale, adamw ? 1 : 0, stream()),
+        "mt_adam");
+}
+
+void mt_norm(at::Tensor meta, int64_t nt, int64_t nchunks, int64_t role, at::Tensor sample, at::Tensor out,
+             double scale, bool maxabs) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() >= nt, "mt_norm: bad out");
+  check(smpk::mt_norm(mt_meta(meta, nt, nchunks), nt, nchunks, static_cast<int>(role), dt_code(sample), scale,
+                      maxabs ? 1 : 0, out.data_ptr<float>(), stream()),
+        "mt_norm");
+}
+
+void mt_lamb1(at::Tensor meta, int64_t nt, int64_t nchunks, at::Tensor g0, at::Tensor p0, bool master, double b1,
+              double b2, double b3, double bc1, double bc2, double eps, double wd, bool decoupled, at::Tensor gnorm,
+              double max_gnorm, double gscale) {
+  TORCH_CHECK(gnorm.is_cuda() && gnorm.scalar_type() == at::kFloat, "mt_lamb1: gnorm must be a float GPU tensor");
+  check(smpk::mt_lamb1(mt_meta(meta, nt, nchunks), nt, nchunks, dt_code(p0), dt_code(g0), master ? 1 : 0, b1, b2, b3,
+                       bc1, bc2, eps, wd, decoupled ? 1 : 0, gnorm.data_ptr<float>(), max_gnorm, gscale, stream()),
+        "mt_lamb1");
+}
+
+void mt_lamb2(at::Tensor meta, int64_t nt, int64_t nchunks, at::Tensor p0, bool master, at::Tensor pn2, at::Tensor un2,
+              double lr, bool use_trust) {
+  check(smpk::mt_lamb2(mt_meta(meta, nt, nchunks), nt, nchunks, dt_code(p0), master ? 1 : 0, pn2.data_ptr<float>(),
+                       un2.data_ptr<float>(), lr, use_trust ? 1 : 0, stream()),
+        "mt_lamb2");
+}
+
+void mt_novograd(at::Tensor meta, int64_t nt, int64_t nchunks, at::Tensor g0, at::Tensor p0, bool master,
+                 at::Tensor norms, double b1, double b3, double bc1, double bc2, double eps, double lr, double wd,
+                 bool decoupled, double gscale) {
+  check(smpk::mt_novograd(mt_meta(meta, nt, nchunks), nt, nchunks, dt_code(p0), dt_code(g0), master ? 1 : 0,
+                          norms.data_ptr<float>(), b1, b3, bc1, bc2, eps, lr, wd, decoupled ? 1 : 0, gscale, stream()),
+        "mt_novograd");
+}
+
+void novograd_blend(at::Tensor norms, at::Tensor fresh, double b2, bool l2, bool first, bool init_zero) {
+  TORCH_CHECK(norms.is_cuda() && fresh.is_cuda() && norms.numel() == fresh.numel(), "novograd_blend: bad tensors");
+  check(smpk::novograd_blend(norms.data_ptr<float>(), fresh.data_ptr<float>(), norms.numel(), b2, l2 ? 1 : 0,
+                             first ? 1 : 0, init_zero ? 1 : 0, stream()),
+        "novograd_blend");
+}
+
 void lamb_stage1(at::Tensor grad, at::Tensor master, at::Tensor m, at::Tensor v, at::Tensor update, double beta1,
                  double beta2, double eps, double wd, double bc1, double bc2, double grad_scale) {
   check_gpu(grad, "grad");
@@ -684,6 +739,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_adam", &fused_adam);
   m.def("fused_sgd", &fused_sgd);
   m.def("fused_adagrad", &fused_adagrad);
+  m.def("mt_adam", &mt_adam);
+  m.def("mt_norm", &mt_norm);
+  m.def("mt_lamb1", &mt_lamb1);
+  m.def("mt_lamb2", &mt_lamb2);
+  m.def("mt_novograd", &mt_novograd);
+  m.def("novograd_blend", &novograd_blend);
   m.def("lamb_stage1", &lamb_stage1);
   m.def("lamb_stage2", &lamb_stage2);
   m.def("lamb_chunked_", &lamb_chunked);

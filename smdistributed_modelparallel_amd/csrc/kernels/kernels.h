@@ -37,6 +37,21 @@ int lamb_stage2_chunked(int param_dt, void* param, float* master, const float* u
                         int64_t nchunks, const float* norms, float lr, int use_trust, hipStream_t s);
 // sum of squares of x (any dtype) * scale^2 accumulated into *out (fp32, atomic).
 int sumsq(int dt, const void* x, int64_t n, float scale, float* out, hipStream_t s);
+// multi-tensor apply over tensor lists (optim.hip: meta = role pointer table + chunk table)
+int mt_adam(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master, float lr,
+            float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, int adamw, hipStream_t s);
+int mt_norm(const int64_t* meta, int64_t nt, int64_t nchunks, int role, int dt, float scale, int maxabs, float* out,
+            hipStream_t s);
+int mt_lamb1(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master, float b1,
+             float b2, float b3, float bc1, float bc2, float eps, float wd, int decoupled, const float* gnorm,
+             float max_gnorm, float gscale, hipStream_t s);
+int mt_lamb2(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int master, const float* pn2,
+             const float* un2, float lr, int use_trust, hipStream_t s);
+int mt_novograd(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master,
+                const float* norms, float b1, float b3, float bc1, float bc2, float eps, float lr, float wd,
+                int decoupled, float gscale, hipStream_t s);
+int novograd_blend(float* norms, const float* fresh, int64_t nt, float b2, int l2, int first, int init_zero,
+                   hipStream_t s);
 // *out = max(*out, 1 if any element non-finite).
 int nonfinite(int dt, const void* x, int64_t n, float* out, hipStream_t s);
 // y = a * x + b * y (elementwise, same dtype) ; y may equal x.

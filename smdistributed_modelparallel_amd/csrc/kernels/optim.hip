@@ -293,7 +293,301 @@ __global__ void __launch_bounds__(kThreads) lamb2_chunked_kernel(P* __restrict__
   }
 }
 
+// ---- multi-tensor apply (amp_C multi_tensor_* equivalents, N4 / K12-K16) ------------------
+// One launch updates a whole LIST of separately allocated tensors (the standalone FusedAdam /
+// FusedLAMB / FusedNovoGrad path; the DistributedOptimizer path runs on flat buffers instead).
+// meta (int64, device): kRoles x nt tensor pointers (role-major; 0 = absent) followed by
+// nchunks x 3 (tensor, start, end) element ranges of <= 65536 elements; one block per chunk.
+// Roles: 0 grad (G), 1 param (P), 2 fp32 master (MASTER) -- without it P is fp32 and is its own
+// master --, 3 first moment, 4 second moment, 5 fp32 update scratch (LAMB).
+constexpr int kRoles = 6;
+
+struct MTChunk {
+  int t;
+  int64_t s, e;
+};
+
+__device__ __forceinline__ MTChunk mt_chunk(const int64_t* meta, int64_t nt) {
+  const int64_t* c = meta + kRoles * nt + 3 * static_cast<int64_t>(blockIdx.x);
+  return MTChunk{static_cast<int>(c[0]), c[1], c[2]};
+}
+
+template <typename T>
+__device__ __forceinline__ T* mt_ptr(const int64_t* meta, int64_t nt, int role, int t) {
+  return reinterpret_cast<T*>(static_cast<uintptr_t>(meta[role * nt + t]));
+}
+
+// elements [s, e) of one chunk, 4 per thread per step (chunk bases are 4-aligned; load4 /
+// store4 fall back to scalar accesses at a tensor's tail or an unaligned base)
+#define SMPK_MT_LOOP(i) for (int64_t i = ch.s + threadIdx.x * kVec; i < ch.e; i += kThreads * kVec)
+
+template <typename P, typename G, bool MASTER>
+__global__ void __launch_bounds__(kThreads) mt_adam_kernel(const int64_t* __restrict__ meta, int64_t nt, float lr,
+                                                           float b1, float b2, float eps, float wd, float bc1,
+                                                           float bc2, float gscale, int adamw) {
+  const MTChunk ch = mt_chunk(meta, nt);
+  const G* g = mt_ptr<const G>(meta, nt, 0, ch.t);
+  P* prm = mt_ptr<P>(meta, nt, 1, ch.t);
+  float* mst = MASTER ? mt_ptr<float>(meta, nt, 2, ch.t) : reinterpret_cast<float*>(prm);
+  float* m = mt_ptr<float>(meta, nt, 3, ch.t);
+  float* v = mt_ptr<float>(meta, nt, 4, ch.t);
+  const float step_size = lr / bc1, inv_sqrt_bc2 = rsqrtf(bc2);
+  SMPK_MT_LOOP(i) {
+    float gg[4], p[4], mm[4], vv[4];
+    load4(g, i, ch.e, gg);
+    load4(mst, i, ch.e, p);
+    load4(m, i, ch.e, mm);
+    load4(v, i, ch.e, vv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float gj = gg[j] * gscale;
+      if (adamw) {
+        p[j] -= lr * wd * p[j];
+      } else {
+        gj += wd * p[j];
+      }
+      mm[j] = b1 * mm[j] + (1.f - b1) * gj;
+      vv[j] = b2 * vv[j] + (1.f - b2) * gj * gj;
+      p[j] -= step_size * mm[j] / (sqrtf(vv[j]) * inv_sqrt_bc2 + eps);
+    }
+    store4(mst, i, ch.e, p);
+    store4(m, i, ch.e, mm);
+    store4(v, i, ch.e, vv);
+    if (MASTER) store4(prm, i, ch.e, p);
+  }
+}
+
+// per-tensor sum of squares (MAXABS: max |x|) of role `role`, accumulated into out[t]
+template <typename T, bool MAXABS>
+__global__ void __launch_bounds__(kThreads) mt_norm_kernel(const int64_t* __restrict__ meta, int64_t nt, int role,
+                                                           float scale, float* __restrict__ out) {
+  __shared__ float smem[16];
+  const MTChunk ch = mt_chunk(meta, nt);
+  const T* x = mt_ptr<const T>(meta, nt, role, ch.t);
+  float a = 0.f;
+  SMPK_MT_LOOP(i) {
+    float xv[4];
+    load4(x, i, ch.e, xv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float y = xv[j] * scale;
+      a = MAXABS ? fmaxf(a, fabsf(y)) : fmaf(y, y, a);
+    }
+  }
+  a = MAXABS ? block_max(a, smem) : block_sum(a, smem);
+  if (threadIdx.x == 0) {
+    if (MAXABS) {
+      atomicMax(reinterpret_cast<int*>(out + ch.t), __float_as_int(a));  // a >= 0: int order = float order
+    } else {
+      atomicAdd(out + ch.t, a);
+    }
+  }
+}
+
+// LAMB stage 1 (apex LAMBStage1Functor): update = m_hat / (sqrt(v_hat) + eps) [+ wd * p], with
+// the gradient divided by the clipped global gradient norm; the update goes to the scratch role
+template <typename P, typename G, bool MASTER>
+__global__ void __launch_bounds__(kThreads) mt_lamb1_kernel(const int64_t* __restrict__ meta, int64_t nt, float b1,
+                                                            float b2, float b3, float bc1, float bc2, float eps,
+                                                            float wd, int decoupled, const float* __restrict__ gnorm,
+                                                            float max_gnorm, float gscale) {
+  const MTChunk ch = mt_chunk(meta, nt);
+  const G* g = mt_ptr<const G>(meta, nt, 0, ch.t);
+  const float* mst = MASTER ? mt_ptr<const float>(meta, nt, 2, ch.t) : mt_ptr<const float>(meta, nt, 1, ch.t);
+  float* m = mt_ptr<float>(meta, nt, 3, ch.t);
+  float* v = mt_ptr<float>(meta, nt, 4, ch.t);
+  float* u = mt_ptr<float>(meta, nt, 5, ch.t);
+  const float gn = *gnorm;
+  const float clip = (max_gnorm > 0.f && gn > max_gnorm) ? gn / max_gnorm : 1.f;
+  const float gmul = gscale / clip;
+  SMPK_MT_LOOP(i) {
+    float gg[4], p[4], mm[4], vv[4], uu[4];
+    load4(g, i, ch.e, gg);
+    load4(mst, i, ch.e, p);
+    load4(m, i, ch.e, mm);
+    load4(v, i, ch.e, vv);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float sg = gg[j] * gmul;
+      if (!decoupled) sg += wd * p[j];
+      mm[j] = mm[j] * b1 + b3 * sg;
+      vv[j] = vv[j] * b2 + (1.f - b2) * sg * sg;
+      uu[j] = (mm[j] / bc1) / (sqrtf(vv[j] / bc2) + eps);
+      if (decoupled) uu[j] += wd * p[j];
+    }
+    store4(m, i, ch.e, mm);
+    store4(v, i, ch.e, vv);
+    store4(u, i, ch.e, uu);
+  }
+}
+
+// LAMB stage 2 (apex LAMBStage2Functor): p -= lr * trust * update, trust = ||p|| / ||u|| per
+// tensor (when use_nvlamb or weight decay is on)
+template <typename P, bool MASTER>
+__global__ void __launch_bounds__(kThreads) mt_lamb2_kernel(const int64_t* __restrict__ meta, int64_t nt,
+                                                            const float* __restrict__ pn2,
+                                                            const float* __restrict__ un2, float lr, int use_trust) {
+  const MTChunk ch = mt_chunk(meta, nt);
+  P* prm = mt_ptr<P>(meta, nt, 1, ch.t);
+  float* mst = MASTER ? mt_ptr<float>(meta, nt, 2, ch.t) : reinterpret_cast<float*>(prm);
+  const float* u = mt_ptr<const float>(meta, nt, 5, ch.t);
+  float ratio = lr;
+  if (use_trust) {
+    const float a = sqrtf(pn2[ch.t]), b = sqrtf(un2[ch.t]);
+    ratio = (a != 0.f && b != 0.f) ? lr * (a / b) : lr;
+  }
+  SMPK_MT_LOOP(i) {
+    float p[4], uu[4];
+    load4(mst, i, ch.e, p);
+    load4(u, i, ch.e, uu);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] -= ratio * uu[j];
+    store4(mst, i, ch.e, p);
+    if (MASTER) store4(prm, i, ch.e, p);
+  }
+}
+
+// NovoGrad (apex NovoGradFunctor): per-tensor second moment = blended gradient NORM (not its
+// square); moment mode 0 = regularisation inside the moment, 1 = decoupled weight decay
+template <typename P, typename G, bool MASTER>
+__global__ void __launch_bounds__(kThreads) mt_novograd_kernel(const int64_t* __restrict__ meta, int64_t nt,
+                                                               const float* __restrict__ norms, float b1, float b3,
+                                                               float bc1, float bc2, float eps, float lr, float wd,
+                                                               int decoupled, float gscale) {
+  const MTChunk ch = mt_chunk(meta, nt);
+  const G* g = mt_ptr<const G>(meta, nt, 0, ch.t);
+  P* prm = mt_ptr<P>(meta, nt, 1, ch.t);
+  float* mst = MASTER ? mt_ptr<float>(meta, nt, 2, ch.t) : reinterpret_cast<float*>(prm);
+  float* m = mt_ptr<float>(meta, nt, 3, ch.t);
+  const float denom = norms[ch.t] / bc2 + eps;
+  SMPK_MT_LOOP(i) {
+    float gg[4], p[4], mm[4];
+    load4(g, i, ch.e, gg);
+    load4(mst, i, ch.e, p);
+    load4(m, i, ch.e, mm);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gj = gg[j] * gscale;
+      if (!decoupled) {
+        mm[j] = b1 * mm[j] + b3 * (gj / denom + wd * p[j]);
+        p[j] -= lr * (mm[j] / bc1);
+      } else {
+        mm[j] = b1 * mm[j] + b3 * gj;
+        p[j] -= lr * ((mm[j] / bc1) / denom + wd * p[j]);
+      }
+    }
+    store4(mst, i, ch.e, p);
+    store4(m, i, ch.e, mm);
+    if (MASTER) store4(prm, i, ch.e, p);
+  }
+}
+
+// blended per-tensor NovoGrad norms (apex multi_tensor_norm_out with a = b2, b = 1 - b2):
+// L2 gn = sqrt(b2 gn^2 + (1 - b2) n^2) from the new sum of squares; L-inf gn = b2 gn + (1 - b2) n.
+// First step: gn starts at n (or at 0 with init_zero).
+__global__ void __launch_bounds__(kThreads) novograd_blend_kernel(float* __restrict__ norms,
+                                                                  const float* __restrict__ fresh, int64_t nt, float b2,
+                                                                  int l2, int first, int init_zero) {
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (t >= nt) return;
+  const float n = l2 ? sqrtf(fresh[t]) : fresh[t];
+  const float old = first ? (init_zero ? 0.f : n) : norms[t];
+  norms[t] = l2 ? sqrtf(b2 * old * old + (1.f - b2) * n * n) : b2 * old + (1.f - b2) * n;
+}
+#undef SMPK_MT_LOOP
+
 }  // namespace
+
+int mt_adam(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master, float lr,
+            float b1, float b2, float eps, float wd, float bc1, float bc2, float gscale, int adamw, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  SMPK_DISPATCH(grad_dt, G, {
+    if (!master) {
+      if (param_dt != F32) return -2;
+      mt_adam_kernel<float, G, false><<<grid, kThreads, 0, s>>>(meta, nt, lr, b1, b2, eps, wd, bc1, bc2, gscale, adamw);
+    } else {
+      SMPK_DISPATCH(param_dt, P, {
+        mt_adam_kernel<P, G, true><<<grid, kThreads, 0, s>>>(meta, nt, lr, b1, b2, eps, wd, bc1, bc2, gscale, adamw);
+      });
+    }
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int mt_norm(const int64_t* meta, int64_t nt, int64_t nchunks, int role, int dt, float scale, int maxabs, float* out,
+            hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  SMPK_DISPATCH(dt, T, {
+    if (maxabs) {
+      mt_norm_kernel<T, true><<<grid, kThreads, 0, s>>>(meta, nt, role, scale, out);
+    } else {
+      mt_norm_kernel<T, false><<<grid, kThreads, 0, s>>>(meta, nt, role, scale, out);
+    }
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int mt_lamb1(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master, float b1,
+             float b2, float b3, float bc1, float bc2, float eps, float wd, int decoupled, const float* gnorm,
+             float max_gnorm, float gscale, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  SMPK_DISPATCH(grad_dt, G, {
+    if (!master) {
+      if (param_dt != F32) return -2;
+      mt_lamb1_kernel<float, G, false><<<grid, kThreads, 0, s>>>(meta, nt, b1, b2, b3, bc1, bc2, eps, wd, decoupled,
+                                                                  gnorm, max_gnorm, gscale);
+    } else {
+      mt_lamb1_kernel<float, G, true><<<grid, kThreads, 0, s>>>(meta, nt, b1, b2, b3, bc1, bc2, eps, wd, decoupled,
+                                                                 gnorm, max_gnorm, gscale);
+    }
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int mt_lamb2(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int master, const float* pn2,
+             const float* un2, float lr, int use_trust, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  if (!master) {
+    if (param_dt != F32) return -2;
+    mt_lamb2_kernel<float, false><<<grid, kThreads, 0, s>>>(meta, nt, pn2, un2, lr, use_trust);
+  } else {
+    SMPK_DISPATCH(param_dt, P, { mt_lamb2_kernel<P, true><<<grid, kThreads, 0, s>>>(meta, nt, pn2, un2, lr, use_trust); });
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+int mt_novograd(const int64_t* meta, int64_t nt, int64_t nchunks, int param_dt, int grad_dt, int master,
+                const float* norms, float b1, float b3, float bc1, float bc2, float eps, float lr, float wd,
+                int decoupled, float gscale, hipStream_t s) {
+  if (nchunks <= 0) return 0;
+  const unsigned grid = static_cast<unsigned>(nchunks);
+  SMPK_DISPATCH(grad_dt, G, {
+    if (!master) {
+      if (param_dt != F32) return -2;
+      mt_novograd_kernel<float, G, false><<<grid, kThreads, 0, s>>>(meta, nt, norms, b1, b3, bc1, bc2, eps, lr, wd,
+                                                                     decoupled, gscale);
+    } else {
+      SMPK_DISPATCH(param_dt, P, {
+        mt_novograd_kernel<P, G, true><<<grid, kThreads, 0, s>>>(meta, nt, norms, b1, b3, bc1, bc2, eps, lr, wd,
+                                                                  decoupled, gscale);
+      });
+    }
+  });
+  return static_cast<int>(hipGetLastError());
+}
+
+int novograd_blend(float* norms, const float* fresh, int64_t nt, float b2, int l2, int first, int init_zero,
+                   hipStream_t s) {
+  if (nt <= 0) return 0;
+  novograd_blend_kernel<<<static_cast<unsigned>((nt + kThreads - 1) / kThreads), kThreads, 0, s>>>(
+      norms, fresh, nt, b2, l2, first, init_zero);
+  return static_cast<int>(hipGetLastError());
+}
+
 
 int lamb_norms_chunked(const float* master, const float* update, const int64_t* chunks, int64_t nchunks,
                        float* norms, hipStream_t s) {

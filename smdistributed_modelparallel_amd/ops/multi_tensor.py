@@ -156,3 +156,64 @@ def cast_copy_(src, dst, scale=1.0):
     else:
         dst.copy_(src.float() * scale if scale != 1.0 else src)
     return dst
+
+
+# ------------------------------------------------------------------ multi-tensor apply
+MT_CHUNK = 1 << 16  # elements per block (apex: 2048 x 32)
+MT_ROLES = ("grad", "param", "master", "m", "v", "update")
+
+
+class MTList:
+    """A list of tensors for one multi-tensor launch (amp_C ``multi_tensor_applier``): role
+    name -> list of tensors (same length; None = role absent).  On the GPU the role pointers
+    and the <= 64K-element chunk table travel in one int64 tensor (`optim.hip` meta layout);
+    it is rebuilt only when a pointer changed (gradients set to None re-allocate)."""
+
+    __slots__ = ("roles", "n", "numel", "_key", "_meta", "_nchunks", "_host")
+
+    def __init__(self):
+        self._key = None
+        self._meta = None
+        self._host = None
+
+    def set(self, **roles):
+        self.roles = roles
+        first = next(iter(roles.values()))
+        self.n = len(first)
+        self.numel = [t.numel() for t in first]
+        return self
+
+    def meta(self, device):
+        ptrs = []
+        for r in MT_ROLES:
+            lst = self.roles.get(r)
+            ptrs.extend([0] * self.n if lst is None else [0 if t is None else t.data_ptr() for t in lst])
+        key = tuple(ptrs)
+        if key != self._key:
+            import numpy as np
+
+            chunks = []
+            for ti, n in enumerate(self.numel):
+                st = np.arange(0, n, MT_CHUNK, dtype=np.int64)
+                chunks.append(np.stack([np.full_like(st, ti), st, np.minimum(st + MT_CHUNK, n)], axis=1))
+            table = np.concatenate(chunks) if chunks else np.zeros((0, 3), dtype=np.int64)
+            host = np.concatenate([np.array(ptrs, dtype=np.uint64).view(np.int64), table.reshape(-1)])
+            # pinned staging kept alive on the object until the next rebuild (async upload)
+            self._host = torch.from_numpy(host).pin_memory()
+            self._meta = self._host.to(device, non_blocking=True)
+            self._nchunks = int(table.shape[0])
+            self._key = key
+        return self._meta, self.n, self._nchunks
+
+
+def mt_norms(lst, role, out, maxabs=False, scale=1.0):
+    """Per-tensor sum of squares (or max |x|) of `role` accumulated into out[t] (fp32)."""
+    tensors = lst.roles[role]
+    if out.is_cuda:
+        meta, nt, nc = lst.meta(out.device)
+        ext().mt_norm(meta, nt, nc, MT_ROLES.index(role), tensors[0], out, scale, maxabs)
+        return out
+    for i, t in enumerate(tensors):
+        x = t.float() * scale
+        out[i] = torch.maximum(out[i], x.abs().max()) if maxabs else out[i] + x.pow(2).sum()
+    return out

@@ -9,7 +9,7 @@ from tests.dist_utils import run_workers
 
 def test_lamb_and_novograd_match_reference():
     outs = run_workers("opt_cpu", 1, [], timeout=120)
-    assert "OK lamb" in outs[0] and "OK novograd" in outs[0]
+    assert "OK lamb" in outs[0] and "OK novograd" in outs[0] and "OK lamb-standalone" in outs[0]
 
 
 def test_lamb_chunk_table_covers_pieces(monkeypatch):

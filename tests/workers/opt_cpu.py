@@ -55,31 +55,90 @@ def lamb():
     print("OK lamb", flush=True)
 
 
-def novograd():
-    torch.manual_seed(1)
-    ps = [torch.randn(5, 4, requires_grad=True), torch.randn(3, requires_grad=True)]
-    rs = [p.detach().clone().double() for p in ps]
-    opt = FusedNovoGrad(ps, lr=0.1, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01)
-    v = [None, None]
+def ref_novograd(rs, gs_steps, lr, b1, b2, eps, wd, reg_inside=False, norm_type=2, init_zero=False):
+    """apex multi_tensor_novograd semantics, float64: per-tensor gradient NORM blended as
+    sqrt(b2 n_old^2 + (1 - b2) n^2) (L2) / b2 n_old + (1 - b2) n (L-inf), first step from n."""
+    v = [None] * len(rs)
     m = [torch.zeros_like(r) for r in rs]
-    for step in range(1, 4):
-        gs = [torch.randn_like(p) for p in ps]
-        for p, g in zip(ps, gs):
-            p.grad = g.clone()
-        opt.step()
+    for step, gs in enumerate(gs_steps, 1):
+        bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
         for i, (r, g) in enumerate(zip(rs, gs)):
             g = g.double()
-            n2 = float((g * g).sum())
-            v[i] = n2 if v[i] is None else 0.98 * v[i] + 0.02 * n2
-            upd = g / (v[i] ** 0.5 + 1e-8) + 0.01 * r
-            m[i] = 0.9 * m[i] + 0.1 * upd
-            r -= 0.1 * m[i] / (1 - 0.9 ** step)
-    for p, r in zip(ps, rs):
-        assert torch.allclose(p.detach().double(), r, atol=1e-5), (p - r).abs().max()
+            n = float(g.norm()) if norm_type == 2 else float(g.abs().max())
+            old = (0.0 if init_zero else n) if v[i] is None else v[i]
+            v[i] = (b2 * old * old + (1 - b2) * n * n) ** 0.5 if norm_type == 2 else b2 * old + (1 - b2) * n
+            denom = v[i] / bc2 + eps
+            if reg_inside:
+                m[i] = b1 * m[i] + (1 - b1) * (g / denom + wd * r)
+                r -= lr * m[i] / bc1
+            else:
+                m[i] = b1 * m[i] + (1 - b1) * g
+                r -= lr * ((m[i] / bc1) / denom + wd * r)
+
+
+def ref_lamb_standalone(rs, gs_steps, lr, b1, b2, eps, wd, max_norm, adam_w=True):
+    """apex FusedLAMB: global-norm clipped gradient, Adam direction (+ decoupled or L2 decay),
+    per-tensor trust ratio."""
+    m = [torch.zeros_like(r) for r in rs]
+    v = [torch.zeros_like(r) for r in rs]
+    for step, gs in enumerate(gs_steps, 1):
+        gn = sum(float(g.double().pow(2).sum()) for g in gs) ** 0.5
+        clip = gn / max_norm if gn > max_norm else 1.0
+        for i, (r, g) in enumerate(zip(rs, gs)):
+            sg = g.double() / clip
+            if not adam_w:
+                sg = sg + wd * r
+            m[i] = b1 * m[i] + (1 - b1) * sg
+            v[i] = b2 * v[i] + (1 - b2) * sg * sg
+            u = (m[i] / (1 - b1 ** step)) / ((v[i] / (1 - b2 ** step)).sqrt() + eps)
+            if adam_w:
+                u = u + wd * r
+            a, b = float(r.norm()), float(u.norm())
+            r -= (lr * a / b if (a > 0 and b > 0) else lr) * u
+
+
+def _grads(ps, steps, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [[torch.randn(p.shape, generator=g) for p in ps] for _ in range(steps)]
+
+
+def novograd():
+    torch.manual_seed(1)
+    for kw in (dict(), dict(reg_inside_moment=True), dict(norm_type=0), dict(init_zero=True)):
+        ps = [torch.randn(5, 4, requires_grad=True), torch.randn(3, requires_grad=True)]
+        rs = [p.detach().clone().double() for p in ps]
+        opt = FusedNovoGrad(ps, lr=0.1, betas=(0.9, 0.98), eps=1e-8, weight_decay=0.01, **kw)
+        steps = _grads(ps, 3, 7)
+        for gs in steps:
+            for p, g in zip(ps, gs):
+                p.grad = g.clone()
+            opt.step()
+        ref_novograd(rs, steps, 0.1, 0.9, 0.98, 1e-8, 0.01, reg_inside=kw.get("reg_inside_moment", False),
+                     norm_type=kw.get("norm_type", 2), init_zero=kw.get("init_zero", False))
+        for p, r in zip(ps, rs):
+            assert torch.allclose(p.detach().double(), r, atol=1e-5), (kw, (p - r).abs().max())
     print("OK novograd", flush=True)
+
+
+def lamb_standalone():
+    torch.manual_seed(2)
+    for adam_w in (True, False):
+        ps = [torch.randn(6, 5, requires_grad=True), torch.randn(5, requires_grad=True)]
+        rs = [p.detach().clone().double() for p in ps]
+        opt = FusedLAMB(ps, lr=0.05, weight_decay=0.01, max_grad_norm=1.0, adam_w_mode=adam_w)
+        steps = _grads(ps, 3, 9)
+        for gs in steps:
+            for p, g in zip(ps, gs):
+                p.grad = g.clone()
+            opt.step()
+        ref_lamb_standalone(rs, steps, 0.05, 0.9, 0.999, 1e-6, 0.01, 1.0, adam_w)
+        for p, r in zip(ps, rs):
+            assert torch.allclose(p.detach().double(), r, atol=1e-5), (adam_w, (p - r).abs().max())
+    print("OK lamb-standalone", flush=True)
 
 
 if __name__ == "__main__":
     lamb()
     novograd()
+    lamb_standalone()
     smp.barrier()

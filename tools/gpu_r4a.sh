@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4, first GPU pass: kernel/optimizer/one-shot GPU tests of the in-tree build, then the
+# attention A/B against abtest/_C_base.so (round-3 build) and a short default bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/r4a
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_attention_gpu.py \
+  tests/test_dropout_gpu.py tests/test_optimizers_gpu.py tests/test_oneshot_gpu.py > gpurun_out/r4a/pytest.log 2>&1 \
+  || { tail -40 gpurun_out/r4a/pytest.log; exit 1; }
+tail -3 gpurun_out/r4a/pytest.log
+for i in 1 2; do
+  timeout -k 10 120 python tools/attn_time.py abtest/_C_base.so 2>&1 | grep -v "^\[\|amdgpu.ids" || exit 1
+  timeout -k 10 120 python tools/attn_time.py 2>&1 | grep -v "^\[\|amdgpu.ids" || exit 1
+done
+timeout -k 10 300 python bench.py --steps 6 --warmup 3 > gpurun_out/r4a/bench.log 2>&1 || { tail -20 gpurun_out/r4a/bench.log; exit 1; }
+tail -1 gpurun_out/r4a/bench.log
