@@ -154,6 +154,12 @@ def write_tunableop_results(path):
         f.write("\n".join(lines) + "\n")
 
 
+def p2p_selfcheck():
+    from smdistributed_modelparallel_amd.runtime.transport import SELFCHECK
+
+    return SELFCHECK["verdict"]
+
+
 def main():
     args = parse()
     import smdistributed_modelparallel_amd.torch as smp
@@ -163,6 +169,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", 1))
     resolve_layout(args, world)
+    # an unattended multi-GPU run must not hang silently: a step running longer than this
+    # dumps every thread's stack, ABORTs the peers and exits non-zero (backend/core.py
+    # watchdog); TunableOp tuning steps run for minutes, so they get a longer budget
+    os.environ.setdefault("SMP_STEP_TIMEOUT_S", "3600" if args.tunableop == "tune" else "600")
     cfg = {
         "pipeline_parallel_degree": args.pp,
         "tensor_parallel_degree": args.tp,
@@ -257,12 +267,21 @@ def main():
         if dist.is_initialized() and dist.get_world_size() > 1:
             dist.barrier()
 
+    from smdistributed_modelparallel_amd.parallel.comm_timer import timer as comm_timer
+
     sync()
+    comm_timer.reset()
+    comm_timer.enabled = True  # two HIP events around each communication wait (no sync)
     t0 = time.perf_counter()
     for i in range(args.steps):
         out = one(i)
     sync()
     dt = time.perf_counter() - t0
+    comm_timer.enabled = False
+    exposed = comm_timer.collect()
+    ex = torch.tensor([exposed["dp"], exposed["p2p"]], dtype=torch.float64, device=dev)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -304,6 +323,16 @@ def main():
                 "dropout": args.dropout,
                 "gemm_selection": "tunableop" if tmode != "off" else "heuristic",
             },
+            "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+            # world sizes of the process groups the backend actually formed (1: not created)
+            "groups": {name: (dist.get_world_size(g) if g is not None else 1)
+                       for name, g in (("world", smp.state.pgs.world), ("dp", smp.state.pgs.dp),
+                                       ("pp", smp.state.pgs.pp), ("tp", smp.state.pgs.tp))},
+            "p2p": {"mode": smp.state.transport.mode if args.pp > 1 else None,
+                    "ipc_selfcheck": p2p_selfcheck()},
+            # per-step compute-stream stall on communication (max over ranks): the DP bucket
+            # all-reduces left after backward, and pipeline activation / gradient pulls
+            "exposed_comm_ms": {"dp": round(float(ex[0]) / args.steps, 2), "p2p": round(float(ex[1]) / args.steps, 2)},
             "tokens_per_s": round(tokens_per_s, 1),
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),
             "final_loss": round(loss_val, 4),

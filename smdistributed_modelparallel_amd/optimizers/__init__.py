@@ -10,6 +10,7 @@ Wrapped in ``smp.DistributedOptimizer`` the model is instead updated per flat-bu
 import torch
 import torch.distributed as dist
 
+from .. import torch as _smp_torch  # noqa: F401  (the smp package first: it imports .optimizer itself)
 from ..ops import multi_tensor as mt
 from .optimizer import DistributedOptimizer  # noqa: F401
 

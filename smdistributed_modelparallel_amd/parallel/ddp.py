@@ -28,6 +28,7 @@ import torch.distributed as dist
 
 from ..backend.logger import get_logger
 from ..ops.linear import wgrad_sync
+from .comm_timer import timer as comm_timer
 
 logger = get_logger()
 
@@ -159,11 +160,12 @@ class BucketReducer:
             if not b.launched:
                 self._launch(b)
         self.next_launch = len(self.flat.buckets)
-        for b in self.flat.buckets:
-            if b.work is not None:
-                if hasattr(b.work, "wait"):
-                    b.work.wait()
-                b.work = None
+        with comm_timer.region("dp", self.flat.grad.device):
+            for b in self.flat.buckets:
+                if b.work is not None:
+                    if hasattr(b.work, "wait"):
+                        b.work.wait()
+                    b.work = None
 
     def shadow(self):
         """Joined rank (model.join): issue this reducer's bucket collectives in bucket order

@@ -330,12 +330,18 @@ class ModuleManager:
         """Partition metrics (reference `module_manager.py:1337-1392`): parameter bytes and the
         fraction of traced modules per pipeline device, and the forward communication volume
         (MB) -- traced input + output bytes of every module whose device differs from its
-        parent's, found by a walk of the module tree from the main module."""
+        parent's, found by a walk of the module tree from the main module.
+
+        Untraced runs (PP = 1, ``skip_tracing``, a partition file) count every module of the
+        model instead of the traced ones, so the fraction still reflects the placement (the
+        reference reports 0 there: its population is the trace)."""
         var_size = [0] * pp_size
         module_fraction = [0.0] * pp_size
         traced = [m for m in model.modules() if m in self._output_sizes]
+        if not traced:
+            traced = [m for m in model.modules() if (self.get_partition(m) if pp_size > 1 else 0) is not None]
         for m in traced:
-            dev = self.get_partition(m)
+            dev = self.get_partition(m) if pp_size > 1 else 0
             if dev is None:
                 continue
             module_fraction[dev] += 1

@@ -41,6 +41,7 @@ import torch.distributed as dist
 
 from ..backend.collectives import SERVER_CHANNEL, dumps, loads
 from ..backend.logger import get_logger
+from ..parallel.comm_timer import timer as comm_timer
 
 logger = get_logger()
 
@@ -123,15 +124,22 @@ def ipc_self_check(core, device, numel=1 << 18):
     return not flat, flat
 
 
+# verdict of the init-time IPC self-check: "passed", "failed -> <fallback>", or "not run"
+SELFCHECK = {"verdict": "not run", "failures": []}
+
+
 def resolve_mode(core, device, backend):
     """choose_mode + (for ``ipc`` with PP > 1) the init-time self-check and fallback."""
     mode = choose_mode(core, device, backend)
+    SELFCHECK.update(verdict="not run", failures=[])
     if mode != "ipc" or core.pp_size() == 1 or os.environ.get("SMP_P2P_SELFCHECK", "1") == "0":
         return mode
     ok, fails = ipc_self_check(core, device)
     if ok:
+        SELFCHECK["verdict"] = "passed"
         return mode
     fallback = "rccl" if backend == "nccl" else "host"
+    SELFCHECK.update(verdict=f"failed -> {fallback}", failures=fails[:8])
     if os.environ.get("SMP_P2P", "").lower() == "ipc" and not os.environ.get("SMP_P2P_SELFCHECK_FAIL"):
         from ..backend.exceptions import SMPRuntimeError
 
@@ -269,7 +277,8 @@ class PipelineTransport:
             with torch.cuda.stream(self._comm):
                 out = [self._materialize(src, m) for m in meta]
                 ev.record(self._comm)
-            compute.wait_event(ev)
+            with comm_timer.region("p2p", self.device):
+                compute.wait_event(ev)
             for t in out:
                 if t.is_cuda:
                     t.record_stream(compute)
@@ -295,7 +304,8 @@ class PipelineTransport:
         _, shape, dtype = m
         buf = torch.empty(shape, dtype=dtype, device=self.device)
         w = dist.irecv(buf, src, group=self.pgs.p2p[(src, self.rank)])
-        w.wait()  # stream-ordered: compute stream waits for the RCCL event
+        with comm_timer.region("p2p", self.device):
+            w.wait()  # stream-ordered: compute stream waits for the RCCL event
         self.bytes_recv += buf.numel() * buf.element_size()
         return buf
 

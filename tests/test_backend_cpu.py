@@ -512,3 +512,17 @@ def test_distributed_model_to_cuda_semantics(tmp_path):
     r = subprocess.run([sys.executable, "-c", _MOVES_CODE], cwd=tmp_path, env=env, capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 0 and "MOVES_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+def test_partition_metrics_without_trace():
+    """module_fraction for untraced runs (the bench printed 0.0 with every module on
+    device 0): the population falls back to every module of the model."""
+    import torch.nn as nn
+
+    from smdistributed_modelparallel_amd.runtime.module_manager import ModuleManager
+
+    mm = ModuleManager(None, lambda: 0)
+    net = nn.Sequential(nn.Linear(4, 4), nn.ReLU(), nn.Linear(4, 2))
+    var_size, frac, comm = mm.get_metrics(net, 1)
+    assert frac == [1.0] and comm == 0.0
+    assert var_size[0] == sum(p.numel() * p.element_size() for p in net.parameters())

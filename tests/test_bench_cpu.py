@@ -43,6 +43,20 @@ def test_bench_json_line(nproc):
     assert cfg["parallelism"] == f"pp1xtp1xdp{nproc}"
     # value is the whole-job aggregate: global batch x steps / max-over-ranks wall time
     assert abs(rec["value"] - cfg["global_batch"] / (rec["ms_per_step"] / 1000.0)) < 0.02 * rec["value"] + 1e-3
+    _check_audit_fields(rec, world=nproc, dp=nproc, pp=1)
+
+
+def _check_audit_fields(rec, world, dp, pp):
+    """the record says which backend and groups were formed, the pipeline transport
+    and its self-check verdict, and the exposed (non-overlapped) communication per step."""
+    assert rec["dist_backend"] == ("gloo" if world > 1 else rec["dist_backend"])
+    assert rec["groups"]["world"] == world and rec["groups"]["dp"] == dp and rec["groups"]["pp"] == pp
+    assert set(rec["p2p"]) == {"mode", "ipc_selfcheck"}
+    ex = rec["exposed_comm_ms"]
+    assert set(ex) == {"dp", "p2p"} and all(v >= 0.0 for v in ex.values())
+    if dp > 1:
+        assert ex["dp"] > 0.0  # gloo all-reduces block the host: some wait is always exposed
+    assert ex["dp"] + ex["p2p"] <= rec["ms_per_step"] * 1.05
 
 
 def test_bench_pp_layout_four_ranks():
@@ -57,6 +71,8 @@ def test_bench_pp_layout_four_ranks():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     rec = json.loads(lines[0])
+    _check_audit_fields(rec, world=4, dp=1, pp=4)
+    assert rec["p2p"]["mode"] is not None
     cfg = rec["config"]
     assert cfg["parallelism"] == "pp4xtp1xdp1" and cfg["layout"] == "pp" and cfg["pipeline"] == "interleaved"
     assert cfg["microbatches"] == 4 and cfg["global_batch"] == 4 and sum(cfg["layer_split"]) == 4
