@@ -38,11 +38,12 @@ def parse():
                     help="micro-batch size.  DP layout default 32 x 2048 tokens (GEMM M = 65536): amortises the "
                          "per-step optimizer / LM-head / transposition work and fills the chip with attention "
                          "blocks, ~190 GB of the 288 GB HBM3E (same-box A/B vs 16: +4.4 %% samples/s).  PP layout "
-                         "default 8: one stage's work (12 layers + head) on one MI355X runs 117 / 134 / 142 samples/s "
-                         "at mbs 4 / 8 / 16 (profiles/r3/pp_stage_mbs.md); 8 x 32 microbatches keeps the bubble at "
-                         "8.6 %% and the in-flight activations of pp + 2 microbatches well inside 288 GB")
+                         "default 16: one stage's work (12 layers + head) on one MI355X runs 117 / 134 / 142 samples/s "
+                         "at mbs 4 / 8 / 16 (profiles/r3/pp_stage_mbs.md), the fastest measured; 16 x 32 "
+                         "microbatches keeps the bubble at 8.6 %% and the in-flight activations of pp + 2 "
+                         "microbatches (~33 GB per 16-sample microbatch set) well inside 288 GB")
     ap.add_argument("--microbatches", type=int, default=None,
-                    help="DP default 1; PP default 32 (pipeline bubble (pp-1)/(m+pp-1) = 8.6 %% at PP=4; 8 x 32 = 256 "
+                    help="DP default 1; PP default 32 (pipeline bubble (pp-1)/(m+pp-1) = 8.6 %% at PP=4; 16 x 32 = 512 "
                          "samples per pipeline per step)")
     ap.add_argument("--pp", type=int, default=None)
     ap.add_argument("--tp", type=int, default=1)
@@ -73,7 +74,7 @@ def resolve_layout(args, world):
             layout = "pp"
     if layout == "pp":
         args.pp = args.pp or 4
-        args.mbs = args.mbs or 8
+        args.mbs = args.mbs or 16
         args.microbatches = args.microbatches or 32
     else:
         args.pp = args.pp or 1

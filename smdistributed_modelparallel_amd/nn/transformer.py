@@ -192,16 +192,17 @@ class _Dropout(nn.Module):
 
 def _all_ones(attention_mask):
     """An all-ones padding mask masks nothing: drop it (attention then runs the unmasked
-    kernels).  Decided once per mask tensor (one host sync, cached on the tensor), and only
-    outside pipelines, where a sync per microbatch would stall the schedule.
-    SMP_SKIP_ALL_ONES_MASK_CHECK=1 disables the check."""
+    kernels).  Decided once per mask tensor (one host sync, cached on the tensor).  Under
+    pipelines the decision comes with the microbatch slice (made for the whole batch on
+    pp_rank 0 before the split, `torch/step.py`); a mask without one is kept, since a sync per
+    microbatch would stall the schedule.  SMP_SKIP_ALL_ONES_MASK_CHECK=1 disables the check."""
     if os.environ.get("SMP_SKIP_ALL_ONES_MASK_CHECK", "0") == "1" or not torch.is_tensor(attention_mask):
-        return False
-    if state.initialized and state.core.pp_size() > 1:
         return False
     cached = getattr(attention_mask, "_smp_all_ones", None)
     if cached is not None and cached[0] == attention_mask._version:
         return cached[1]
+    if state.initialized and state.core.pp_size() > 1:
+        return False
     val = bool((attention_mask != 0).all())
     try:
         attention_mask._smp_all_ones = (attention_mask._version, val)

@@ -23,6 +23,39 @@ from .state_mod import state
 logger = get_logger()
 
 
+def _mask_candidates(obj, out):
+    if isinstance(obj, torch.Tensor):
+        if obj.dim() == 2 and obj.dtype in (torch.bool, torch.uint8, torch.int32, torch.int64) and obj.numel() > 0:
+            out.append(obj)
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            _mask_candidates(o, out)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            _mask_candidates(o, out)
+    return out
+
+
+def _decide_all_ones(args, kwargs):
+    """Pipelines: whether each 2-D integer / bool input (padding masks among them) is all
+    non-zero, decided ONCE per step on pp_rank 0 before the split -- one batched reduction and
+    one host read, cached on the tensor (by version) -- and inherited by every microbatch slice.
+    An all-ones padding mask is then dropped by the parent (`nn/transformer._all_ones`) before
+    the layers run, so no stage builds a key bias or runs the biased attention kernels; a
+    per-microbatch check would stall the schedule (reference decides its masks on the
+    leader as well, `server_queue.py:629-675`)."""
+    cands = [t for t in _mask_candidates((args, kwargs), [])
+             if getattr(t, "_smp_all_ones", (None,))[0] != t._version]
+    if not cands:
+        return
+    flags = torch.stack([(t != 0).all() for t in cands]).tolist()
+    for t, f in zip(cands, flags):
+        try:
+            t._smp_all_ones = (t._version, bool(f))
+        except (AttributeError, RuntimeError):  # pragma: no cover
+            pass
+
+
 class PTTensorSplitter(TensorSplitter):
     def is_tensor(self, x):
         return isinstance(x, torch.Tensor)
@@ -30,9 +63,18 @@ class PTTensorSplitter(TensorSplitter):
     def tensor_size(self, x, axis):
         return x.size(axis)
 
+    def split(self, args, kwargs, num_mb):
+        if state.initialized and state.core.pp_size() > 1 and os.environ.get("SMP_SKIP_ALL_ONES_MASK_CHECK") != "1":
+            _decide_all_ones(args, kwargs)
+        return super().split(args, kwargs, num_mb)
+
     def slice_tensor(self, x, num_mb, mb, axis):
         size = x.size(axis) // num_mb
-        return x.narrow(axis, mb * size, size)
+        out = x.narrow(axis, mb * size, size)
+        flag = getattr(x, "_smp_all_ones", None)
+        if flag is not None and flag[0] == x._version:
+            out._smp_all_ones = (out._version, flag[1])  # a slice of an all-ones tensor is all ones
+        return out
 
 
 class StepMemoryMetricsCollector:
