@@ -5,8 +5,7 @@
 namespace smpk {
 namespace attn {
 #define SMPK_DQ64_EXTERN(T, C, DR, BI)                                                 \
-  extern template void launch_dq<T, 64, C, DR, BI, true>(const AttnBwdParams&, unsigned, hipStream_t); \
-  extern template void launch_dq<T, 64, C, DR, BI, false>(const AttnBwdParams&, unsigned, hipStream_t);
+  extern template void launch_dq<T, 64, C, DR, BI>(const AttnBwdParams&, unsigned, hipStream_t);
 SMPK_ATTN_VARIANTS(SMPK_DQ64_EXTERN)
 }  // namespace attn
 SMPK_ATTN_HEAD_DIM(64)

@@ -7,8 +7,7 @@
 namespace smpk {
 namespace attn {
 #define SMPK_DQ64_INST(T, C, DR, BI)                                                   \
-  template void launch_dq<T, 64, C, DR, BI, true>(const AttnBwdParams&, unsigned, hipStream_t); \
-  template void launch_dq<T, 64, C, DR, BI, false>(const AttnBwdParams&, unsigned, hipStream_t);
+  template void launch_dq<T, 64, C, DR, BI>(const AttnBwdParams&, unsigned, hipStream_t);
 SMPK_ATTN_VARIANTS(SMPK_DQ64_INST)
 }  // namespace attn
 }  // namespace smpk

@@ -718,30 +718,6 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   if (hh == 0) p.lse[bh * p.sq + qrow] = (lt > 0.f) ? (m_i + log2f(lt)) / kLog2e : -INFINITY;
 }
 
-// ============================================================= delta = rowsum(dO * O)
-template <typename T>
-__global__ void __launch_bounds__(kThreads) attn_delta_kernel(AttnBwdParams p) {
-  // 16 lanes per (b, h, query) row, 8 elements per lane per step (16-byte loads)
-  const int sub = threadIdx.x & 15;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * 16 + (threadIdx.x >> 4);
-  const int64_t total = p.f.b * p.f.h * p.f.sq;
-  const bool valid = row < total;
-  float acc = 0.f;
-  if (valid) {
-    const int64_t q = row % p.f.sq, bh = row / p.f.sq, b = bh / p.f.h, h = bh % p.f.h;
-    const T* O = static_cast<const T*>(p.f.o) + b * p.f.o_sb + h * p.f.o_sh + q * p.f.o_ss;
-    const T* dO = static_cast<const T*>(p.dout) + b * p.do_sb + h * p.do_sh + q * p.do_ss;
-    for (int d = sub * 8; d < p.f.d; d += 128) {
-      Vec16<T> a = load16<T>(O + d), g = load16<T>(dO + d);
-#pragma unroll
-      for (int j = 0; j < Vec16<T>::N; ++j) acc += to_f32(a.v[j]) * to_f32(g.v[j]);
-    }
-  }
-#pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (valid && sub == 0) p.delta[row] = acc;
-}
-
 // ===================================================================== dK / dV
 // Block = 4 waves x 32 keys (key on the MFMA lane); Q/dO tiles of 64 queries, two 32-query
 // sub-steps.  S and dP accumulators start from the per-query row constants
@@ -1014,10 +990,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 // forward (edge masks only on edge tiles).  Accumulators start at zero (an inline-constant
 // operand of the first MFMA) and the row constants enter the exponent's fma / the dS
 // subtraction instead of 64 register moves per tile.
-// FD (fused delta): the block computes delta = rowsum(dO o O) of its own query rows from the dO
+// Fused delta: the block computes delta = rowsum(dO o O) of its own query rows from the dO
 // fragments it holds anyway plus one read of the O rows, and publishes it for the dK/dV kernel
 // launched after it -- no separate delta pass over O and dO.
-template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool FD = false>
+template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS>
 __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(AttnBwdParams P) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr int NSPLIT = DkdvSplit<D>::v, DO = D / NSPLIT;  // dQ columns per block
@@ -1067,7 +1043,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   const float inv_scale = 1.f / p.scale;
   const float lse2 = lse * kLog2e;  // p = exp2(S sl2 - lse2)
   float dl;
-  if constexpr (FD) {
+  {
     // lane (r, hh) holds elements [16 t + 8 hh, +8) of dO row qrow: the matching O elements,
     // a lane-local partial dot product, and the other half-row from lane ^ 32
     const uint16_t* Orow = static_cast<const uint16_t*>(p.o) + b * p.o_sb + h * p.o_sh;
@@ -1082,8 +1058,6 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     }
     dl = pair_sum32(part);
     if (col0 == 0 && hh == 0 && qrow < sq) P.delta[bh * p.sq + qrow] = dl;
-  } else {
-    dl = qrow < sq ? P.delta[bh * p.sq + qrow] : 0.f;
   }
   const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
   const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
@@ -1225,43 +1199,23 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
 
 // ------------------------------------------------------------------ launchers
 
-// SMP_ATTN_DMA=0 keeps the register-staged K/V path for D = 64 / 128
-inline bool attn_dma_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("SMP_ATTN_DMA");
-    return e == nullptr || e[0] != '0';
-  }();
-  return v;
-}
-
 template <typename T, int D, bool C, bool DR, bool BI>
 int launch_fwd_v(const AttnParams& p, hipStream_t s) {
   const unsigned grid = static_cast<unsigned>(((p.sq + 127) / 128) * p.b * p.h);
-  if constexpr ((D == 64 || D == 128) && !BI) {
-    if (attn_dma_enabled()) {
-      attn_fwd_kernel<T, D, C, DR, BI, true><<<grid, kThreads, 0, s>>>(p);
-      return static_cast<int>(hipGetLastError());
-    }
+  if constexpr ((D == 64 || D == 128) && !BI) {  // K/V tiles by LDS-DMA
+    attn_fwd_kernel<T, D, C, DR, BI, true><<<grid, kThreads, 0, s>>>(p);
+    return static_cast<int>(hipGetLastError());
   }
   attn_fwd_kernel<T, D, C, DR, BI><<<grid, kThreads, 0, s>>>(p);
   return static_cast<int>(hipGetLastError());
 }
 
-// SMP_ATTN_FUSED_DELTA=0: separate delta kernel, then dK/dV, then dQ (A/B switch)
-inline bool attn_fused_delta() {
-  static const bool v = [] {
-    const char* e = getenv("SMP_ATTN_FUSED_DELTA");
-    return e == nullptr || e[0] != '0';
-  }();
-  return v;
-}
-
 // dQ launch as its own function template: a head dim can instantiate it in a separate
 // translation unit built with other flags (D = 64: attention_d64_dq.hip, no SLP vectorisation
 // -- packed fp32 VALU beside the MFMAs costs the dQ kernel 4.5 %, profiles/r3/s3_rehearsal.md)
-template <typename T, int D, bool C, bool DR, bool BI, bool FD>
+template <typename T, int D, bool C, bool DR, bool BI>
 void launch_dq(const AttnBwdParams& p, unsigned g, hipStream_t s) {
-  attn_bwd_dq_kernel<T, D, C, DR, BI, FD><<<g, kThreads, 0, s>>>(p);
+  attn_bwd_dq_kernel<T, D, C, DR, BI><<<g, kThreads, 0, s>>>(p);
 }
 
 // X(T, C, DR, BI) for every dtype x variant of one head dim
@@ -1277,16 +1231,10 @@ template <typename T, int D, bool C, bool DR, bool BI>
 int launch_bwd_v(const AttnBwdParams& p, hipStream_t s) {
   const unsigned gk = static_cast<unsigned>(((p.f.sk + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
   const unsigned gq = static_cast<unsigned>(((p.f.sq + 127) / 128) * p.f.b * p.f.h * DkdvSplit<D>::v);
-  if (attn_fused_delta()) {
-    // dQ first: it writes delta for the dK/dV kernel (same stream)
-    launch_dq<T, D, C, DR, BI, true>(p, gq, s);
-    attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
-    return static_cast<int>(hipGetLastError());
-  }
-  const int64_t rows = p.f.b * p.f.h * p.f.sq;
-  attn_delta_kernel<T><<<static_cast<unsigned>((rows + 15) / 16), kThreads, 0, s>>>(p);
+  // dQ first: it computes delta = rowsum(dO o O) for its rows and writes it for the dK/dV
+  // kernel (same stream)
+  launch_dq<T, D, C, DR, BI>(p, gq, s);
   attn_bwd_dkdv_kernel<T, D, C, DR, BI><<<gk, kThreads, 0, s>>>(p);
-  launch_dq<T, D, C, DR, BI, false>(p, gq, s);
   return static_cast<int>(hipGetLastError());
 }
 

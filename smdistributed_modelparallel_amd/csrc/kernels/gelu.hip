@@ -297,81 +297,6 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_kernel(const T* __res
   }
 }
 
-// Forward over the column walker: bias in registers, U rows of 16-byte loads in flight.
-template <typename T, int ACT>
-__global__ void __launch_bounds__(256) bias_gelu_fwd_walk(const T* __restrict__ x, const T* __restrict__ bias,
-                                                          T* __restrict__ y, int64_t rows, int64_t cols,
-                                                          int64_t rows_per_part, int cvb, int rl) {
-  constexpr int N = Vec16<T>::N;
-  const int cvl = threadIdx.x % cvb, r_l = threadIdx.x / cvb;
-  const int64_t c = (static_cast<int64_t>(blockIdx.x) * cvb + cvl) * N;
-  if (r_l >= rl || c >= cols) return;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.y) * rows_per_part;
-  const int64_t r1 = r0 + rows_per_part < rows ? r0 + rows_per_part : rows;
-  float bb[N];
-  if (bias) {
-    Vec16<T> bv = load16(bias + c);
-#pragma unroll
-    for (int j = 0; j < N; ++j) bb[j] = to_f32(bv.v[j]);
-  } else {
-#pragma unroll
-    for (int j = 0; j < N; ++j) bb[j] = 0.f;
-  }
-  int64_t r = r0 + r_l;
-  for (; r + (kUnroll - 1) * rl < r1; r += kUnroll * rl) {
-    Vec16<T> a[kUnroll];
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = load16(x + (r + u * rl) * cols + c);
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      Vec16<T> o;
-#pragma unroll
-      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a[u].v[j]) + bb[j]));
-      store16(y + (r + u * rl) * cols + c, o);
-    }
-  }
-  for (; r < r1; r += rl) {
-    Vec16<T> a = load16(x + r * cols + c);
-    Vec16<T> o;
-#pragma unroll
-    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a.v[j]) + bb[j]));
-    store16(y + r * cols + c, o);
-  }
-}
-
-// ---------------------------------------------------------------- flat streaming
-// Grid-stride over 16-byte vectors in memory order (the access pattern of a plain copy:
-// every wave-instruction reads 1 KB that directly follows the previous one), U vectors in
-// flight per lane; the bias vector of each column comes from L1/L2 (a 12.8 KB row).
-template <typename T, int ACT, int U>
-__global__ void __launch_bounds__(256) bias_gelu_fwd_flat(const T* __restrict__ x, const T* __restrict__ bias,
-                                                          T* __restrict__ y, int64_t nvec, int cv) {
-  constexpr int N = Vec16<T>::N;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-  int64_t v = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
-  for (; v + (U - 1) * stride < nvec; v += U * stride) {
-    Vec16<T> a[U], bv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) a[u] = load16(x + (v + u * stride) * N);
-#pragma unroll
-    for (int u = 0; u < U; ++u) bv[u] = load16(bias + static_cast<int>((v + u * stride) % cv) * N);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      Vec16<T> o;
-#pragma unroll
-      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a[u].v[j]) + to_f32(bv[u].v[j])));
-      store16(y + (v + u * stride) * N, o);
-    }
-  }
-  for (; v < nvec; v += stride) {
-    const Vec16<T> a = load16(x + v * N), bv = load16(bias + static_cast<int>(v % cv) * N);
-    Vec16<T> o;
-#pragma unroll
-    for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a.v[j]) + to_f32(bv.v[j])));
-    store16(y + v * N, o);
-  }
-}
-
 // ---------------------------------------------------------------- one-pass streaming
 // One 16-byte vector per lane, one pass (grid = vectors / 256, no grid-stride loop): each
 // block streams 4 KB of consecutive memory once.  tools/membw/stream_variants.hip on MI355X
@@ -404,12 +329,6 @@ __global__ void __launch_bounds__(256) bias_gelu_once(const T* __restrict__ dy, 
   store16(y + static_cast<int64_t>(v) * N, o);
 }
 
-// SMP_GELU_ONCE=0 restores the grid-stride kernels (forward: flat, backward: elementwise)
-inline bool gelu_once_enabled() {
-  const char* e = getenv("SMP_GELU_ONCE");
-  return e == nullptr || e[0] != '0';
-}
-
 template <typename T, bool BWD>
 void launch_once(const void* dy, const void* x, const void* bias, void* y, int64_t nvec, int64_t cv, bool exact,
                  hipStream_t s) {
@@ -423,198 +342,6 @@ void launch_once(const void* dy, const void* x, const void* bias, void* y, int64
                                                 static_cast<const T*>(bias), static_cast<T*>(y),
                                                 static_cast<uint32_t>(nvec), static_cast<uint32_t>(cv));
 }
-
-// Previous forward default (tools/membw_probe.py, MI355X, [65536, 6400] bf16: 341 us = 4.9 TB/s
-// vs 415 us for the column walker); SMP_GELU_FLAT=0 restores the walker.
-inline bool gelu_flat_enabled() {
-  const char* e = getenv("SMP_GELU_FLAT");
-  return e == nullptr || e[0] != '0';
-}
-
-// ---------------------------------------------------------------- row streaming
-// Alternative layout for rows of <= 1024 16-byte vectors (<= 8192 bf16): a block owns a
-// contiguous range of whole rows and its 256 lanes sweep each row in order (lane t takes
-// column vectors t, t + 256, ..., VPL of them), two rows in flight.  Every wave-instruction
-// reads 1 KB of one row and a block streams one contiguous region, so HBM sees long
-// sequential runs instead of the column walker's 800-byte pieces of rows 64 KB apart;
-// the bias (and, backward, the dbias accumulators) stay in registers because a lane's
-// columns never change.  Backward writes one fp32 partial row per block, no LDS.
-template <typename T, int ACT, int VPL>
-__global__ void __launch_bounds__(256) bias_gelu_fwd_rows(const T* __restrict__ x, const T* __restrict__ bias,
-                                                          T* __restrict__ y, int64_t rows, int cv,
-                                                          int64_t rows_per_block) {
-  constexpr int N = Vec16<T>::N;
-  const int t = threadIdx.x;
-  const int64_t cols = static_cast<int64_t>(cv) * N;
-  float bb[VPL][N];
-  bool on[VPL];
-#pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    on[k] = t + k * 256 < cv;
-    Vec16<T> bv;
-    bv.raw = make_uint4(0, 0, 0, 0);
-    if (bias && on[k]) bv = load16(bias + (t + k * 256) * N);
-#pragma unroll
-    for (int j = 0; j < N; ++j) bb[k][j] = to_f32(bv.v[j]);
-  }
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  int64_t r = r0;
-  for (; r + 1 < r1; r += 2) {
-    Vec16<T> a[2][VPL];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int k = 0; k < VPL; ++k)
-        if (on[k]) a[q][k] = load16(x + (r + q) * cols + (t + k * 256) * N);
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int k = 0; k < VPL; ++k)
-        if (on[k]) {
-          Vec16<T> o;
-#pragma unroll
-          for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a[q][k].v[j]) + bb[k][j]));
-          store16(y + (r + q) * cols + (t + k * 256) * N, o);
-        }
-  }
-  if (r < r1)
-#pragma unroll
-    for (int k = 0; k < VPL; ++k)
-      if (on[k]) {
-        Vec16<T> a = load16(x + r * cols + (t + k * 256) * N);
-        Vec16<T> o;
-#pragma unroll
-        for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(act_fwd<ACT>(to_f32(a.v[j]) + bb[k][j]));
-        store16(y + r * cols + (t + k * 256) * N, o);
-      }
-}
-
-template <typename T, int ACT, int VPL>
-__global__ void __launch_bounds__(256) bias_gelu_bwd_dbias_rows(const T* __restrict__ dy, const T* __restrict__ x,
-                                                                const T* __restrict__ bias, T* __restrict__ dx,
-                                                                float* __restrict__ part, int64_t rows, int cv,
-                                                                int64_t rows_per_block) {
-  constexpr int N = Vec16<T>::N;
-  const int t = threadIdx.x;
-  const int64_t cols = static_cast<int64_t>(cv) * N;
-  float bb[VPL][N], acc[VPL][N];
-  bool on[VPL];
-#pragma unroll
-  for (int k = 0; k < VPL; ++k) {
-    on[k] = t + k * 256 < cv;
-    Vec16<T> bv;
-    bv.raw = make_uint4(0, 0, 0, 0);
-    if (on[k]) bv = load16(bias + (t + k * 256) * N);
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      bb[k][j] = to_f32(bv.v[j]);
-      acc[k][j] = 0.f;
-    }
-  }
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
-  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  int64_t r = r0;
-  for (; r + 1 < r1; r += 2) {
-    Vec16<T> a[2][VPL], d[2][VPL];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int k = 0; k < VPL; ++k)
-        if (on[k]) {
-          a[q][k] = load16(x + (r + q) * cols + (t + k * 256) * N);
-          d[q][k] = load16(dy + (r + q) * cols + (t + k * 256) * N);
-        }
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int k = 0; k < VPL; ++k)
-        if (on[k]) {
-          Vec16<T> o;
-#pragma unroll
-          for (int j = 0; j < N; ++j) {
-            o.v[j] = from_f32<T>(to_f32(d[q][k].v[j]) * act_grad<ACT>(to_f32(a[q][k].v[j]) + bb[k][j]));
-            acc[k][j] += to_f32(o.v[j]);
-          }
-          store16(dx + (r + q) * cols + (t + k * 256) * N, o);
-        }
-  }
-  if (r < r1)
-#pragma unroll
-    for (int k = 0; k < VPL; ++k)
-      if (on[k]) {
-        Vec16<T> a = load16(x + r * cols + (t + k * 256) * N);
-        Vec16<T> d = load16(dy + r * cols + (t + k * 256) * N);
-        Vec16<T> o;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          o.v[j] = from_f32<T>(to_f32(d.v[j]) * act_grad<ACT>(to_f32(a.v[j]) + bb[k][j]));
-          acc[k][j] += to_f32(o.v[j]);
-        }
-        store16(dx + r * cols + (t + k * 256) * N, o);
-      }
-  float* prow = part + static_cast<int64_t>(blockIdx.x) * cols;
-#pragma unroll
-  for (int k = 0; k < VPL; ++k)
-    if (on[k]) {
-      float4* p4 = reinterpret_cast<float4*>(prow + (t + k * 256) * N);
-#pragma unroll
-      for (int j = 0; j < N / 4; ++j)
-        p4[j] = make_float4(acc[k][4 * j], acc[k][4 * j + 1], acc[k][4 * j + 2], acc[k][4 * j + 3]);
-    }
-}
-
-// Opt-in (SMP_GELU_ROWS=1).  Measured on MI355X at T = 65536 (tools/gelu_ab.py,
-// profiles/r1_gelu_variants.md): forward 388 vs 414 us at 4h = 6400 but the fused backward
-// 684 vs 601 us, and the GPT-2 XL step 0.5 % slower, so the column walker stays the default.
-inline bool gelu_rows_enabled() {
-  const char* e = getenv("SMP_GELU_ROWS");
-  return e && e[0] == '1';
-}
-
-constexpr int kRowsMaxVpl = 4;
-constexpr int64_t kRowsBwdParts = 1024;
-
-// Row-streaming path applies: vectorisable row of <= 1024 vectors, enough rows to fill the chip.
-template <typename T>
-inline int rows_vpl(int64_t rows, int64_t cols) {
-  constexpr int N = Vec16<T>::N;
-  if (!gelu_rows_enabled() || cols % N != 0 || rows < 2048) return 0;
-  const int64_t cv = cols / N;
-  const int64_t vpl = (cv + 255) / 256;
-  return vpl <= kRowsMaxVpl ? static_cast<int>(vpl) : 0;
-}
-
-template <typename T, int ACT>
-void launch_fwd_rows(int vpl, const T* x, const T* bias, T* y, int64_t rows, int cv, hipStream_t s) {
-  int64_t rpb = (rows + 2047) / 2048;  // ~2048 blocks: 8 per CU
-  if (rpb < 2) rpb = 2;
-  const unsigned g = static_cast<unsigned>((rows + rpb - 1) / rpb);
-  switch (vpl) {
-    case 1: bias_gelu_fwd_rows<T, ACT, 1><<<g, 256, 0, s>>>(x, bias, y, rows, cv, rpb); break;
-    case 2: bias_gelu_fwd_rows<T, ACT, 2><<<g, 256, 0, s>>>(x, bias, y, rows, cv, rpb); break;
-    case 3: bias_gelu_fwd_rows<T, ACT, 3><<<g, 256, 0, s>>>(x, bias, y, rows, cv, rpb); break;
-    default: bias_gelu_fwd_rows<T, ACT, 4><<<g, 256, 0, s>>>(x, bias, y, rows, cv, rpb); break;
-  }
-}
-
-template <typename T, int ACT>
-int launch_bwd_rows(int vpl, const T* dy, const T* x, const T* bias, T* dx, float* part, int64_t rows, int cv,
-                    hipStream_t s) {
-  int64_t parts = rows / 16 < kRowsBwdParts ? rows / 16 : kRowsBwdParts;
-  if (parts < 1) parts = 1;
-  const int64_t rpb = (rows + parts - 1) / parts;
-  parts = (rows + rpb - 1) / rpb;
-  const unsigned g = static_cast<unsigned>(parts);
-  switch (vpl) {
-    case 1: bias_gelu_bwd_dbias_rows<T, ACT, 1><<<g, 256, 0, s>>>(dy, x, bias, dx, part, rows, cv, rpb); break;
-    case 2: bias_gelu_bwd_dbias_rows<T, ACT, 2><<<g, 256, 0, s>>>(dy, x, bias, dx, part, rows, cv, rpb); break;
-    case 3: bias_gelu_bwd_dbias_rows<T, ACT, 3><<<g, 256, 0, s>>>(dy, x, bias, dx, part, rows, cv, rpb); break;
-    default: bias_gelu_bwd_dbias_rows<T, ACT, 4><<<g, 256, 0, s>>>(dy, x, bias, dx, part, rows, cv, rpb); break;
-  }
-  return static_cast<int>(parts);
-}
-
 // [parts, cols] fp32 -> [cols] in two deterministic stages (slices of parts, then slices).
 __global__ void __launch_bounds__(256) parts_reduce_stage1(const float* __restrict__ part, float* __restrict__ out,
                                                            int parts, int64_t cols, int slices) {
@@ -679,42 +406,8 @@ int bias_gelu_fwd(int dt, const void* x, const void* bias, void* y, int64_t rows
     constexpr int N = Vec16<T>::N;
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
                                           reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
-    const int vpl = vec ? rows_vpl<T>(rows, cols) : 0;
-    if (vec && total / N < (int64_t{1} << 31) && gelu_once_enabled()) {
+    if (vec && total / N < (int64_t{1} << 31)) {
       launch_once<T, false>(nullptr, x, bias, y, total / N, cols / N, exact, s);
-    } else if (vec && bias != nullptr && gelu_flat_enabled()) {
-      const int64_t nvec = total / N;
-      int64_t grid = nvec / (256 * 4);
-      if (grid > 2048) grid = 2048;
-      if (grid < 1) grid = 1;
-      if (exact)
-        bias_gelu_fwd_flat<T, 1, 4><<<static_cast<unsigned>(grid), 256, 0, s>>>(
-            static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), nvec, static_cast<int>(cols / N));
-      else
-        bias_gelu_fwd_flat<T, 0, 4><<<static_cast<unsigned>(grid), 256, 0, s>>>(
-            static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), nvec, static_cast<int>(cols / N));
-    } else if (vpl) {
-      if (exact)
-        launch_fwd_rows<T, 1>(vpl, static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows,
-                              static_cast<int>(cols / N), s);
-      else
-        launch_fwd_rows<T, 0>(vpl, static_cast<const T*>(x), static_cast<const T*>(bias), static_cast<T*>(y), rows,
-                              static_cast<int>(cols / N), s);
-    } else if (vec) {
-      const ColWalk w = col_walk(cols / N);
-      // ~2048+ blocks, >= 4 x unroll rows per lane
-      int64_t parts = (2048 + w.groups - 1) / w.groups;
-      const int64_t max_parts = rows / (static_cast<int64_t>(w.rl) * kUnroll);
-      if (parts > max_parts) parts = max_parts;
-      if (parts < 1) parts = 1;
-      const int64_t rpp = (rows + parts - 1) / parts;
-      dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
-      if (exact)
-        bias_gelu_fwd_walk<T, 1><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
-                                                   static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
-      else
-        bias_gelu_fwd_walk<T, 0><<<g, 256, 0, s>>>(static_cast<const T*>(x), static_cast<const T*>(bias),
-                                                   static_cast<T*>(y), rows, cols, rpp, w.cvb, w.rl);
     } else {
       if (exact)
         bias_gelu_fwd_kernel<T, false, 1><<<elt_grid(total, 1), 256, 0, s>>>(
@@ -736,7 +429,7 @@ int bias_gelu_bwd(int dt, const void* dy, const void* x, const void* bias, void*
     const bool vec = (cols % N == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                                           reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) &
                                          15) == 0;
-    if (vec && total / N < (int64_t{1} << 31) && gelu_once_enabled())
+    if (vec && total / N < (int64_t{1} << 31))
       launch_once<T, true>(dy, x, bias, dx, total / N, cols / N, exact, s);
     else if (vec && exact)
       launch_gelu_bwd<T, true, 1>(dy, x, bias, dx, rows, cols, s);
@@ -779,13 +472,9 @@ int col_sum(int dt, const void* x, void* out, float* workspace, int64_t rows, in
   return static_cast<int>(hipGetLastError());
 }
 
-// Workspace rows (partials) bias_gelu_bwd_dbias needs: the row-streaming path's block count
-// (<= 1024) or col_sum_parts; the caller adds 32 rows for the second reduction stage.
-int gelu_dbias_parts(int64_t rows) {
-  const int64_t p = rows / 16 < kRowsBwdParts ? rows / 16 : kRowsBwdParts;
-  const int64_t c = col_sum_parts(rows);
-  return static_cast<int>(p > c ? p : c);
-}
+// Workspace rows (partials) bias_gelu_bwd_dbias needs (col_sum_parts); the caller adds 32
+// rows for the second reduction stage.
+int gelu_dbias_parts(int64_t rows) { return col_sum_parts(rows); }
 
 // dx = dy * gelu'(x + bias) and dbias = colsum(dx) in one pass over dy/x.
 // Returns -2 when the shape/alignment needs the unfused path.  workspace as col_sum.
@@ -801,18 +490,6 @@ int bias_gelu_bwd_dbias(int dt, const void* dy, const void* x, const void* bias,
                      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                        reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(bias)) & 15) == 0;
     if (!vec) return -2;
-    if (const int vpl = rows_vpl<T>(rows, cols)) {
-      const int rparts =
-          exact ? launch_bwd_rows<T, 1>(vpl, static_cast<const T*>(dy), static_cast<const T*>(x),
-                                        static_cast<const T*>(bias), static_cast<T*>(dx), workspace, rows,
-                                        static_cast<int>(cols / N), s)
-                : launch_bwd_rows<T, 0>(vpl, static_cast<const T*>(dy), static_cast<const T*>(x),
-                                        static_cast<const T*>(bias), static_cast<T*>(dx), workspace, rows,
-                                        static_cast<int>(cols / N), s);
-      reduce_parts<T>(workspace, rparts, cols, workspace + static_cast<int64_t>(rparts) * cols,
-                      static_cast<T*>(dbias), s, accumulate);
-      return static_cast<int>(hipGetLastError());
-    }
     const ColWalk w = col_walk(cols / N);
     dim3 g(static_cast<unsigned>(w.groups), static_cast<unsigned>(parts));
     if (exact)

@@ -547,20 +547,13 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
 
 // Number of partial rows the backward will produce for (rows, cols): callers size
 // dw_part/db_part as [parts, cols] fp32.
-// SMP_LN_BWD_PARTS caps the partial rows (= backward workgroups) of the register paths; more
-// workgroups keep more rows in flight per CU (the block-per-rows kernel streams its rows one
-// at a time behind a barrier) at the price of a larger dgamma/dbeta partial reduction.
-// Default 1024: in the GPT-2 XL step's kernel trace the block-per-rows kernel takes 176 us at
-// 1024 partial rows and 191 us at 1792 (bench-level A/B of 1024 / 1792 / 3584 was within the
-// box's +-1 % noise).
-static inline int64_t ln_bwd_parts_cap() {
-  static const int64_t v = [] {
-    const char* e = getenv("SMP_LN_BWD_PARTS");
-    const long p = e != nullptr ? atol(e) : 1024;
-    return static_cast<int64_t>(p >= 64 && p <= 65536 ? p : 1024);
-  }();
-  return v;
-}
+// Cap on the partial rows (= backward workgroups) of the register paths; more workgroups keep
+// more rows in flight per CU (the block-per-rows kernel streams its rows one at a time behind a
+// barrier) at the price of a larger dgamma/dbeta partial reduction.  1024: in the GPT-2 XL
+// step's kernel trace the block-per-rows kernel takes 176 us at 1024 partial rows and 191 us at
+// 1792 (bench-level A/B of 1024 / 1792 / 3584 was within the box's +-1 % noise).
+constexpr int64_t kLnBwdPartsCap = 1024;
+static inline int64_t ln_bwd_parts_cap() { return kLnBwdPartsCap; }
 
 static inline int ln_bwd_parts(int64_t rows, int64_t cols, bool reg_path) {
   if (!reg_path) return static_cast<int>(rows);

@@ -8,67 +8,44 @@
 // forward GEMMs of the same size: its row-major-operand kernels transpose through
 // registers, and 256 x 256 output tiles give 49-175 workgroups for 256 CUs.
 //
-// Design:
-//  * operands are staged row-major exactly as they sit in HBM (512-B rows, fully
-//    coalesced 16-B loads, no transpose kernels) and the MFMA fragments -- which need 8
-//    consecutive reduction elements per lane -- come from ds_read_b64_tr_b16, the gfx950
-//    LDS transpose read;
-//  * v_mfma_f32_32x32x16_bf16 (f16), 256 threads = 4 waves in 2 x 2, each wave owns a
-//    128 x 128 output block = 16 accumulator tiles (256 fp32 AGPRs);
-//  * 64-token tiles, register-staged (the next tile's global loads are issued before the
-//    current tile's 64 MFMAs per wave), one 64 KB LDS buffer with XOR-swizzled 16-B
-//    chunks (conflict-free transposed reads); staging registers are native vectors (HIP's
-//    uint4 class left them in scratch) and loads are unpredicated (edge chunks re-read a
-//    valid chunk) so no vmcnt(0) lands before the MFMAs;
-//  * split-K over tokens: the split count is chosen on the host so that the grid fills the
-//    256 CUs in whole waves of workgroups (tile count x splits / 256 close to an integer);
-//    each split writes an fp32 partial tile and a vectorised reduction adds the partials
-//    into the gradient (beta = 1: the gradient buffer accumulates across microbatches, no
-//    temporary dW and no separate "grad += dW" pass);
+// Design (one kernel, wgrad_glds16_kernel):
+//  * operands are staged row-major exactly as they sit in HBM (512-B rows, fully coalesced)
+//    by LDS-DMA (global_load_lds from inline asm, so hipcc does not drain the prefetch before
+//    every ds_read) into a two-stage ring of 64-token tiles, one barrier per tile; the XOR
+//    swizzle of the 16-B chunks moves to the source address (conflict-free transposed reads);
+//  * the MFMA fragments -- 8 consecutive reduction elements per lane -- come from
+//    ds_read_b64_tr_b16, the gfx950 LDS transpose read;
+//  * v_mfma_f32_16x16x32_bf16 (f16), 512 threads = 8 waves (2 per SIMD) in 2 x 4, each wave
+//    owns a 128 x 64 block of the 256 x 256 output tile (32 accumulator tiles);
+//  * split-K over tokens: the split count comes from the host (a fixed per-shape table in
+//    ops/linear.py, or the occupancy model wgrad_splits); each split writes an fp32 partial
+//    tile and a vectorised reduction adds the partials into the gradient (beta = 1: the
+//    gradient buffer accumulates across microbatches, no temporary dW);
 //  * workgroups are dealt to XCDs in contiguous runs of (split, n-tile) so that the
-//    workgroups sharing an A strip share one XCD's L2.
+//    workgroups sharing an A strip share one XCD's L2;
+//  * optional bias gradient (sum over tokens of dY) from the same staged dY tiles.
 //
-// Status (MI355X, GPT-2 XL shapes, tools/wgrad_bench.py, profiles/r2/wgrad_kernel.md): the
-// register-staged version ran 630-775 TFLOP/s; the LDS-DMA version (wgrad_glds_kernel:
-// global_load_lds from inline asm so hipcc does not drain the prefetch before every ds_read,
-// two 64 KB stages, one barrier per tile, bijective XCD mapping) 750-900 TFLOP/s against
-// hipBLASLt's 700-1030.  ops/linear.py times both per shape on first use and keeps the faster
-// (in the GPT-2 XL step: the kernel wins the 1600 x 1600 weight gradient).  A stream-K
-// schedule (one persistent workgroup per CU) was slower: workgroups sharing a tile read
-// disjoint token ranges, so concurrent workgroups no longer share A / B strips in L2.
+// Measured and removed (A/B records in profiles/r2/wgrad_kernel.md, profiles/r3/wgrad_variants.md):
+// a register-staged 32x32x16 kernel (630-775 TFLOP/s), the 32x32x16 LDS-DMA kernel with 4 or 8
+// waves and 2-5 stages (750-900), a phased ping-pong 8-wave variant, DMA issue spread over the
+// k-steps (no gain), and a stream-K schedule (10-35 % slower: workgroups sharing a tile then
+// read disjoint token ranges and stop sharing A / B strips in L2).
 #include "common.h"
 #include "kernels.h"
 
 namespace smpk {
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 // native 16-B vector (HIP's uint4 is a class wrapper that SROA leaves in scratch here)
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-template <typename T>
-struct WMF;
-template <>
-struct WMF<bf16> {
-  typedef __bf16 e8 __attribute__((ext_vector_type(8)));
-  static __device__ __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <>
-struct WMF<f16> {
-  typedef _Float16 e8 __attribute__((ext_vector_type(8)));
-  static __device__ __forceinline__ f32x16 mma(e8 a, e8 b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
-};
-
-constexpr int kT = 256;     // threads
 constexpr int TM = 256;     // output tile rows (N)
 constexpr int TN = 256;     // output tile cols (K)
 constexpr int TK = 64;      // tokens per staged tile
+constexpr int kTK = TK;     // tokens per LDS stage of the kernel
+constexpr int kNS = 2;      // LDS stages (2 x 64 KB operand tiles + 16 KB column sums)
 constexpr int RW = 256;     // LDS row width (elements) of both staged tiles
 constexpr int CH = RW / 8;  // 16-B chunks per row
 
@@ -77,35 +54,6 @@ constexpr int CH = RW / 8;  // 16-B chunks per row
 __device__ __forceinline__ int swz(int row, int chunk) {
   const int g = ((row & 3) << 2) | ((row >> 2) & 3);
   return row * RW + ((chunk ^ g) << 3);
-}
-
-// Staging of one operand tile (TK rows x 256 columns, 8 x 16 B per thread): thread t owns
-// chunk t % 32 of rows t / 32 + 8 i.  Chunks past vc re-read the last valid chunk: those
-// columns only feed output rows / columns beyond the matrix, which are never written -- so
-// the loads are unconditional and stay in flight across the MFMA work (a predicated load
-// whose zero-fill shares the destination register forces a vmcnt(0) before it).
-constexpr int NR = TK * CH / kT;  // 8 registers per operand
-
-__device__ __forceinline__ void stage_load(u32x4 (&v)[NR], const uint16_t* src, int64_t ld, int vc) {
-  const int r0 = threadIdx.x / CH, c0 = threadIdx.x % CH;
-  const int c = c0 < vc ? c0 : vc - 1;
-  const uint16_t* p = src + static_cast<int64_t>(r0) * ld + c * 8;
-#pragma unroll
-  for (int i = 0; i < NR; ++i) v[i] = *reinterpret_cast<const u32x4*>(p + static_cast<int64_t>(8 * i) * ld);
-}
-
-// rows r0 + 8 i: row bits 0-3 alternate between r0 and r0 + 8, so two swizzled bases
-__device__ __forceinline__ void stage_store(const u32x4 (&v)[NR], uint16_t* lds, int lo0, int lo1) {
-#pragma unroll
-  for (int i = 0; i < NR; ++i) *reinterpret_cast<u32x4*>(lds + ((i & 1) ? lo1 : lo0) + (i >> 1) * 16 * RW) = v[i];
-}
-
-template <typename T>
-__device__ __forceinline__ typename WMF<T>::e8 ld_tr(const uint16_t* tile, int off_lo, int off_hi) {
-  s16x4 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_lo));
-  s16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(tile + off_hi));
-  s16x8 v = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
-  return __builtin_bit_cast(typename WMF<T>::e8, v);
 }
 
 // Workgroup -> (split, n tile, k tile), XCD-aware: the hardware deals workgroups to the 8
@@ -129,109 +77,6 @@ __device__ __forceinline__ void wg_map(int tiles_n, int tiles_k, int group, int&
   const int r = p - gid * gfull;
   tn = first + r % gs;
   tk = r / gs;
-}
-
-template <typename T>
-__global__ __launch_bounds__(kT, 1) void wgrad_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
-                                                        float* __restrict__ ws, int64_t Tn, int N, int K,
-                                                        int64_t lda, int64_t ldb, int64_t t_split, int group) {
-  __shared__ __attribute__((aligned(16))) uint16_t sA[TK * RW];
-  __shared__ __attribute__((aligned(16))) uint16_t sB[TK * RW];
-  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
-  int split, tn, tk;
-  wg_map(tiles_n, tiles_k, group, split, tn, tk);
-  const int n0 = tn * TM, k0 = tk * TN;
-  const int64_t t_begin = split * t_split;
-  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int hh = lane >> 5;
-
-  // transposed-read offsets: lane supplies (row 4hh+q [+8], cols c..c+3) and receives
-  // column (lane & 31) of each 32-wide block, rows {4hh..4hh+3, 4hh+8..4hh+11}
-  int aLo[4], aHi[4], bLo[4], bHi[4];
-  {
-    const int q = (lane & 15) >> 2, pp = lane & 3;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ca = wm * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
-      const int cb = wn * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
-      aLo[i] = swz(4 * hh + q, ca >> 3) + (ca & 7);
-      aHi[i] = swz(4 * hh + 8 + q, ca >> 3) + (ca & 7);
-      bLo[i] = swz(4 * hh + q, cb >> 3) + (cb & 7);
-      bHi[i] = swz(4 * hh + 8 + q, cb >> 3) + (cb & 7);
-    }
-  }
-
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16{0.f};
-
-  const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
-  const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
-  // one register set: tile t+1's loads are issued before tile t's MFMAs and written to LDS
-  // after them (two 2-register-set variants spilled: 256 arch VGPRs + 256 accumulators)
-  u32x4 ra[NR], rb[NR];
-  const int lo0 = swz(threadIdx.x / CH, threadIdx.x % CH), lo1 = swz(threadIdx.x / CH + 8, threadIdx.x % CH);
-
-  int64_t t0 = t_begin;
-  if (t0 < t_end) {
-    stage_load(ra, A + t0 * lda + n0, lda, vcA);
-    stage_load(rb, B + t0 * ldb + k0, ldb, vcB);
-    stage_store(ra, sA, lo0, lo1);
-    stage_store(rb, sB, lo0, lo1);
-  }
-  __syncthreads();
-  while (t0 < t_end) {
-    const int64_t tnext = t0 + TK;
-    {
-      // branch-free: the last tile re-reads itself (never stored)
-      const int64_t tl = tnext < t_end ? tnext : t0;
-      stage_load(ra, A + tl * lda + n0, lda, vcA);
-      stage_load(rb, B + tl * ldb + k0, ldb, vcB);
-    }
-#pragma unroll
-    for (int s = 0; s < TK / 16; ++s) {
-      typename WMF<T>::e8 fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
-        fb[i] = ld_tr<T>(sB, bLo[i] + s * 16 * RW, bHi[i] + s * 16 * RW);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
-    }
-    __syncthreads();
-    if (tnext < t_end) {
-      stage_store(ra, sA, lo0, lo1);
-      stage_store(rb, sB, lo0, lo1);
-    }
-    __syncthreads();
-    t0 = tnext;
-  }
-
-  // fp32 partial tile -> workspace [split][N][K]; lane holds column (lane & 31) of each
-  // 32 x 32 block, rows (r & 3) + 8 (r >> 2) + 4 hh
-  float* out = ws + static_cast<int64_t>(split) * N * K;
-  const int col_l = lane & 31;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = k0 + wn * 128 + 32 * j + col_l;
-    if (k >= K) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nb = n0 + wm * 128 + 32 * i + 4 * hh;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int n = nb + (r & 3) + 8 * (r >> 2);
-        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
-      }
-    }
-  }
 }
 
 // ---------------------------------------------------------------- LDS-DMA variant
@@ -278,22 +123,6 @@ __device__ __forceinline__ void stage_glds(uint16_t* lds, const uint16_t* src, i
   }
 }
 
-// instruction i (< TKS / W / 2) of stage_glds: the two rows RPW w + 2 i + {0, 1}
-template <int W, int TKS>
-__device__ __forceinline__ void stage_glds_one(uint16_t* lds, const uint16_t* src, int64_t ld, int vc, int wave,
-                                               int lane, int i) {
-  constexpr int RPW = TKS / W;
-  const int pc = lane & 31, half = lane >> 5;
-  const int r = RPW * wave + 2 * i + half;
-  const int g = ((r & 3) << 2) | ((r >> 2) & 3);
-  int c = pc ^ g;
-  c = c < vc ? c : vc - 1;
-  if (ld < (1 << 24))
-    lds_dma16_sv(src, static_cast<uint32_t>((r * static_cast<int>(ld) + c * 8) * 2), lds + (RPW * wave + 2 * i) * RW);
-  else
-    glds16(src + static_cast<int64_t>(r) * ld + c * 8, lds + (RPW * wave + 2 * i) * RW);
-}
-
 // s_waitcnt vmcnt(N) leaving expcnt / lgkmcnt unconstrained (gfx9 encoding)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -301,325 +130,9 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// WN waves along the output columns (2 -> 4 waves of 128 x 128, 4 -> 8 waves of 128 x 64:
-// two waves per SIMD, each with half the accumulators).  NS-stage ring of TKS-token tiles:
-// the DMA of tile t + NS - 1 is issued right after the barrier that opens tile t, so a load
-// has NS - 1 tiles of MFMA work to land; one barrier per tile.
-// SPREAD: the next tile's DMA instructions are issued one A and one B piece per 16-token
-// k-step, between that step's LDS reads and its MFMAs, instead of as one burst after the
-// barrier (an LDS-DMA issue holds the wave ~60 cycles; in a burst both waves of a SIMD stall
-// their MFMAs at the same time).
-template <typename T, int WN, int TKS, int NS, bool SPREAD = false>
-__global__ __launch_bounds__(128 * WN, 1) void wgrad_glds_kernel(const uint16_t* __restrict__ A,
-                                                             const uint16_t* __restrict__ B, float* __restrict__ ws,
-                                                             int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
-                                                             int64_t t_split, int group) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // NS stages x (A, B) x TKS rows
-  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
-  int split, tn, tk;
-  wg_map(tiles_n, tiles_k, group, split, tn, tk);
-  const int n0 = tn * TM, k0 = tk * TN;
-  const int64_t t_begin = split * t_split;
-  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  constexpr int W = 2 * WN, NJ = 8 / WN, WCOLS = 32 * NJ;
-  constexpr int L = 2 * (TKS / W / 2);  // DMA instructions per wave per tile (A and B)
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int hh = lane >> 5;
-  int aLo[4], aHi[4], bLo[NJ], bHi[NJ];
-  {
-    const int q = (lane & 15) >> 2, pp = lane & 3;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ca = wm * 128 + 32 * i + 16 * ((lane >> 4) & 1) + 4 * pp;
-      aLo[i] = swz(4 * hh + q, ca >> 3) + (ca & 7);
-      aHi[i] = swz(4 * hh + 8 + q, ca >> 3) + (ca & 7);
-    }
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int cb = wn * WCOLS + 32 * j + 16 * ((lane >> 4) & 1) + 4 * pp;
-      bLo[j] = swz(4 * hh + q, cb >> 3) + (cb & 7);
-      bHi[j] = swz(4 * hh + 8 + q, cb >> 3) + (cb & 7);
-    }
-  }
-  f32x16 acc[4][NJ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x16{0.f};
-  const int vcA = (N - n0) >= TM ? CH : (N - n0) / 8;
-  const int vcB = (K - k0) >= TN ? CH : (K - k0) / 8;
-  const int64_t ntiles = (t_end - t_begin) / TKS;
-  const uint16_t* pa = A + t_begin * lda + n0;
-  const uint16_t* pb = B + t_begin * ldb + k0;
-  constexpr int STAGE = 2 * TKS * RW;  // elements per stage (A then B)
-  const bool active = n0 + wm * 128 < N && k0 + wn * WCOLS < K;  // wave-uniform
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p) {
-    if (p < ntiles) {
-      stage_glds<W, TKS>(smem + p * STAGE, pa + p * TKS * lda, lda, vcA, wave, lane);
-      stage_glds<W, TKS>(smem + p * STAGE + TKS * RW, pb + p * TKS * ldb, ldb, vcB, wave, lane);
-    }
-  }
-  int cur_slot = 0, load_slot = NS - 1;
-  for (int64_t t = 0; t < ntiles; ++t) {
-    if (t + NS - 2 < ntiles)
-      wait_vm<(NS - 2) * L>();  // this wave's DMA of tile t landed (later tiles may fly)
-    else
-      wait_vm<0>();
-    __syncthreads();  // ... everyone's, and every wave is done reading tile t - 1's slot
-    const bool issue = t + NS - 1 < ntiles;
-    uint16_t* nxt = smem + load_slot * STAGE;
-    const int64_t tt = t + NS - 1;
-    if (!SPREAD && issue) {
-      stage_glds<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane);
-      stage_glds<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane);
-    }
-    load_slot = load_slot + 1 == NS ? 0 : load_slot + 1;
-    const uint16_t* sA = smem + cur_slot * STAGE;
-    const uint16_t* sB = sA + TKS * RW;
-    cur_slot = cur_slot + 1 == NS ? 0 : cur_slot + 1;
-#pragma unroll
-    for (int s = 0; s < TKS / 16; ++s) {
-      typename WMF<T>::e8 fa[4], fb[NJ];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = ld_tr<T>(sA, aLo[i] + s * 16 * RW, aHi[i] + s * 16 * RW);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) fb[j] = ld_tr<T>(sB, bLo[j] + s * 16 * RW, bHi[j] + s * 16 * RW);
-      if constexpr (SPREAD) {
-        constexpr int PER = (TKS / W / 2) / (TKS / 16);  // pieces per operand per k-step
-        static_assert(PER >= 1 && PER * (TKS / 16) == TKS / W / 2, "pieces split evenly over the k-steps");
-        if (issue) {
-#pragma unroll
-          for (int q = 0; q < PER; ++q) {
-            stage_glds_one<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane, s * PER + q);
-            stage_glds_one<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane, s * PER + q);
-          }
-        }
-      }
-      // a wave whose whole output block lies past the matrix edge (e.g. 3 of the 4 column
-      // waves of the last 64 of 1600 columns) skips its MFMAs
-      if (active) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = WMF<T>::mma(fa[i], fb[j], acc[i][j]);
-      }
-    }
-  }
-  float* out = ws + static_cast<int64_t>(split) * N * K;
-  const int col_l = lane & 31;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k = k0 + wn * WCOLS + 32 * j + col_l;
-    if (k >= K) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nb = n0 + wm * 128 + 32 * i + 4 * hh;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int n = nb + (r & 3) + 8 * (r >> 2);
-        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
-      }
-    }
-  }
-}
-
-// n-tiles per workgroup group in wg_map (SMP_WGRAD_GROUP, default 1: measured no better at 2-8)
-inline int wgrad_group() {
-  static const int v = [] {
-    const char* e = getenv("SMP_WGRAD_GROUP");
-    const int g = e != nullptr ? atoi(e) : 1;
-    return g >= 1 && g <= 32 ? g : 1;
-  }();
-  return v;
-}
-
-// ---------------------------------------------------------------- phased (ping-pong) variant
-// 8 waves (2 along N x 4 along K, 128 x 64 outputs each), 64-token K-tiles in two buffers.
-// A buffer holds four 16 KB QUARTERS, each the part of the tile one MFMA phase consumes:
-//   slot 0: A columns {0..63, 128..191}   (qm = 0 of both N wave rows)
-//   slot 1: B columns {64 w + 0..31}      (qn = 0 of the four K wave columns)
-//   slot 2: B columns {64 w + 32..63}     (qn = 1)
-//   slot 3: A columns {64..127, 192..255} (qm = 1)
-// Each tile runs 4 phases, one output quadrant each: (qm, qn) = (0,0) (0,1) (1,1) (1,0).
-// A phase = [this phase's transposed LDS reads; DMA of one quarter of the NEXT tile; counted
-// vmcnt; barrier; 8 MFMAs at raised priority; barrier].  Quarter j of tile t + 1 is issued in
-// phase j of tile t and first read 3-4 phases later; the wait is counted (vmcnt 4, never 0 in
-// steady state).  With PP the two N wave rows run one barrier apart (the second row takes an
-// extra barrier up front), so on every SIMD one wave multiplies while the other reads LDS and
-// issues DMA.  A wave waits for the data of phase p + 1 before its mid-phase barrier of phase
-// p: with the one-barrier stagger that still precedes every reader's phase p + 1.
-constexpr int QR = 128;       // elements per quarter row (256 B)
-constexpr int QE = TK * QR;   // elements per quarter
-constexpr int QBUF = 4 * QE;  // elements per K-tile buffer
-
-// 16 chunks per 256-B row, chunk ^= 4 (row & 3): the 4-row x 32-column transposed reads of a
-// 32-lane half hit all 64 banks once
-__device__ __forceinline__ int qswz(int row, int col) {
-  return row * QR + ((((col >> 3) ^ ((row & 3) << 2))) << 3) + (col & 7);
-}
-
-// one quarter (64 tokens x 128 region columns): region column x reads source column
-// qoff + (x >> plog) * stride + (x & (piece - 1)) of the tile; 16 four-row DMA instructions,
-// two per wave.  Columns at or past vcols (matrix edge) re-read column 0 -- they only feed
-// outputs that are never stored.
-__device__ __forceinline__ void stage_quarter(uint16_t* region, const uint16_t* src, int64_t ld, int qoff, int plog,
-                                              int stride, int vcols, int wave, int lane) {
-  const int sub = lane >> 4;
-  const int lc = (lane & 15) ^ (sub << 2);
-  const int x = lc * 8;
-  int col = qoff + (x >> plog) * stride + (x & ((1 << plog) - 1));
-  col = col < vcols ? col : 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = 2 * wave + i;
-    glds16(src + static_cast<int64_t>(4 * m + sub) * ld + col, region + 4 * m * QR);
-  }
-}
-
-__device__ __forceinline__ void phase_sync() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <typename T>
-__device__ __forceinline__ void ld_frags(typename WMF<T>::e8 (&f)[4], const uint16_t* region, int off) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) f[s] = ld_tr<T>(region, off + s * 16 * QR, off + s * 16 * QR + 8 * QR);
-}
-
-template <typename T>
-__device__ __forceinline__ void mma_quadrant(f32x16& c0, f32x16& c1, const typename WMF<T>::e8 (&a0)[4],
-                                             const typename WMF<T>::e8 (&a1)[4], const typename WMF<T>::e8 (&b)[4]) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    c0 = WMF<T>::mma(a0[s], b[s], c0);
-    c1 = WMF<T>::mma(a1[s], b[s], c1);
-  }
-  __builtin_amdgcn_s_setprio(0);
-}
-
-template <typename T, bool PP>
-__global__ __launch_bounds__(512, 1) void wgrad_pp_kernel(const uint16_t* __restrict__ A,
-                                                          const uint16_t* __restrict__ B, float* __restrict__ ws,
-                                                          int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
-                                                          int64_t t_split, int group) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];  // 2 K-tile buffers x 4 quarters
-  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
-  int split, tn, tk;
-  wg_map(tiles_n, tiles_k, group, split, tn, tk);
-  const int n0 = tn * TM, k0 = tk * TN;
-  const int64_t t_begin = split * t_split;
-  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  int aOff0, aOff1, bOff;
-  {
-    const int row = 4 * (lane >> 5) + ((lane & 15) >> 2);
-    const int c = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-    aOff0 = qswz(row, wr * 64 + c);
-    aOff1 = qswz(row, wr * 64 + 32 + c);
-    bOff = qswz(row, wc * 32 + c);
-  }
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{0.f};
-  const int vA = (N - n0) >= TM ? TM : N - n0;
-  const int vB = (K - k0) >= TN ? TN : K - k0;
-  const int64_t ntiles = t_end > t_begin ? (t_end - t_begin) / TK : 0;
-  const uint16_t* pa = A + t_begin * lda + n0;
-  const uint16_t* pb = B + t_begin * ldb + k0;
-  if (ntiles > 0) {
-    stage_quarter(smem + 0 * QE, pa, lda, 0, 6, 128, vA, wave, lane);
-    stage_quarter(smem + 1 * QE, pb, ldb, 0, 5, 64, vB, wave, lane);
-    stage_quarter(smem + 2 * QE, pb, ldb, 32, 5, 64, vB, wave, lane);
-    stage_quarter(smem + 3 * QE, pa, lda, 64, 6, 128, vA, wave, lane);
-    wait_vm<4>();  // slots 0, 1 of tile 0
-    phase_sync();
-    if (PP && wr == 1) phase_sync();
-    typename WMF<T>::e8 fa0[4], fa1[4], fb0[4], fb1[4];
-    for (int64_t t = 0; t < ntiles; ++t) {
-      const uint16_t* cb = smem + (t & 1) * QBUF;
-      uint16_t* nb = smem + ((t + 1) & 1) * QBUF;
-      const bool next = t + 1 < ntiles;
-      const uint16_t* na = pa + (t + 1) * TK * lda;
-      const uint16_t* nbp = pb + (t + 1) * TK * ldb;
-      // phase 0: (qm 0, qn 0)
-      ld_frags<T>(fa0, cb + 0 * QE, aOff0);
-      ld_frags<T>(fa1, cb + 0 * QE, aOff1);
-      ld_frags<T>(fb0, cb + 1 * QE, bOff);
-      if (next) {
-        stage_quarter(nb + 0 * QE, na, lda, 0, 6, 128, vA, wave, lane);
-        wait_vm<4>();  // slot 2 of tile t
-      } else {
-        wait_vm<0>();
-      }
-      phase_sync();
-      mma_quadrant<T>(acc[0][0], acc[1][0], fa0, fa1, fb0);
-      phase_sync();
-      // phase 1: (qm 0, qn 1)
-      ld_frags<T>(fb1, cb + 2 * QE, bOff);
-      if (next) {
-        stage_quarter(nb + 1 * QE, nbp, ldb, 0, 5, 64, vB, wave, lane);
-        wait_vm<4>();  // slot 3 of tile t
-      } else {
-        wait_vm<0>();
-      }
-      phase_sync();
-      mma_quadrant<T>(acc[0][1], acc[1][1], fa0, fa1, fb1);
-      phase_sync();
-      // phase 2: (qm 1, qn 1)
-      ld_frags<T>(fa0, cb + 3 * QE, aOff0);
-      ld_frags<T>(fa1, cb + 3 * QE, aOff1);
-      if (next) stage_quarter(nb + 2 * QE, nbp, ldb, 32, 5, 64, vB, wave, lane);
-      phase_sync();
-      mma_quadrant<T>(acc[2][1], acc[3][1], fa0, fa1, fb1);
-      phase_sync();
-      // phase 3: (qm 1, qn 0)
-      if (next) {
-        stage_quarter(nb + 3 * QE, na, lda, 64, 6, 128, vA, wave, lane);
-        wait_vm<4>();  // slots 0, 1 of tile t + 1
-      }
-      phase_sync();
-      mma_quadrant<T>(acc[2][0], acc[3][0], fa0, fa1, fb0);
-      phase_sync();
-    }
-    if (PP && wr == 0) phase_sync();
-  }
-  float* out = ws + static_cast<int64_t>(split) * N * K;
-  const int col_l = lane & 31, hh = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int k = k0 + wc * 64 + 32 * j + col_l;
-    if (k >= K) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nb = n0 + wr * 128 + 32 * i + 4 * hh;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int n = nb + (r & 3) + 8 * (r >> 2);
-        if (n < N) out[static_cast<int64_t>(n) * K + k] = acc[i][j][r];
-      }
-    }
-  }
-}
-
-template <typename T, bool PP>
-int launch_pp(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
-              int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
-  constexpr size_t lds = 2 * QBUF * sizeof(uint16_t);  // 128 KB
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<T, PP>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr_set = true;
-  }
-  wgrad_pp_kernel<T, PP><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
-  return 0;
-}
+// n-tiles per workgroup group in wg_map: 1 = a row of k-tiles shares one A strip per XCD
+// (groups of 2-8 n-tiles measured no better, profiles/r2/wgrad_kernel.md)
+constexpr int kWgradGroup = 1;
 
 // ------------------------------------------------------ 16x16x32 MFMA variant
 // Same staging (LDS-DMA ring, swizzled 512-B rows) and 8-wave 128 x 64 output blocks, but
@@ -677,7 +190,7 @@ __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, i
 // segments each, partial tiles summed in order -- was built on these segments and measured
 // 10-35 % SLOWER on every GPT-2 XL shape (profiles/r3/wgrad_variants.md): concurrent
 // workgroups then stream disjoint token ranges and stop sharing A / B strips in L2.)
-template <typename T, int TKS, int NS, bool SPREAD>
+template <typename T, int TKS, int NS>
 __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                uint16_t* smem, int N, int K, int64_t lda, int64_t ldb, int tn, int tk,
                                                int64_t t_begin, int64_t ntiles, float* __restrict__ out,
@@ -747,7 +260,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
     const bool issue = t + NS - 1 < ntiles;
     uint16_t* nxt = smem + load_slot * STAGE;
     const int64_t tt = t + NS - 1;
-    if (!SPREAD && issue) {
+    if (issue) {
       stage_glds<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane);
       stage_glds<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane);
     }
@@ -782,17 +295,6 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
       if (cs_wave) fb[0] = ones;
 #pragma unroll
       for (int i = 0; i < NI / 2; ++i) fa[i] = ld_tr16<T>(sA, aLo[i] + s * 32 * RW, aHi[i] + s * 32 * RW);
-      if constexpr (SPREAD) {
-        constexpr int PER = (TKS / W / 2) / (TKS / 32);
-        static_assert(PER >= 1 && PER * (TKS / 32) == TKS / W / 2, "pieces split evenly over the k-steps");
-        if (issue) {
-#pragma unroll
-          for (int q = 0; q < PER; ++q) {
-            stage_glds_one<W, TKS>(nxt, pa + tt * TKS * lda, lda, vcA, wave, lane, s * PER + q);
-            stage_glds_one<W, TKS>(nxt + TKS * RW, pb + tt * TKS * ldb, ldb, vcB, wave, lane, s * PER + q);
-          }
-        }
-      }
       // the A fragments in two halves of 4 (fewer live registers)
       if (active) {
 #pragma unroll
@@ -848,7 +350,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
   }
 }
 
-template <typename T, int TKS, int NS, bool SPREAD>
+template <typename T, int TKS, int NS>
 __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B, float* __restrict__ ws,
                                                              int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
@@ -860,13 +362,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __
   const int64_t t_begin = split * t_split;
   const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
   const bool idle = wgrad_cs_idle(K);
-  glds16_segment<T, TKS, NS, SPREAD>(
+  glds16_segment<T, TKS, NS>(
       A, B, smem, N, K, lda, ldb, tn, tk, t_begin, (t_end - t_begin) / TKS, ws + static_cast<int64_t>(split) * N * K,
       K, 0, 0, cs == nullptr ? nullptr : cs + (static_cast<int64_t>(split) * (idle ? 1 : tiles_k) + (idle ? 0 : tk)) * N,
       cs != nullptr && !idle, tiles_k, tk, cs != nullptr && idle);
 }
 
-template <typename T, int TKS, int NS, bool SPREAD>
+template <typename T, int TKS, int NS>
 int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
                   int64_t ldb, int64_t t_split, int grid, hipStream_t s, float* cs = nullptr) {
   // operand ring + the column-sum accumulators (16 row groups x 256 fp32)
@@ -874,76 +376,13 @@ int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tok
   static_assert(lds <= 160 * 1024, "LDS per CU");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds16_kernel<T, TKS, NS, SPREAD>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds16_kernel<T, TKS, NS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr_set = true;
   }
-  wgrad_glds16_kernel<T, TKS, NS, SPREAD><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
-                                                                 wgrad_group(), cs);
+  wgrad_glds16_kernel<T, TKS, NS><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
+                                                                 kWgradGroup, cs);
   return 0;
-}
-
-// SMP_WGRAD_PIPE: 0 = 4 waves, 2 x 64-token stages; 1 = 8 waves, 2 x 64; 2 = 8 waves,
-// 4 x 32; 3 = 8 waves, 5 x 32 (all 160 KB of LDS); 4 = phased, lockstep; 5 = phased ping-pong;
-// 6 / 7 = 1 / 2 with the DMA spread over the k-steps; 8 / 9 = 1 / 6 on 16x16x32 MFMAs.
-// Default 8 (tools/gpu_wgrad_ab.sh, same box, interleaved, ms at T = 65536: 4800x1600 s8
-// 1.123 vs 1.163, 6400x1600 s4 1.359-1.364 vs 1.419, 1600x6400 s4 1.454-1.471 vs 1.498,
-// 1600x1600 s5 0.360-0.363 vs 0.370; spreading the DMA over the k-steps: no gain)
-inline int wgrad_pipe() {
-  static const int v = [] {
-    const char* e = getenv("SMP_WGRAD_PIPE");
-    if (e != nullptr && e[0] >= '0' && e[0] <= '9') return e[0] - '0';
-    const char* w = getenv("SMP_WGRAD_WAVES");
-    return (w != nullptr && w[0] == '4') ? 0 : 8;
-  }();
-  return v;
-}
-
-template <typename T, int WN, int TKS, int NS, bool SPREAD = false>
-int launch_glds(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
-                int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
-  constexpr size_t lds = static_cast<size_t>(NS) * 2 * TKS * RW * sizeof(uint16_t);
-  static_assert(lds <= 160 * 1024, "LDS per CU");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_glds_kernel<T, WN, TKS, NS, SPREAD>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    attr_set = true;
-  }
-  wgrad_glds_kernel<T, WN, TKS, NS, SPREAD><<<grid, 128 * WN, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, wgrad_group());
-  return 0;
-}
-
-template <typename T>
-int launch_glds_pipe(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
-                     int64_t ldb, int64_t t_split, int grid, hipStream_t s) {
-  switch (wgrad_pipe()) {
-    case 0:
-      return launch_glds<T, 2, 64, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 2:
-      return launch_glds<T, 4, 32, 4>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 3:
-      return launch_glds<T, 4, 32, 5>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 4:
-      return launch_pp<T, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 5:
-      return launch_pp<T, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 6:
-      return launch_glds<T, 4, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 7:
-      return launch_glds<T, 4, 32, 4, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 8:
-      return launch_glds16<T, 64, 2, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    case 9:
-      return launch_glds16<T, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    default:
-      return launch_glds<T, 4, 64, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-  }
-}
-
-inline bool wgrad_use_glds() {
-  const char* e = getenv("SMP_WGRAD_GLDS");
-  return e == nullptr || e[0] != '0';
 }
 
 // C (+)= sum over splits of ws, 4 elements per thread
@@ -1013,29 +452,12 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   int64_t t_split = (tokens + splits - 1) / splits;
   t_split = (t_split + TK - 1) / TK * TK;
   const int grid = tiles * splits;
-  if (bias != nullptr) {
-    // the column-sum pass lives in the 16x16x32 kernel
-    const auto* pa = static_cast<const uint16_t*>(a);
-    const auto* pb = static_cast<const uint16_t*>(b);
-    if (wgrad_pipe() == 9)
-      launch_glds16<bf16, 64, 2, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
-    else
-      launch_glds16<bf16, 64, 2, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
-  } else if (wgrad_use_glds()) {
-    const auto* pa = static_cast<const uint16_t*>(a);
-    const auto* pb = static_cast<const uint16_t*>(b);
-    if (dt == BF16)
-      launch_glds_pipe<bf16>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    else if (dt == F16)
-      launch_glds_pipe<f16>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
-    else
-      return -2;
-  } else if (dt == BF16)
-    wgrad_kernel<bf16><<<grid, kT, 0, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                            tokens, n, k, lda, ldb, t_split, 1);
+  const auto* pa = static_cast<const uint16_t*>(a);
+  const auto* pb = static_cast<const uint16_t*>(b);
+  if (bias != nullptr || dt == BF16)
+    launch_glds16<bf16, kTK, kNS>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
   else if (dt == F16)
-    wgrad_kernel<f16><<<grid, kT, 0, s>>>(static_cast<const uint16_t*>(a), static_cast<const uint16_t*>(b), ws,
-                                           tokens, n, k, lda, ldb, t_split, 1);
+    launch_glds16<f16, kTK, kNS>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
   else
     return -2;
   hipError_t e = hipGetLastError();

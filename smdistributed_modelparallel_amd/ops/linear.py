@@ -26,6 +26,10 @@ import os
 import torch
 import torch.nn.functional as F
 
+from ..backend.logger import get_logger
+
+logger = get_logger()
+
 _WT_EPOCH = [0]
 _WT_MIN_NUMEL = 1 << 20
 _WT_ENABLED = os.environ.get("SMP_TRANSPOSED_DGRAD", "1") != "0"
@@ -114,94 +118,25 @@ def _col_sum(x2, out=None):
 
 
 # ----------------------------------------------------------------- weight-gradient algorithm
-# dW[N, K] += dY[T, N]^T X[T, K] reduces over all T = batch x sequence tokens: few output
-# tiles (GPT-2 XL: 81-280 of 192-256 for 256 CUs) and both operands strided along the
-# reduction, the layout hipBLASLt runs slowest.  Two alternatives can win, depending on the
-# shape (MI355X, T = 65536, TunableOp-selected kernels; tools/wgrad_probe.py):
-#   "tn"  -- transpose dY and X (HIP LDS transpose, HBM rate) and run the GEMM with both
-#            operands contiguous along T: [4800, 1600] 1.32 -> 0.87 + 0.33 ms (transposes);
-#   "sk8" -- split T into 8 chunks, one batched GEMM into bf16 partials, then their sum:
-#            [1600, 1600] 0.49 -> 0.39 ms;
-# while for [6400, 1600] / [1600, 6400] the plain strided GEMM ("nn") stays fastest.  The
-# choice is made per (T, N, K, dtype) by timing the candidates on the real operands the first
-# time a shape occurs inside a step (gradient restored after each trial), then cached for the
-# process.  Opt-in (SMP_WGRAD_AUTOTUNE=1): the isolated wins above did not survive the full
-# step -- same-box A/B of the GPT-2 XL bench, alternating, 766.6 / 770.1 ms/step off vs
-# 770.1 / 765.8 on (tools/gpu_ab_env.sh) -- and a per-rank timing pick can differ across
-# data-parallel ranks, so "nn" stays the default.
-_WGRAD_TUNE = os.environ.get("SMP_WGRAD_AUTOTUNE", "0") == "1"
-_WGRAD_CHOICE = {}
-_WGRAD_MIN_T = 16384
-_WGRAD_TEMP_CAP = 1 << 30  # bytes of temporaries a candidate may allocate
-
-
-def _wgrad_candidates(T, N, K, esize):
-    out = ["nn"]
-    if T * (N + K) * esize <= _WGRAD_TEMP_CAP:
-        out.append("tn")
-    if T % 8 == 0 and 8 * N * K * esize <= _WGRAD_TEMP_CAP:
-        out.append("sk8")
-    return out
-
-
-def _wgrad_run(method, g, dy2, x2):
-    if method == "tn":
-        from ._ext import ext
-
-        dyt = torch.empty((dy2.shape[1], dy2.shape[0]), dtype=dy2.dtype, device=dy2.device)
-        xt = torch.empty((x2.shape[1], x2.shape[0]), dtype=x2.dtype, device=x2.device)
-        ext().transpose_into(dy2, dyt)
-        ext().transpose_into(x2, xt)
-        g.addmm_(dyt, xt.t())
-    elif method == "sk8":
-        T = dy2.shape[0]
-        parts = torch.bmm(dy2.view(8, T // 8, dy2.shape[1]).transpose(1, 2), x2.view(8, T // 8, x2.shape[1]))
-        g.add_(parts.sum(0, dtype=torch.float32))
-    else:
-        g.addmm_(dy2.t(), x2)
-
-
-def _wgrad_pick(g, dy2, x2):
-    cands = _wgrad_candidates(dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.element_size())
-    if len(cands) == 1:
-        return cands[0]
-    saved = g.clone()
-    best, best_t, times = "nn", float("inf"), {}
-    for m in cands:
-        try:
-            _wgrad_run(m, g, dy2, x2)  # warm-up (kernel selection, allocator)
-            start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            start.record()
-            for _ in range(3):
-                _wgrad_run(m, g, dy2, x2)
-            end.record()
-            end.synchronize()
-            t = start.elapsed_time(end)
-        except torch.OutOfMemoryError:
-            t = float("inf")
-        g.copy_(saved)
-        times[m] = t
-        if t < best_t * 0.97:  # a candidate must beat the current pick by > 3 %
-            best, best_t = m, t
-    del saved
-    if os.environ.get("SMP_WGRAD_LOG") == "1":
-        print(f"wgrad autotune T={dy2.shape[0]} N={dy2.shape[1]} K={x2.shape[1]}: "
-              + ", ".join(f"{m} {t / 3:.3f} ms" for m, t in times.items()) + f" -> {best}", flush=True)
-    return best
-
-
-# Hand-written split-K MFMA weight-gradient kernel (csrc/kernels/wgrad.hip): reads both
-# token-major operands as they are (LDS-DMA staging, LDS transpose reads, no transpose
-# kernels) and accumulates into the gradient with beta = 1.  It beats hipBLASLt on some
-# shapes and loses on others (profiles/r2/wgrad_kernel.md), so the first time a shape occurs
-# inside a step both are timed on the real operands (gradient restored after each trial) and
-# the faster one is kept for the process.  SMP_WGRAD_KERNEL=0 never uses the kernel,
-# =1 always does.
+# dW[N, K] += dY[T, N]^T X[T, K] reduces over all T = batch x sequence tokens: few output tiles
+# and both operands strided along the reduction, the layout hipBLASLt runs slowest.  The
+# hand-written split-K MFMA kernel (csrc/kernels/wgrad.hip) reads both token-major operands as
+# they are and accumulates into the gradient with beta = 1.  Which one runs, and at how many
+# splits, comes from a FIXED per-shape table measured on MI355X -- no timing trials in the
+# backward, no host synchronisation, and the same split-K accumulation order on every run and
+# every rank.  Shapes off the table use the library GEMM.  (Measured and removed: transposing
+# the operands for a TN GEMM and a batched split-K through the library -- isolated wins that
+# did not survive the step, profiles/r2/gemm_epilogue_and_wgrad_stream.md; weight gradients on
+# a side HIP stream -- 773.6 vs 776.0 ms/step, 256 x 256-tile GEMM workgroups fill a CU.)
+#
+# SMP_WGRAD_KERNEL=0 never uses the kernel, =1 always does (occupancy-model split count);
+# SMP_WGRAD_PICK=timed times library vs kernel split counts per shape on first use (the
+# measurement mode that produced the table; per-process, so ranks may pick differently).
 _WGRAD_KERNEL = os.environ.get("SMP_WGRAD_KERNEL", "auto")
-_WGRAD_KERNEL_MIN_T = int(os.environ.get("SMP_WGRAD_KERNEL_MIN_TOKENS", "4096"))
+_WGRAD_KERNEL_MIN_T = 4096
 _WGRAD_KERNEL_CHOICE = {}
 _WGRAD_KERNEL_SPLIT_BEST = {}  # (T, N, K) -> fastest kernel split count seen by the timing pick
-_WGRAD_PICK_ROUNDS = max(1, int(os.environ.get("SMP_WGRAD_PICK_ROUNDS", "2")))
+_WGRAD_PICK_ROUNDS = 2
 
 
 def _wgrad_native_ok(g, dy2, x2):
@@ -212,41 +147,32 @@ def _wgrad_native_ok(g, dy2, x2):
             and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0)
 
 
-# Fixed picks (SMP_WGRAD_PICK=static, or torch.use_deterministic_algorithms(True)): the
-# per-shape winners measured on MI355X at T = 65536 (profiles/r2/session4_wgrad_pick_ab.md),
-# keyed by (N, K); other shapes use the library GEMM.  No timing trials, no host sync in the
-# backward, and the same split-K accumulation order in every run and on every rank.
-# (4800, 1600): s7 in the GPT-2 XL b32 step with the fused bias sums (1092-1099 us vs s5 1131,
-# s8 1167 + a larger partial reduce; profiles/r3/wgrad_variants.md).
+# The table: (N, K) -> kernel split count (0 = library GEMM), for T >= _WGRAD_STATIC_MIN_T tokens.
+# GPT-2 XL (T = 65536, profiles/r2/session4_wgrad_pick_ab.md, profiles/r3/wgrad_variants.md);
+# (4800, 1600): s7 in the b32 step with the fused bias sums (1092-1099 us vs s5 1131, s8 1167).
+# BASELINE config 3-5 rank shapes (scaled-batch TP): tools/wgrad_table.py, profiles/r4/.
 _WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7}
-# kernel split count for (1600, 6400) when the fused bias pass makes the kernel the choice
+# kernel split count for a library-table shape when the fused bias pass makes the kernel the choice
 _WGRAD_STATIC_KERNEL = {(1600, 6400): 4}
-# "time" (default): table shapes at >= _WGRAD_STATIC_MIN_T tokens take the table (timing trials
-# there flip between near-equal split counts from run to run: s5 / s7 for QKV), other shapes
-# are timed; "timed": always time; "static": always the table (library off-table).
-_WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "time")
-_WGRAD_STATIC_MIN_T = 32768
+_WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "table")
+_WGRAD_STATIC_MIN_T = 16384
 
 
 def _wgrad_static_pick(dy2, x2):
-    return _WGRAD_STATIC.get((dy2.shape[1], x2.shape[1]), 0) if dy2.shape[0] >= 16384 else 0
+    return _WGRAD_STATIC.get((dy2.shape[1], x2.shape[1]), 0) if dy2.shape[0] >= _WGRAD_STATIC_MIN_T else 0
 
 
 def _wgrad_kernel_splits(g, dy2, x2):
-    """Split count for the MFMA kernel at this (T, N, K, dtypes), or 0 for the library GEMM.
-
-    Timed once per shape: the kernel at its occupancy-model split count and at a few smaller
-    counts (fewer fp32 partials to reduce; the model ignores that traffic), and the library.
-    ``SMP_WGRAD_PICK=static`` or deterministic algorithms: the fixed table above instead."""
+    """Split count for the MFMA kernel at this (T, N, K, dtypes), or 0 for the library GEMM:
+    the fixed table (default), or -- SMP_WGRAD_PICK=timed -- timed once per shape: the kernel
+    at its occupancy-model split count and a ladder of smaller counts, and the library."""
     if _WGRAD_KERNEL == "1" or g.dtype != dy2.dtype:  # (fp32 accumulators: no library equivalent)
         return -1  # kernel, default split count
     key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype, g.dtype)
     hit = _WGRAD_KERNEL_CHOICE.get(key)
     if hit is not None:
         return hit
-    if _WGRAD_PICK == "static" or torch.are_deterministic_algorithms_enabled() or (
-            _WGRAD_PICK == "time" and dy2.shape[0] >= _WGRAD_STATIC_MIN_T
-            and (dy2.shape[1], x2.shape[1]) in _WGRAD_STATIC):
+    if _WGRAD_PICK != "timed" or torch.are_deterministic_algorithms_enabled():
         _WGRAD_KERNEL_CHOICE[key] = _wgrad_static_pick(dy2, x2)
         return _WGRAD_KERNEL_CHOICE[key]
     from ._ext import ext
@@ -265,8 +191,8 @@ def _wgrad_kernel_splits(g, dy2, x2):
     for name, fn in cands:
         fn()  # warm-up (library solution selection, allocator)
     g.copy_(saved)
-    # two interleaved rounds, best of each: the first use of a shape falls in a warm-up step
-    # where clocks still move, and a single back-to-back round favoured whichever ran last
+    # interleaved rounds, best of each: the first use of a shape falls in a warm-up step where
+    # clocks still move, and a single back-to-back round favoured whichever ran last
     for _ in range(_WGRAD_PICK_ROUNDS):
         for name, fn in cands:
             start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -283,10 +209,9 @@ def _wgrad_kernel_splits(g, dy2, x2):
     ks = {sp: t for sp, t in times.items() if sp != 0}
     if ks:
         _WGRAD_KERNEL_SPLIT_BEST[(key[0], key[1], key[2])] = min(ks, key=ks.get)
-    if os.environ.get("SMP_WGRAD_LOG") == "1":
-        print(f"wgrad T={key[0]} N={key[1]} K={key[2]}: "
-              + ", ".join(f"{'library' if s == 0 else f'kernel s{s}'} {t / 3:.3f} ms" for s, t in times.items())
-              + f" -> {'library' if best == 0 else f'kernel s{best}'}", flush=True)
+    logger.debug(f"wgrad T={key[0]} N={key[1]} K={key[2]}: "
+                 + ", ".join(f"{'library' if s == 0 else f'kernel s{s}'} {t / 3:.3f} ms" for s, t in times.items())
+                 + f" -> {'library' if best == 0 else f'kernel s{best}'}")
     return best
 
 
@@ -304,10 +229,10 @@ def _wgrad_kernel_wins(g, dy2, x2):
 # that wave sums dY on the matrix core (B fragment = ones): no cost on the busy SIMDs, so it is
 # always fused.  Otherwise the sums go through LDS inside the MFMA loop, which in-step costs
 # about what a separate column-sum pass does (GPT-2 XL b32 kernel traces: fc1 wgrad +150 us
-# vs. bias-GeLU backward -148 us), so that mode is only used for wide dY (>=
-# SMP_WGRAD_DBIAS_MIN_N columns).
+# vs. bias-GeLU backward -148 us), so that mode is only used for wide dY (>= 4096 columns).
+# SMP_WGRAD_DBIAS=0 turns the fused bias sums off (separate column-sum pass).
 _WGRAD_DBIAS = os.environ.get("SMP_WGRAD_DBIAS", "1") != "0"
-_WGRAD_DBIAS_MIN_N = int(os.environ.get("SMP_WGRAD_DBIAS_MIN_N", "4096"))
+_WGRAD_DBIAS_MIN_N = 4096
 
 
 def _wgrad_dbias_free(k):
@@ -331,13 +256,7 @@ def _wgrad_accumulate(g, dy2, x2, dbias=None):
 
             ext().wgrad_(g, dy2, x2, True, max(s, 0), dbias if fuse else None, True)
             return fuse
-    method = "nn"
-    if _WGRAD_TUNE and g.is_cuda and dy2.shape[0] >= _WGRAD_MIN_T and dy2.is_contiguous() and x2.is_contiguous():
-        key = (dy2.shape[0], dy2.shape[1], x2.shape[1], dy2.dtype)
-        method = _WGRAD_CHOICE.get(key)
-        if method is None:
-            method = _WGRAD_CHOICE[key] = _wgrad_pick(g, dy2, x2)
-    _wgrad_run(method, g, dy2, x2)
+    g.addmm_(dy2.t(), x2)
     return False
 
 
@@ -350,48 +269,6 @@ def _wgrad_dbias_splits(dy2, x2):
         return hit
     k = (dy2.shape[1], x2.shape[1])
     return _WGRAD_STATIC.get(k, 0) or _WGRAD_STATIC_KERNEL.get(k, -1)
-
-
-# Weight gradients on a side HIP stream (opt-in, SMP_WGRAD_STREAM=1): dW = dY^T X is off the
-# backward's critical path (nothing in the step reads it before the reducer / optimizer), so
-# it can run concurrently with the next input-gradient GEMMs, attention backward and the
-# memory-bound LayerNorm / GeLU kernels, filling the issue slots and CUs they leave idle.
-# Every consumer of gradients first calls wgrad_sync() (the reducer before a bucket launch
-# and fp32 fold, the step function after the backward), which orders the current stream
-# after all weight-gradient work issued so far.
-_WGRAD_STREAM = os.environ.get("SMP_WGRAD_STREAM", "0") == "1"
-_SIDE = {}
-_PENDING = [False]
-
-
-def _side_stream(dev):
-    s = _SIDE.get(dev.index)
-    if s is None:
-        s = _SIDE[dev.index] = torch.cuda.Stream(device=dev, priority=0)
-    return s
-
-
-def wgrad_sync():
-    """Order the current stream after every side-stream weight gradient issued so far."""
-    if _PENDING[0]:
-        cur = torch.cuda.current_stream()
-        for s in _SIDE.values():
-            if s.device == cur.device:
-                cur.wait_stream(s)
-        _PENDING[0] = False
-
-
-def _wgrad_async(g, dy2, x2):
-    cur = torch.cuda.current_stream()
-    side = _side_stream(dy2.device)
-    side.wait_stream(cur)  # dY and X are complete
-    with torch.cuda.stream(side):
-        _wgrad_accumulate(g, dy2, x2)
-    # the caching allocator must not hand these blocks to main-stream work before the
-    # side stream has read them
-    dy2.record_stream(side)
-    x2.record_stream(side)
-    _PENDING[0] = True
 
 
 def _fusable(w):
@@ -454,10 +331,7 @@ class _LinearWGradAccum(torch.autograd.Function):
                 # beta = 1 GEMM into the bound flat-buffer view; returning None still runs the
                 # weight's AccumulateGrad node (a no-op), so post-accumulate-grad hooks -- the
                 # reducers' bucket-ready signals -- fire exactly once, after this write
-                if _WGRAD_STREAM and dy2.is_cuda:
-                    _wgrad_async(w.grad, dy2, x.reshape(-1, x.shape[-1]))
-                else:
-                    bdone = _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]), dbias=btarget)
+                bdone = _wgrad_accumulate(w.grad, dy2, x.reshape(-1, x.shape[-1]), dbias=btarget)
             else:
                 # grad slot re-bound/removed since forward: hand the gradient to autograd
                 dw = dy2.t().mm(x.reshape(-1, x.shape[-1]))

@@ -27,7 +27,6 @@ import torch
 import torch.distributed as dist
 
 from ..backend.logger import get_logger
-from ..ops.linear import wgrad_sync
 from .comm_timer import timer as comm_timer
 
 logger = get_logger()
@@ -81,7 +80,6 @@ class BucketReducer:
 
     def _on_grad(self, p):
         if self.flat.fp32_accumulation:
-            wgrad_sync()  # side-stream weight gradients (ops/linear.py) land before the fold
             self.flat.fold_grad(p)  # every microbatch: low-precision grad -> fp32 main_grad
         if self.tracker is not None:
             # pipeline stage: one accumulation of one backward segment; the tracker knows
@@ -114,7 +112,6 @@ class BucketReducer:
         if b.launched:
             return
         b.launched = True
-        wgrad_sync()  # the bucket's side-stream weight gradients land before the collective
         self.launched_before_sync += 0 if self._in_sync else 1
         buf = self.flat.grad[b.start : b.end]
         scale = 1.0 / (self.divisor * (self.active_size or self.group_size))
@@ -149,7 +146,6 @@ class BucketReducer:
 
     def synchronize(self):
         """Launch whatever is left (unused params / non-overlapped mode) and wait."""
-        wgrad_sync()
         if self.flat.fp32_accumulation:
             for p in self.flat.params():
                 self.flat.fold_grad(p)

@@ -11,7 +11,7 @@ import time
 
 import torch
 
-from ..ops.linear import bump_weight_epoch, wgrad_sync
+from ..ops.linear import bump_weight_epoch
 
 from ..backend.collectives import CommGroup
 from ..backend.exceptions import DistributedModelNotWrappedError, SMPInvalidArgumentError
@@ -137,7 +137,6 @@ class StepFunction:
                 else:
                     mb_inputs = None
                 outputs = state.engine.run_step(self, mb_inputs)
-                wgrad_sync()  # side-stream weight gradients complete before anything reads grads
         finally:
             state.in_step_func = False
             core.timeline_end_step()

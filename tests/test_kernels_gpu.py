@@ -88,23 +88,6 @@ def test_bias_gelu(C, dt, rows, cols, exact):
     assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50 * max(1, rows // 200) ** 0.5, rtol=tol * 4)
 
 
-@pytest.mark.parametrize("rows,cols", [(4097, 6400), (3001, 2056)])
-def test_gelu_row_stream_matches_column_walker(C, rows, cols, monkeypatch):
-    """The row-streaming GeLU kernels (rows >= 2048) against the column walker (SMP_GELU_ROWS=0):
-    the same per-element math, so dx and y are bitwise equal; dbias differs only in summation order."""
-    torch.manual_seed(9)
-    dt = torch.bfloat16
-    x = torch.randn(rows, cols, device="cuda", dtype=dt)
-    b = torch.randn(cols, device="cuda", dtype=dt)
-    dy = torch.randn_like(x)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SMP_GELU_ROWS", mode)
-        out[mode] = (C.bias_gelu_fwd(x, b, False), *C.bias_gelu_bwd_dbias(dy, x, b, None, False))
-    assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
-    assert torch.allclose(out["1"][2].float(), out["0"][2].float(), atol=0.05 * rows ** 0.5, rtol=1e-2)
-
-
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("rows,cols", [(32768, 1600), (4097, 4800), (100, 6400), (7, 40), (515, 1001), (64, 8)])
 def test_col_sum_and_accumulate(C, dt, rows, cols):
@@ -474,18 +457,22 @@ def test_lamb_segmented_kernel_matches_cpu():
 
 
 @pytest.mark.parametrize("rows,cols", [(4097, 6400), (3001, 2056), (65, 40)])
-def test_gelu_flat_stream_matches_column_walker(C, rows, cols, monkeypatch):
-    """Forward bias-GeLU in memory order (default, SMP_GELU_FLAT) against the column walker:
-    same per-element math, bitwise-equal output."""
+def test_gelu_one_pass_matches_unfused_dbias(C, rows, cols):
+    """The one-pass bias-GeLU kernels (forward, and the pure elementwise backward used when the
+    weight-gradient kernel supplies the bias gradient) against the column-walker backward that
+    also sums dbias: same per-element math, so y and dx are bitwise equal."""
     torch.manual_seed(11)
     x = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
     b = torch.randn(cols, device="cuda", dtype=torch.bfloat16)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("SMP_GELU_FLAT", mode)
-        monkeypatch.setenv("SMP_GELU_ROWS", "0")
-        out[mode] = (C.bias_gelu_fwd(x, b, False), C.bias_gelu_fwd(x, b, True))
-    assert torch.equal(out["1"][0], out["0"][0]) and torch.equal(out["1"][1], out["0"][1])
+    dy = torch.randn_like(x)
+    for exact in (False, True):
+        dx1 = C.bias_gelu_bwd(dy, x, b, exact)
+        dx2, db = C.bias_gelu_bwd_dbias(dy, x, b, None, exact)
+        assert torch.equal(dx1, dx2)
+        ref = (x.float() + b.float())
+        y = C.bias_gelu_fwd(x, b, exact)
+        yr = torch.nn.functional.gelu(ref, approximate="none" if exact else "tanh")
+        assert (y.float() - yr).abs().max().item() < 2e-2
 
 
 @pytest.mark.parametrize("xdt,wdt", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.float32),

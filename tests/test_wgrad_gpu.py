@@ -1,44 +1,12 @@
-"""Weight-gradient algorithms of ops/linear.py ("nn", "tn", "sk8" and the autotuned pick)
-against an fp32 PyTorch reference."""
+"""Weight-gradient GEMM of ops/linear.py (library GEMM or the split-K MFMA kernel of
+csrc/kernels/wgrad.hip, picked from the fixed per-shape table or -- opt-in -- timed) against
+an fp32 PyTorch reference."""
 import pytest
 import torch
 
 from smdistributed_modelparallel_amd.ops import linear as L
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.mark.parametrize("method", ["nn", "tn", "sk8"])
-@pytest.mark.parametrize("shape", [(16384, 320, 192), (16392, 200, 136)])
-def test_wgrad_methods_match_fp32(method, shape):
-    T, N, K = shape
-    if method == "sk8" and T % 8:
-        pytest.skip("split-K needs T % 8 == 0")
-    g0 = torch.Generator(device="cuda").manual_seed(0)
-    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
-    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
-    g = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g0)
-    ref = g.float() + dy.float().t() @ x.float()
-    L._wgrad_run(method, g, dy, x)
-    err = (g.float() - ref).abs().max().item() / ref.abs().max().item()
-    assert err < 1e-2, (method, err)
-
-
-def test_wgrad_autotune_picks_and_preserves_gradient(monkeypatch):
-    monkeypatch.setattr(L, "_WGRAD_TUNE", True)  # opt-in (SMP_WGRAD_AUTOTUNE=1)
-    monkeypatch.setattr(L, "_WGRAD_KERNEL", "0")  # the hipBLASLt-side algorithm choice
-    T, N, K = 16384, 512, 256
-    g0 = torch.Generator(device="cuda").manual_seed(1)
-    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
-    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
-    g = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g0)
-    ref = g.float() + dy.float().t() @ x.float()
-    key = (T, N, K, torch.bfloat16)
-    L._WGRAD_CHOICE.pop(key, None)
-    L._wgrad_accumulate(g, dy, x)  # trials restore g; exactly one accumulation lands
-    assert L._WGRAD_CHOICE[key] in ("nn", "tn", "sk8")
-    err = (g.float() - ref).abs().max().item() / ref.abs().max().item()
-    assert err < 1e-2, err
 
 
 @pytest.mark.parametrize("shape", [(4096, 1600, 1600), (65536, 256, 256), (8200, 4800, 1600), (5000, 392, 1048),
@@ -95,8 +63,10 @@ def test_linear_uses_wgrad_kernel_for_bound_grads(monkeypatch):
     assert err < 1e-2, err
 
 
-def test_wgrad_auto_choice_accumulates_once(monkeypatch):
+def test_wgrad_timed_choice_accumulates_once(monkeypatch):
+    """SMP_WGRAD_PICK=timed: the trials restore the gradient; exactly one accumulation lands."""
     monkeypatch.setattr(L, "_WGRAD_KERNEL", "auto")
+    monkeypatch.setattr(L, "_WGRAD_PICK", "timed")
     T, N, K = 8192, 1024, 512
     g0 = torch.Generator(device="cuda").manual_seed(5)
     dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
@@ -111,9 +81,10 @@ def test_wgrad_auto_choice_accumulates_once(monkeypatch):
 
 
 def test_wgrad_static_pick_is_deterministic(monkeypatch):
-    """SMP_WGRAD_PICK=static: the measured per-shape winner without timing trials; two runs
-    give bitwise identical gradients (same split-K accumulation order)."""
-    monkeypatch.setattr(L, "_WGRAD_PICK", "static")
+    """Default table pick: the measured per-shape winner without timing trials; two runs give
+    bitwise identical gradients (same split-K accumulation order).  Off-table shapes take the
+    library GEMM (no trial, no host sync)."""
+    monkeypatch.setattr(L, "_WGRAD_PICK", "table")
     T, N, K = 16384, 1600, 1600  # table entry: kernel, 5 splits
     g0 = torch.Generator(device="cuda").manual_seed(3)
     dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
@@ -132,6 +103,11 @@ def test_wgrad_static_pick_is_deterministic(monkeypatch):
     err = (outs[0].float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2, err
     L._WGRAD_KERNEL_CHOICE.pop(key, None)
+    off = (T, 1024, 512, torch.bfloat16, torch.bfloat16)
+    L._WGRAD_KERNEL_CHOICE.pop(off, None)
+    g = torch.zeros(1024, 512, device="cuda", dtype=torch.bfloat16)
+    L._wgrad_accumulate(g, dy[:, :1024].contiguous(), x[:, :512].contiguous())
+    assert L._WGRAD_KERNEL_CHOICE[off] == 0
 
 
 # K 1600 / 1048: idle-wave MFMA column sums; K 6400 / 1000: LDS column sums

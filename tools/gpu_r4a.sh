@@ -4,8 +4,8 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r4a
-timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_attention_gpu.py \
-  tests/test_dropout_gpu.py tests/test_optimizers_gpu.py tests/test_oneshot_gpu.py > gpurun_out/r4a/pytest.log 2>&1 \
+timeout -k 10 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_attention_gpu.py \
+  tests/test_dropout_gpu.py tests/test_optimizers_gpu.py tests/test_oneshot_gpu.py tests/test_wgrad_gpu.py tests/test_kernels_gpu.py > gpurun_out/r4a/pytest.log 2>&1 \
   || { tail -40 gpurun_out/r4a/pytest.log; exit 1; }
 tail -3 gpurun_out/r4a/pytest.log
 for i in 1 2; do
@@ -14,3 +14,5 @@ for i in 1 2; do
 done
 timeout -k 10 300 python bench.py --steps 6 --warmup 3 > gpurun_out/r4a/bench.log 2>&1 || { tail -20 gpurun_out/r4a/bench.log; exit 1; }
 tail -1 gpurun_out/r4a/bench.log
+timeout -k 10 300 python tools/wgrad_table.py > gpurun_out/r4a/wgrad_table.jsonl 2>&1 || { tail -5 gpurun_out/r4a/wgrad_table.jsonl; exit 1; }
+tail -1 gpurun_out/r4a/wgrad_table.jsonl

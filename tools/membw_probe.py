@@ -51,7 +51,6 @@ res["ln_fwd_1600"] = {"us": round(ms * 1e3, 1), "TBps": round(2 * xl.numel() * 2
 yl = torch.empty_like(xl)
 ms = t(lambda: yl.copy_(xl))
 res["copy_1600"] = {"us": round(ms * 1e3, 1), "TBps": round(2 * xl.numel() * 2 / ms / 1e9, 2)}
-os.environ["SMP_GELU_FLAT"] = "1"
 ms = t(lambda: gelu.bias_gelu(x, b))
 res["ops.bias_gelu_flat"] = {"us": round(ms * 1e3, 1), "TBps": round(nb / ms / 1e9, 2)}
 ref = torch.nn.functional.gelu(x.float() + b.float(), approximate="tanh")
