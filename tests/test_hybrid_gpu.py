@@ -47,3 +47,17 @@ def test_sharded_dp2_gpu():
 def test_tp2_sharded_activation_offload_gpu():
     _run(2, 1, 2, 2, extra={"ckpt_layers": True,
                             "cfg": {"offload_activations": True, "_shard_offloaded_activations": True}})
+
+
+def test_gptj6b_width_tp4_gpu():
+    """BASELINE config 3's architecture at full width -- GPT-J 6B: h 4096, 16 heads x 256,
+    rotary (64 dims), parallel attention + MLP, untied LM head with bias -- 2 layers at TP=4
+    (four ranks on the one GPU), fp32 against the unpartitioned model."""
+    _run(4, 1, 4, 2, extra={"base": "gptj-6b"})
+
+
+def test_gptneox20b_width_pp2_tp2_gpu():
+    """BASELINE config 4's architecture at full width -- GPT-NeoX 20B: h 6144, 64 heads x 96,
+    NeoX-style rotary (24 dims), parallel attention -- 2 layers at PP2 x TP2 with optimizer-
+    state sharding over the DP group it spans (config 4 shards it across DP)."""
+    _run(4, 2, 2, 2, extra={"base": "gptneox-20b", "cfg": {"shard_optimizer_state": True}}, env={"SMP_P2P": "ipc"})

@@ -24,17 +24,21 @@ def main():
         cfg["default_partition"] = 0
     cfg.update(extra.get("cfg", {}))
     torch.manual_seed(123)
-    kw = dict(num_layers=4, hidden_size=64, num_attention_heads=4, attention_head_size=16, intermediate_size=128,
-              vocab_size=96, num_positions=32)
+    base = extra.get("base", "gpt2-tiny")
+    if base == "gpt2-tiny":
+        kw = dict(num_layers=4, hidden_size=64, num_attention_heads=4, attention_head_size=16, intermediate_size=128,
+                  vocab_size=96, num_positions=32)
+    else:  # a BASELINE architecture at full width, few layers, small vocabulary
+        kw = dict(num_layers=2, vocab_size=1024, num_positions=64)
     kw.update(extra.get("model", {}))
-    ref = build_gpt("gpt2-tiny", dropout=0.0, **kw)  # built before init: unsharded reference
+    ref = build_gpt(base, dropout=0.0, **kw)  # built before init: unsharded reference
     smp.init(cfg)
     dev = smp.state.device  # GPU runs (tests/test_hybrid_gpu.py): every rank on the box's one GPU
     ref.to(dev)
     delayed = bool(extra.get("delayed"))
     with smp.delay_param_initialization(enabled=delayed):
         with smp.model_creation(tensor_parallelism=tp > 1):
-            net = build_gpt("gpt2-tiny", dropout=0.0, **kw)
+            net = build_gpt(base, dropout=0.0, **kw)
     if delayed:
         assert all(p.is_meta for p in net.parameters())
     elif tp == 1:
