@@ -35,8 +35,8 @@ import torch.nn.functional as F
 from ._ext import ext
 from .linear import _WT_EPOCH, _fusable
 
-# LM-head weight gradient on the MFMA weight-gradient kernel (SMP_LM_HEAD_WGRAD_KERNEL, default on)
-_WGRAD_KERNEL = os.environ.get("SMP_LM_HEAD_WGRAD_KERNEL", "1") != "0"
+# LM-head weight gradient on the MFMA weight-gradient kernel (bf16 operands)
+_WGRAD_KERNEL = True
 
 _ALIGN = 64
 _ENABLED = os.environ.get("SMP_PADDED_LM_HEAD", "0") == "1"

@@ -4,8 +4,7 @@ The reference sends every TP all-reduce to NCCL (`smp/torch/nn/utils.py:548,570`
 `nn/layer_norm.py:41-79`, `nn/cross_entropy.py:34-66`).  For the small ones -- per-row
 statistics of the distributed LayerNorm and the vocab-parallel cross entropy, small-batch
 activations -- a ring all-reduce over xGMI is latency-bound (2 (n-1) link hops).  Here
-messages up to ``SMP_ONESHOT_ALLREDUCE_MAX_BYTES`` (default 1 MiB) on TP groups of at most
-``SMP_ONESHOT_ALLREDUCE_MAX_RANKS`` (default 4) ranks on one node go to the native
+messages up to 1 MiB on TP groups of at most 4 ranks on one node go to the native
 ``IpcAllReduce`` (`csrc/torchrt/ipc_allreduce.cpp`): one kernel, every rank reads every
 peer's registered buffer over xGMI once and reduces in rank order (bitwise-identical results
 on every rank, as TP requires).  Larger messages, other dtypes and CPU tensors take the
@@ -41,8 +40,8 @@ from ..backend.logger import get_logger
 logger = get_logger()
 
 _MODE = os.environ.get("SMP_ONESHOT_ALLREDUCE", "auto")
-_MAX_BYTES = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_BYTES", str(1 << 20)))
-_MAX_RANKS = int(os.environ.get("SMP_ONESHOT_ALLREDUCE_MAX_RANKS", "4"))
+_MAX_BYTES = 1 << 20  # larger messages: RCCL (bandwidth-bound, ring over xGMI)
+_MAX_RANKS = 4  # one-shot reads every peer's slot: cost grows with the group
 _TIMEOUT_S = float(os.environ.get("SMP_ONESHOT_ALLREDUCE_TIMEOUT_S", "600"))
 _DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 

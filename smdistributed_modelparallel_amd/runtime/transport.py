@@ -352,7 +352,7 @@ class PipelineTransport:
         if not self._held:
             return
         if release_timeout is None:
-            release_timeout = float(os.environ.get("SMP_P2P_RELEASE_WAIT_S", "30"))
+            release_timeout = 30.0
         import time
 
         deadline = time.monotonic() + release_timeout

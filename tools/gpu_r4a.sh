@@ -16,3 +16,4 @@ timeout -k 10 300 python bench.py --steps 6 --warmup 3 > gpurun_out/r4a/bench.lo
 tail -1 gpurun_out/r4a/bench.log
 timeout -k 10 300 python tools/wgrad_table.py > gpurun_out/r4a/wgrad_table.jsonl 2>&1 || { tail -5 gpurun_out/r4a/wgrad_table.jsonl; exit 1; }
 tail -1 gpurun_out/r4a/wgrad_table.jsonl
+timeout -k 10 300 python tools/kvariant_time.py intree abtest/_C_wg_prio.so abtest/_C_wg_tk32ns4.so abtest/_C_wg_tk32ns3.so abtest/_C_wg_tk32ns4prio.so 2>&1 | grep -v "^\[\|amdgpu.ids" || exit 1
