@@ -252,18 +252,19 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // padded by the compiler and read stale values on some waves -- non-deterministic maxima).
 __device__ __forceinline__ float max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
-// max / sum of x over the lane pair (lane, lane ^ 32): the swap leaves the lower half's x in
-// one result and the upper half's in the other on every lane, so no lane select is needed
-__device__ __forceinline__ float pair_max32(float x) {
+// value of lane ^ 32 (the other half-wave) without an LDS round trip.  The lane select is
+// needed: with both operands the same value, hipcc may give the swap one register, and then
+// each output holds only the OTHER half's value (measured: max / sum over r[0], r[1] without
+// the select returned 2x the other half's sum -- wrong softmax normalisers).
+__device__ __forceinline__ float xor32(float x) {
   const unsigned u = __builtin_bit_cast(unsigned, x);
   auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return fmaxf(__builtin_bit_cast(float, r[0]), __builtin_bit_cast(float, r[1]));
+  const int lane = threadIdx.x & 63;
+  return __builtin_bit_cast(float, lane < 32 ? r[1] : r[0]);
 }
-__device__ __forceinline__ float pair_sum32(float x) {
-  const unsigned u = __builtin_bit_cast(unsigned, x);
-  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-  return __builtin_bit_cast(float, r[0]) + __builtin_bit_cast(float, r[1]);
-}
+// max / sum of x over the lane pair (lane, lane ^ 32)
+__device__ __forceinline__ float pair_max32(float x) { return fmaxf(x, xor32(x)); }
+__device__ __forceinline__ float pair_sum32(float x) { return x + xor32(x); }
 
 // Register-staged tile copy (issue global loads early, write LDS late: the HBM/L2 latency
 // hides under the MFMA work of the current tile).
@@ -432,6 +433,34 @@ __device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbas
   }
 }
 
+// ------------------------------------------------------------ stored keep bits
+// The forward hashes each element's dropout decision once and stores it as 1 bit: per (b h,
+// query row q, 64-key tile t, half-wave hh) one uint32 at ((bh * ntiles + t) * sq + q) * 2 + hh
+// whose bit 16 s + reg is the decision of key 64 t + 32 s + acc_row(reg, hh) -- exactly the
+// registers a query-on-lane wave holds, so the forward writes and dQ reads one coalesced
+// dword per lane per tile, and dK/dV stages a block's words through LDS.  The backward then
+// never regenerates the hash (~100 VALU per 64-key tile per lane).
+__device__ __forceinline__ int64_t bits_index(int64_t bh, int ntiles, int tile, int sq, int q, int hh) {
+  return ((bh * ntiles + tile) * static_cast<int64_t>(sq) + q) * 2 + hh;
+}
+
+// 4 keep flags (bits 7, 15, 23, 31 of a keep_flags word) -> a 4-bit nibble in bits 0-3
+__device__ __forceinline__ uint32_t flag_nibble(uint32_t f) { return ((f & 0x80808080u) * 0x00204081u) >> 28; }
+
+// the lane's 32 keep bits of a tile from the 8 keep words of its two 32-key halves
+__device__ __forceinline__ uint32_t pack_keep(const uint32_t (&f0)[4], const uint32_t (&f1)[4]) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) w |= (flag_nibble(f0[g]) << (4 * g)) | (flag_nibble(f1[g]) << (16 + 4 * g));
+  return w;
+}
+
+// Dropped entries of a transposed fp32 tile (32-key half u of a stored word) become +0
+__device__ __forceinline__ void drop_tile_bits(f32x16& a, uint32_t w, int u) {
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) a[reg] = and_mask(a[reg], bit_mask(w, static_cast<uint32_t>(16 * u + reg)));
+}
+
 // LDS-DMA of one K or V tile (BN rows x D, D = 64 / 128: the LDS image is exactly [BN][D]):
 // each wave-instruction fills 1 KB = 1024 / (2 D) consecutive rows, lane-linear, so the
 // row's XOR swizzle moves to the SOURCE chunk (physical chunk pc of row r holds logical
@@ -511,6 +540,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
   const int sq = static_cast<int>(p.sq), sk = static_cast<int>(p.sk);
   const int diag = sk - sq;  // key index allowed up to query + diag
   const int win = p.window;
+  const int ntiles64 = (sk + 63) >> 6;
 
   const uint16_t* Q = static_cast<const uint16_t*>(p.q) + b * p.q_sb + h * p.q_sh;
   const uint16_t* K = static_cast<const uint16_t*>(p.k) + b * p.k_sb + h * p.k_sh;
@@ -683,6 +713,8 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       uint32_t f0[4], f1[4];
       drop_words(f0, dkey, qbase, kv0, hh, d0.xr, d0.c);
       drop_words(f1, dkey, qbase, kv0 + 32, hh, d1.xr, d1.c);
+      if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
+        p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
       pf[0] = drop_packed(pf[0], f0[0], f0[1]);
       pf[1] = drop_packed(pf[1], f0[2], f0[3]);
       pf[2] = drop_packed(pf[2], f1[0], f1[1]);
@@ -738,6 +770,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   __shared__ __attribute__((aligned(16))) uint16_t sQ[BQ * DS];
   __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * DS];
   __shared__ __attribute__((aligned(16))) float sL[BQ], sDl[BQ];
+  // keep bits of the Q tile x the block's 128 keys: [64-key half][word half-wave][query]
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[DROP ? 4 * BQ : 4];
   const AttnParams& p = P.f;
   // wave index as a scalar: every wave-derived tile condition (causal / window / edge) then
   // branches on SGPRs instead of being if-converted into per-lane selects on every tile
@@ -785,18 +819,22 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   const float kbias_raw = BIAS ? load_bias(p, b, krow) : 0.f;
   float kbias = 0.f;
   bool blk_bias = false;  // this wave's 32 keys carry a bias
-  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
-  // dropout: the 4 lanes of a key quad (keys 4j..4j+3 = lanes with the same lane >> 2) share
-  // one hash per query; quad position qp hashes query registers 4 qp .. 4 qp + 3 (inputs
-  // q * nquads + key quad, the query part of each a per-lane constant plus qs * nquads)
-  const uint32_t nquads = static_cast<uint32_t>((sk + 3) >> 2);
-  const int qp = lane & 3;
-  uint32_t hin[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    hin[i] = static_cast<uint32_t>(acc_row(4 * qp + i, hh)) * nquads + static_cast<uint32_t>(krow >> 2);
-  const uint32_t kbit = 8u * static_cast<uint32_t>(qp) + 7u;  // this key's flag bit in a keep word
+  // dropout: the forward's keep bits (kDropBits layout).  This lane's key kr = krow & 31 in
+  // 32-key half s = wave & 1 of 64-key tile kb * 2 + wave / 2 is bit 16 s + 4 (kr >> 3) +
+  // (kr & 3) of the words with half-wave index (kr >> 2) & 1.  Thread t stages word
+  // (tile half t >> 7, query (t >> 1) & 63, half-wave t & 1) of each Q tile (coalesced 512 B
+  // runs) into sBits[(t >> 7) * 2 + (t & 1)][query].
+  const int ntiles64 = (sk + 63) >> 6;
+  const uint32_t kbit = 16u * static_cast<uint32_t>(wave & 1) + 4u * static_cast<uint32_t>(r >> 3) +
+                        static_cast<uint32_t>(r & 3);
+  const int bits_row = ((wave >> 1) * 2 + ((r >> 2) & 1)) * BQ;  // this lane's sBits row
+  const int st_tile = kb * 2 + static_cast<int>(threadIdx.x >> 7), st_q = (threadIdx.x >> 1) & 63;
+  const int st_hh = threadIdx.x & 1;
+  uint32_t bits_stage = 0u;
+  auto load_bits = [&](int qt) {
+    const int qq = qt + st_q;
+    bits_stage = qq < sq && st_tile < ntiles64 ? p.drop_bits[bits_index(bh, ntiles64, st_tile, sq, qq, st_hh)] : 0u;
+  };
   const uint32_t rsd_bits = __builtin_bit_cast(uint32_t, p.drop_rs);
   int q_start = 0, q_end = sq;
   if (CAUSAL) {
@@ -819,6 +857,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       l_stage = qq < sq ? LSE[qq] : 0.f;
       d_stage = qq < sq ? DL[qq] : 0.f;
     }
+    if (DROP) load_bits(q_start);
   }
   const int klast = k0w + 31;
   // 64-query tiles: this wave's visible tiles [tv0, tv1) and mask-free tiles [ti0, ti1) (tile
@@ -843,6 +882,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       sL[threadIdx.x] = l_stage == -INFINITY ? 0.f : -l_stage * kLog2e * inv_sl2;
       sDl[threadIdx.x] = -d_stage;
     }
+    if (DROP) sBits[((threadIdx.x >> 7) * 2 + (threadIdx.x & 1)) * BQ + ((threadIdx.x >> 1) & 63)] = bits_stage;
     __syncthreads();
     if (BIAS) {
       kbias = kbias_raw * (1.f / p.scale);
@@ -856,6 +896,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         l_stage = qq < sq ? LSE[qq] : 0.f;
         d_stage = qq < sq ? DL[qq] : 0.f;
       }
+      if (DROP) load_bits(qt + BQ);
     }
   };
   // one 32-query sub-step (queries qs .. qs + 31 = LDS rows 32 sub ..)
@@ -899,16 +940,12 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
       for (int j = 0; j < 16; ++j) s[j] += kbias;
     }
-    // Dropout decisions of the lane's key for the 16 query registers: this lane hashes
-    // query registers 4 qp + i (keep flags of the quad's 4 keys in one word each), and the
-    // word of register j comes from quad lane j / 4 by a DPP broadcast -- 4 hashes per lane
-    // instead of 16, the same random stream as the forward and the dQ kernel.
-    uint32_t kf4[4] = {0u, 0u, 0u, 0u};
+    // the forward's keep words of the 16 query registers (query 32 sub + 8 g + 4 hh + i):
+    // four 16-byte LDS reads (4 distinct addresses per wave: broadcasts)
+    uint4 kw[4];
     if (DROP) {
-      const DropThr dt = drop_block_thr(p, bkey, static_cast<uint32_t>(qs >> 5), static_cast<uint32_t>(k0w >> 5));
-      const uint32_t qsn = static_cast<uint32_t>(qs) * nquads;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) kf4[i] = keep_flags(mix32(dkey ^ (qsn + hin[i])), dt.xr, dt.c);
+      for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(&sBits[bits_row + 32 * sub + 8 * g + 4 * hh]);
     }
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -918,8 +955,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win)) pv = 0.f;
       }
       if (DROP) {
-        // register reg = 4 j + i: word i of quad lane j (quad_perm [j, j, j, j])
-        const uint32_t w = quad_bcast(kf4[reg & 3], reg >> 2);
+        const uint4 w4 = kw[reg >> 2];
+        const uint32_t w = (reg & 3) == 0 ? w4.x : (reg & 3) == 1 ? w4.y : (reg & 3) == 2 ? w4.z : w4.w;
         const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
         s[reg] = pv * z;                             // (P o Z) for dV
         dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
@@ -1059,9 +1096,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     dl = pair_sum32(part);
     if (col0 == 0 && hh == 0 && qrow < sq) P.delta[bh * p.sq + qrow] = dl;
   }
-  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
-  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
+  const int ntiles64 = (sk + 63) >> 6;
   const float rsd = p.drop_rs;
   f32x16 dq[DO / 32];
 #pragma unroll
@@ -1118,6 +1153,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   auto body = [&](int t, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
     const int kv0 = kv_begin + t * BN;
+    const uint32_t kbits = DROP && qrow < sq ? P.f.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] : 0u;
     // D <= 128: both 32-key halves' dS^T, then the dQ MFMAs (the two halves' MFMA chains
     // overlap each other's softmax VALU work).  D = 256: half by half, so only one half's
     // S / dP accumulators are live next to the 16 Q / dO fragments.
@@ -1143,9 +1179,9 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
       if (BIAS && tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       if (DROP) {
-        // dp <- keep o dP (raw), then dS = P o (dP o keep / (1 - p) - delta)
-        const DropThr dt = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + u);
-        drop_tile(dp[u], dkey, qbase, kv0 + 32 * u, hh, dt.xr, dt.c);
+        // dp <- keep o dP (raw), then dS = P o (dP o keep / (1 - p) - delta); the keep bits
+        // are the forward's (loaded with the tile, one dword per lane)
+        drop_tile_bits(dp[u], kbits, u);
       }
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {

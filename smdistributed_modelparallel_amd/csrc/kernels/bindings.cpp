@@ -695,17 +695,33 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
   p.o = o.data_ptr();
   p.o_sb = o.stride(0), p.o_ss = o.stride(1), p.o_sh = o.stride(2);
   p.lse = lse.data_ptr<float>();
+  // dropout: the keep bits for the backward (1 bit per score: b h sq sk / 8 bytes)
+  at::Tensor bits;
+  if (p.drop_on) {
+    bits = at::empty({p.b * p.h, (p.sk + 63) / 64, p.sq, 2}, q.options().dtype(at::kInt));
+    p.drop_bits = reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>());
+  } else {
+    bits = at::empty({0}, q.options().dtype(at::kInt));
+  }
   check(smpk::attention_fwd(dt_code(q), p, stream()), "attention_fwd");
-  return {o, lse};
+  return {o, lse, bits};
 }
 
 // Writes into the provided dq/dk/dv (may be views of one packed gradient buffer).
 void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
                         at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window,
                         c10::optional<at::Tensor> kbias, double dropout_p,
-                        int64_t seed, int64_t offset) {
+                        int64_t seed, int64_t offset, c10::optional<at::Tensor> drop_bits) {
   smpk::AttnBwdParams P{};
   P.f = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
+  if (P.f.drop_on) {
+    TORCH_CHECK(drop_bits.has_value() && drop_bits->defined(), "attention_bwd: dropout needs the forward's keep bits");
+    const at::Tensor& bt = *drop_bits;
+    TORCH_CHECK(bt.is_cuda() && bt.scalar_type() == at::kInt && bt.is_contiguous() &&
+                    bt.numel() == P.f.b * P.f.h * ((P.f.sk + 63) / 64) * P.f.sq * 2,
+                "attention_bwd: keep bits must be the forward's int32 [b h, ceil(sk / 64), sq, 2] tensor");
+    P.f.drop_bits = reinterpret_cast<uint32_t*>(bt.data_ptr<int32_t>());
+  }
   check_bshd(dout, "dout");
   check_bshd(o, "o");
   check_bshd(dq, "dq");
@@ -788,5 +804,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
-        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("drop_bits") = py::none());
 }

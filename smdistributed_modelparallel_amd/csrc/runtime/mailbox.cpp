@@ -43,7 +43,9 @@ void write_all(int fd, const char* p, size_t n) {
   }
 }
 
-// Returns false on orderly EOF before any byte was read.
+// Returns false on EOF before any byte was read -- an orderly close, or a reset (a peer that
+// exits with unread bytes in its receive queue sends RST instead of FIN): both are "the peer
+// left", and the caller tells a shutdown from a death by the goodbye it did or did not send.
 bool read_all(int fd, char* p, size_t n) {
   size_t got = 0;
   while (got < n) {
@@ -54,6 +56,7 @@ bool read_all(int fd, char* p, size_t n) {
     }
     if (r < 0) {
       if (errno == EINTR) continue;
+      if (errno == ECONNRESET && got == 0) return false;
       throw std::runtime_error(std::string("mailbox recv failed: ") + strerror(errno));
     }
     got += static_cast<size_t>(r);

@@ -133,8 +133,8 @@ class _FlashAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, scale, causal, window, kb, dropout_p):
         seed, off = dropout_seed_offset(q.device) if dropout_p > 0.0 else (0, 0)
         bias = kb.bias if kb is not None else None
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
-        ctx.save_for_backward(q, k, v, o, lse)
+        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        ctx.save_for_backward(q, k, v, o, lse, bits)
         ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
         ctx.drop = (dropout_p, seed, off)
@@ -142,13 +142,13 @@ class _FlashAttention(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
-        q, k, v, o, lse = ctx.saved_tensors
+        q, k, v, o, lse, bits = ctx.saved_tensors
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         p, seed, off = ctx.drop
         kb = ctx.kb
         bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
-                                 bias, p, seed, off)
+                                 bias, p, seed, off, bits if p > 0.0 else None)
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -161,8 +161,8 @@ class _FlashAttentionPacked(torch.autograd.Function):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
         bias = kb.bias if kb is not None else None
-        o, lse = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        ctx.save_for_backward(qkv, o, lse, bits)
         ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
         ctx.drop = (dropout_p, seed, off)
@@ -170,13 +170,14 @@ class _FlashAttentionPacked(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, bits = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
         p, seed, off = ctx.drop
         kb = ctx.kb
         bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
-                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off)
+                                 dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off,
+                                 bits if p > 0.0 else None)
         return dqkv, None, None, None, None, None
 
 

@@ -151,7 +151,10 @@ def _wgrad_native_ok(g, dy2, x2):
 # GPT-2 XL (T = 65536, profiles/r2/session4_wgrad_pick_ab.md, profiles/r3/wgrad_variants.md);
 # (4800, 1600): s7 in the b32 step with the fused bias sums (1092-1099 us vs s5 1131, s8 1167).
 # BASELINE config 3-5 rank shapes (scaled-batch TP): tools/wgrad_table.py, profiles/r4/.
-_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7}
+_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7,
+                 # GPT-J TP4 attention output (T = 16384): s4 137 us vs library 168 us; GPT-NeoX
+                 # TP4 QKV: s1 959 vs 1034 us; the other config 3-5 shapes measured library-best
+                 (4096, 1024): 4, (4608, 6144): 1}
 # kernel split count for a library-table shape when the fused bias pass makes the kernel the choice
 _WGRAD_STATIC_KERNEL = {(1600, 6400): 4}
 _WGRAD_PICK = os.environ.get("SMP_WGRAD_PICK", "table")

@@ -33,7 +33,11 @@ def _run(make, dtype, steps=3):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("adamw", [True, False])
 def test_fused_adam_multi_tensor(dtype, adamw):
-    _run(lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.05, adam_w_mode=adamw), dtype)
+    # weight decay 0.0123, not a round number: with 0.05 some bf16 (g, p) pairs have g / p = -4/5
+    # * 2^-4 exactly, so the L2 gradient g + 0.05f p is 0 on the CPU (product rounded first) and
+    # ~1e-9 on the GPU (fused multiply-add) -- below eps = 1e-8 the Adam step then differs by
+    # ~0.1 lr on those few elements (tools/opt_debug.py: 5 of 310K), a rounding artefact
+    _run(lambda ps: FusedAdam(ps, lr=1e-2, weight_decay=0.0123, adam_w_mode=adamw), dtype)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

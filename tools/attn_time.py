@@ -35,27 +35,22 @@ def t(fn, it=20):
 b, s, h, d = 32, 2048, 25, 64
 qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=torch.bfloat16)
 q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-o, lse = C.attention_fwd(q, k, v, 0.125, True, 0)
+o, lse = C.attention_fwd(q, k, v, 0.125, True, 0)[:2]
 do = torch.randn_like(o)
 dqkv = torch.empty_like(qkv)
 zb = torch.zeros(b, s, device="cuda")
 def drop_times():
-    """dropout 0.1: hash-regenerating backward, and (new builds) forward-stored keep bits."""
+    """dropout 0.1: round-3 builds regenerate the keep hash in the backward; round-4 builds
+    store the forward's keep bits (a third output) and the backward reads them."""
     out = {}
     args = (q, k, v, 0.125, True, 0, None, 0.1, 1234, 0)
-    o1, lse1 = C.attention_fwd(*args)[:2]
+    res = C.attention_fwd(*args)
+    extra = {"drop_bits": res[2]} if len(res) > 2 else {}
     out["fwd_drop_us"] = round(t(lambda: C.attention_fwd(*args)), 1)
-    out["bwd_drop_hash_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, o1, lse1, dqkv[:, :, 0], dqkv[:, :, 1],
-                                                                   dqkv[:, :, 2], 0.125, True, 0, None, 0.1, 1234, 0)), 1)
-    try:
-        res = C.attention_fwd(*args, True)
-    except TypeError:
-        return out
-    mask = res[2]
-    out["fwd_drop_store_us"] = round(t(lambda: C.attention_fwd(*args, True)), 1)
-    out["bwd_drop_bits_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, res[0], res[1], dqkv[:, :, 0],
-                                                                   dqkv[:, :, 1], dqkv[:, :, 2], 0.125, True, 0, None,
-                                                                   0.1, 1234, 0, mask)), 1)
+    out["bwd_drop_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, res[0], res[1], dqkv[:, :, 0], dqkv[:, :, 1],
+                                                              dqkv[:, :, 2], 0.125, True, 0, None, 0.1, 1234, 0,
+                                                              **extra)), 1)
+    out["keep_bits"] = bool(extra)
     return out
 
 

@@ -1,10 +1,13 @@
 """Time the weight-gradient kernel of several `_C` builds (paths in argv; "intree" = the
 in-tree build) on the GPT-2 XL step shapes at T = 65536 with the table's split counts and the
-in-step fused bias sums; builds interleaved, best of `rounds`.  One JSON line per build."""
+in-step fused bias sums; best of 3 rounds, builds interleaved round by round, each (build,
+round) in its own child process (two builds cannot share one process: both register the same
+pybind types).  One JSON line per build."""
 import importlib.machinery
 import importlib.util
 import json
 import os
+import subprocess
 import sys
 
 import torch
@@ -27,33 +30,50 @@ def load(path):
 T = 65536
 SHAPES = {"qkv": (4800, 1600, 7, True), "proj": (1600, 1600, 5, True), "fc1": (6400, 1600, 4, True),
           "fc2_kernel_s4": (1600, 6400, 4, False)}
+
+def time_build(C):
+    out = {}
+    for name, (dy, x, g, bias, sp, fl) in ops.items():
+        fn = lambda: C.wgrad_(g, dy, x, True, sp, bias, True)  # noqa: E731
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            fn()
+        e.record()
+        e.synchronize()
+        out[name] = s.elapsed_time(e) / 10 * 1e3
+    return out
+
+
+if len(sys.argv) == 3 and sys.argv[1] == "--child":
+    ops = {}
+    for name, (n, k, sp, db) in SHAPES.items():
+        dy = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
+        x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
+        g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
+        bias = torch.zeros(n, device="cuda", dtype=torch.bfloat16) if db else None
+        ops[name] = (dy, x, g, bias, sp, 2.0 * T * n * k)
+    print("RESULT " + json.dumps(time_build(load(sys.argv[2]))), flush=True)
+    sys.exit(0)
+
 builds = sys.argv[1:] or ["intree"]
-mods = {b: load(b) for b in builds}
-ops = {}
-for name, (n, k, sp, db) in SHAPES.items():
-    dy = torch.randn(T, n, device="cuda", dtype=torch.bfloat16)
-    x = torch.randn(T, k, device="cuda", dtype=torch.bfloat16)
-    g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
-    bias = torch.zeros(n, device="cuda", dtype=torch.bfloat16) if db else None
-    ops[name] = (dy, x, g, bias, sp, 2.0 * T * n * k)
 best = {b: {} for b in builds}
 for rnd in range(3):
-    for b, C in mods.items():
-        for name, (dy, x, g, bias, sp, fl) in ops.items():
-            fn = lambda: C.wgrad_(g, dy, x, True, sp, bias, True)  # noqa: E731
-            for _ in range(2):
-                fn()
-            torch.cuda.synchronize()
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(10):
-                fn()
-            e.record()
-            e.synchronize()
-            us = s.elapsed_time(e) / 10 * 1e3
-            best[b][name] = min(best[b].get(name, 1e30), us)
+    for b in builds:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", b], capture_output=True, text=True,
+                           timeout=240)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+        if r.returncode != 0 or not line:
+            print(r.stdout[-2000:], r.stderr[-2000:], flush=True)
+            sys.exit(r.returncode or 1)
+        for k, v in json.loads(line[0][7:]).items():
+            best[b][k] = min(best[b].get(k, 1e30), v)
 for b in builds:
     tot = best[b]["qkv"] + best[b]["proj"] + best[b]["fc1"]
+    fl = {name: 2.0 * T * n * k for name, (n, k, _, _) in SHAPES.items()}
     print(json.dumps({"build": b, **{k: round(v, 1) for k, v in best[b].items()},
-                      "tflops": {k: round(ops[k][5] / v / 1e6, 1) for k, v in best[b].items()},
+                      "tflops": {k: round(fl[k] / v / 1e6, 1) for k, v in best[b].items()},
                       "qkv+proj+fc1_us": round(tot, 1)}), flush=True)
