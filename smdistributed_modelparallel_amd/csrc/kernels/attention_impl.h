@@ -43,6 +43,7 @@ namespace smpk {
 namespace attn {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -102,21 +103,6 @@ __device__ __forceinline__ uint32_t bit_mask(uint32_t f, uint32_t bit) {
   return static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(f), bit, 1u));
 }
 
-// lane 4 (lane / 4) + j's v, for every lane of the quad (DPP quad_perm [j, j, j, j]); j is a
-// compile-time constant after unrolling
-__device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int j) {
-  const int x = static_cast<int>(v);
-  switch (j) {
-    case 0:
-      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0x00, 0xF, 0xF, true));
-    case 1:
-      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0x55, 0xF, 0xF, true));
-    case 2:
-      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0xAA, 0xF, 0xF, true));
-    default:
-      return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0xFF, 0xF, 0xF, true));
-  }
-}
 
 __device__ __forceinline__ float and_mask(float x, uint32_t m) {
   return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m);
@@ -240,6 +226,20 @@ __device__ __forceinline__ typename MF<T>::e8 pack8(const f32x16& a, int s) {
   typename MF<T>::e8 r;
 #pragma unroll
   for (int j = 0; j < 8; ++j) r[j] = MF<T>::cvt(a[8 * s + j]);
+  return r;
+}
+
+// The same from the register pairs (2j, 2j + 1) of a pair array: one v_cvt_pk per pair, no
+// cross-pair shuffles (element-wise code written on f32x2 pairs keeps hipcc's packed fp32 ops
+// and the conversions on the same pairing)
+template <typename T>
+__device__ __forceinline__ typename MF<T>::e8 pack8p(const f32x2 (&a)[8], int s) {
+  typename MF<T>::e8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[2 * j] = MF<T>::cvt(a[4 * s + j].x);
+    r[2 * j + 1] = MF<T>::cvt(a[4 * s + j].y);
+  }
   return r;
 }
 
@@ -419,19 +419,6 @@ __device__ __forceinline__ E drop_packed(E v, uint32_t f0, uint32_t f1) {
   return __builtin_bit_cast(E, w);
 }
 
-// Dropped entries of a transposed fp32 tile become +0 (kept ones keep their value; the
-// 1 / keep-probability factor is applied by the caller).
-__device__ __forceinline__ void drop_tile(f32x16& a, uint32_t key, uint32_t qbase, int kbase, int hh, uint32_t xr,
-                                          uint32_t c) {
-  uint32_t f[4];
-  drop_words(f, key, qbase, kbase, hh, xr, c);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const uint32_t sh = f[g] << 8;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[4 * g + i] = and_mask(a[4 * g + i], elem_mask(f[g], sh, i));
-  }
-}
 
 // ------------------------------------------------------------ stored keep bits
 // The forward hashes each element's dropout decision once and stores it as 1 bit: per (b h,
@@ -455,11 +442,6 @@ __device__ __forceinline__ uint32_t pack_keep(const uint32_t (&f0)[4], const uin
   return w;
 }
 
-// Dropped entries of a transposed fp32 tile (32-key half u of a stored word) become +0
-__device__ __forceinline__ void drop_tile_bits(f32x16& a, uint32_t w, int u) {
-#pragma unroll
-  for (int reg = 0; reg < 16; ++reg) a[reg] = and_mask(a[reg], bit_mask(w, static_cast<uint32_t>(16 * u + reg)));
-}
 
 // LDS-DMA of one K or V tile (BN rows x D, D = 64 / 128: the LDS image is exactly [BN][D]):
 // each wave-instruction fills 1 KB = 1024 / (2 D) consecutive rows, lane-linear, so the
@@ -661,6 +643,28 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       s0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qt, s0);
       s1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * DS), qt, s1);
     }
+    // While the S MFMAs run: the dropout hashes (independent of S) and, D = 64, the V operand
+    // fragments of this tile's PV MFMAs (their LDS latency then hides under the softmax
+    // instead of stalling each PV MFMA; +32 VGPRs, occupancy unchanged)
+    uint32_t f0[4], f1[4];
+    if (DROP) {
+      const DropThr d0 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5));
+      const DropThr d1 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + 1);
+      drop_words(f0, dkey, qbase, kv0, hh, d0.xr, d0.c);
+      drop_words(f1, dkey, qbase, kv0 + 32, hh, d1.xr, d1.c);
+      if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
+        p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
+    }
+    constexpr bool VPRE = D == 64 && !BIAS;
+    typename MF<T>::e8 vfr[VPRE ? D / 32 : 1][4];
+    if constexpr (VPRE) {
+#pragma unroll
+      for (int i = 0; i < D / 32; ++i) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) vfr[i][s] = ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (BIAS && tile_bias) {
       add_from_keys(s0, sB, hh);
       add_from_keys(s1, sB + 32, hh);
@@ -695,26 +699,27 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       m_i = m_new;
       m_use = mu;
     }
-    float rs0 = 0.f, rs1 = 0.f;
+    // p = exp2(S sl2 - m): exponent arguments two at a time (v_pk_fma_f32), packed row sums
+    const f32x2 sl2v = {sl2, sl2}, nm = {-m_use, -m_use};
+    f32x2 rs0 = {0.f, 0.f}, rs1 = {0.f, 0.f};
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const float e0 = fast_exp2(fmaf(s0[reg], sl2, -m_use));
-      const float e1 = fast_exp2(fmaf(s1[reg], sl2, -m_use));
-      s0[reg] = e0;
-      s1[reg] = e1;
-      rs0 += e0;
-      rs1 += e1;
+    for (int reg = 0; reg < 16; reg += 2) {
+      f32x2 a0 = {s0[reg], s0[reg + 1]}, a1 = {s1[reg], s1[reg + 1]};
+      a0 = __builtin_elementwise_fma(a0, sl2v, nm);
+      a1 = __builtin_elementwise_fma(a1, sl2v, nm);
+      a0 = f32x2{fast_exp2(a0.x), fast_exp2(a0.y)};
+      a1 = f32x2{fast_exp2(a1.x), fast_exp2(a1.y)};
+      s0[reg] = a0.x;
+      s0[reg + 1] = a0.y;
+      s1[reg] = a1.x;
+      s1[reg + 1] = a1.y;
+      rs0 += a0;
+      rs1 += a1;
     }
-    l_i += rs0 + rs1;
+    rs0 += rs1;
+    l_i += rs0.x + rs0.y;
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
-      const DropThr d0 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5));
-      const DropThr d1 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + 1);
-      uint32_t f0[4], f1[4];
-      drop_words(f0, dkey, qbase, kv0, hh, d0.xr, d0.c);
-      drop_words(f1, dkey, qbase, kv0 + 32, hh, d1.xr, d1.c);
-      if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
-        p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
       pf[0] = drop_packed(pf[0], f0[0], f0[1]);
       pf[1] = drop_packed(pf[1], f0[2], f0[3]);
       pf[2] = drop_packed(pf[2], f1[0], f1[1]);
@@ -723,8 +728,12 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
+      for (int s = 0; s < 4; ++s) {
+        if constexpr (VPRE)
+          o[i] = MF<T>::mma(vfr[i][s], pf[s], o[i]);
+        else
+          o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
+      }
     }
   };
   int t = 0;
@@ -947,27 +956,39 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
       for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(&sBits[bits_row + 32 * sub + 8 * g + 4 * hh]);
     }
+    // element-wise on register pairs (2j, 2j + 1): packed fp32 multiplies / FMAs
+    f32x2 po[8], dso[8];
+    const f32x2 sl2v = {sl2, sl2};
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      float pv = fast_exp2(s[reg] * sl2);
+    for (int j = 0; j < 8; ++j) {
+      const int reg = 2 * j;
+      const f32x2 sa = f32x2{s[reg], s[reg + 1]} * sl2v;
+      f32x2 pv = {fast_exp2(sa.x), fast_exp2(sa.y)};
       if constexpr (MASK) {
-        const int qq = qs + acc_row(reg, hh);
-        if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win)) pv = 0.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int qq = qs + acc_row(reg + e, hh);
+          if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win))
+            pv[e] = 0.f;
+        }
       }
+      const f32x2 dpv = {dp[reg], dp[reg + 1]};
       if (DROP) {
+        // keep / (1 - p) or 0 from the forward's bits (words reg, reg + 1 of group reg / 4)
         const uint4 w4 = kw[reg >> 2];
-        const uint32_t w = (reg & 3) == 0 ? w4.x : (reg & 3) == 1 ? w4.y : (reg & 3) == 2 ? w4.z : w4.w;
-        const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
-        s[reg] = pv * z;                             // (P o Z) for dV
-        dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
+        const uint32_t wa = (reg & 2) ? w4.z : w4.x, wb = (reg & 2) ? w4.w : w4.y;
+        const f32x2 z = {__builtin_bit_cast(float, bit_mask(wa, kbit) & rsd_bits),
+                         __builtin_bit_cast(float, bit_mask(wb, kbit) & rsd_bits)};
+        po[j] = pv * z;                                                              // (P o Z) for dV
+        dso[j] = pv * __builtin_elementwise_fma(dpv, z, f32x2{ndl[reg], ndl[reg + 1]});  // P o (Z o dP - delta)
       } else {
-        s[reg] = pv;
-        dp[reg] *= pv;
+        po[j] = pv;
+        dso[j] = dpv * pv;
       }
     }
     // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
-    typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
-    typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
+    typename MF<T>::e8 pf0 = pack8p<T>(po, 0), pf1 = pack8p<T>(po, 1);
+    typename MF<T>::e8 sf0 = pack8p<T>(dso, 0), sf1 = pack8p<T>(dso, 1);
 #pragma unroll
     for (int i = 0; i < DO / 32; ++i) {
       const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
@@ -1097,7 +1118,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     if (col0 == 0 && hh == 0 && qrow < sq) P.delta[bh * p.sq + qrow] = dl;
   }
   const int ntiles64 = (sk + 63) >> 6;
-  const float rsd = p.drop_rs;
+  const uint32_t rsd_bits = __builtin_bit_cast(uint32_t, p.drop_rs);
+  const f32x2 sl2v = {sl2, sl2}, nlse2 = {-lse2, -lse2}, ndl2 = {-dl, -dl};
   f32x16 dq[DO / 32];
 #pragma unroll
   for (int i = 0; i < DO / 32; ++i) dq[i] = f32x16{0};
@@ -1168,6 +1190,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
         for (int st = 0; st < 4; ++st) ktf[i][st] = ld_tr<T>(sK, tro.lo[i] + 16 * st * DS, tro.hi[i] + 16 * st * DS);
     }
     f32x16 s[2], dp[2];
+    f32x2 dsp[2][8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       s[u] = f32x16{0};
@@ -1178,22 +1201,32 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
         dp[u] = MF<T>::mma(ld8<T>(sV + ro.o[k] + 32 * u * DS), df[k], dp[u]);
       }
       if (BIAS && tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
-      if (DROP) {
-        // dp <- keep o dP (raw), then dS = P o (dP o keep / (1 - p) - delta); the keep bits
-        // are the forward's (loaded with the tile, one dword per lane)
-        drop_tile_bits(dp[u], kbits, u);
-      }
+      // dS^T = P o (Z o dP - delta), Z = keep / (1 - p) from the forward's bits (one dword per
+      // lane per tile) -- element-wise on register pairs (packed fp32 FMAs / multiplies)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        float pv = fast_exp2(fmaf(s[u][reg], sl2, -lse2));
+      for (int j = 0; j < 8; ++j) {
+        const int reg = 2 * j;
+        const f32x2 a = __builtin_elementwise_fma(f32x2{s[u][reg], s[u][reg + 1]}, sl2v, nlse2);
+        f32x2 pv = {fast_exp2(a.x), fast_exp2(a.y)};
         if constexpr (MASK) {
-          const int kk = kv0 + 32 * u + acc_row(reg, hh);
-          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win)) pv = 0.f;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int kk = kv0 + 32 * u + acc_row(reg + e, hh);
+            if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win))
+              pv[e] = 0.f;
+          }
         }
-        dp[u][reg] = DROP ? pv * fmaf(dp[u][reg], rsd, -dl) : pv * (dp[u][reg] - dl);  // dS^T
+        const f32x2 d = {dp[u][reg], dp[u][reg + 1]};
+        if (DROP) {
+          const f32x2 z = {__builtin_bit_cast(float, bit_mask(kbits, 16u * u + reg) & rsd_bits),
+                           __builtin_bit_cast(float, bit_mask(kbits, 16u * u + reg + 1) & rsd_bits)};
+          dsp[u][j] = pv * __builtin_elementwise_fma(d, z, ndl2);
+        } else {
+          dsp[u][j] = pv * (d + ndl2);
+        }
       }
       if (SEQ) {
-        const typename MF<T>::e8 sf0 = pack8<T>(dp[u], 0), sf1 = pack8<T>(dp[u], 1);
+        const typename MF<T>::e8 sf0 = pack8p<T>(dsp[u], 0), sf1 = pack8p<T>(dsp[u], 1);
 #pragma unroll
         for (int i = 0; i < DO / 32; ++i) {
           const int a0 = 32 * u * DS, a1 = (32 * u + 16) * DS;
@@ -1203,7 +1236,8 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
     }
     if (!SEQ) {
-      typename MF<T>::e8 sf[4] = {pack8<T>(dp[0], 0), pack8<T>(dp[0], 1), pack8<T>(dp[1], 0), pack8<T>(dp[1], 1)};
+      typename MF<T>::e8 sf[4] = {pack8p<T>(dsp[0], 0), pack8p<T>(dsp[0], 1), pack8p<T>(dsp[1], 0),
+                                  pack8p<T>(dsp[1], 1)};
 #pragma unroll
       for (int i = 0; i < DO / 32; ++i) {
 #pragma unroll

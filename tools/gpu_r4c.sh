@@ -5,6 +5,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4c
+timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_attention_gpu.py tests/test_dropout_gpu.py > gpurun_out/r4c/attn_tests.log 2>&1 || { tail -30 gpurun_out/r4c/attn_tests.log; exit 1; }
+tail -1 gpurun_out/r4c/attn_tests.log
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/r4c/prof_base -o base -- python3 tools/attn_time.py abtest/_C_base.so > gpurun_out/r4c/prof_base.log 2>&1 || { tail -5 gpurun_out/r4c/prof_base.log; exit 1; }
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/r4c/prof_intree -o intree -- python3 tools/attn_time.py > gpurun_out/r4c/prof_intree.log 2>&1 || { tail -5 gpurun_out/r4c/prof_intree.log; exit 1; }
 echo profiles done

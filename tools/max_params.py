@@ -86,7 +86,7 @@ def _host_rss_gb():
 
 def shard(args):
     """BASELINE config 5 (GPT-3 175B shape, PP=4 x TP=2) -- ONE rank's shard on one GPU: the
-    heaviest stage (embedding + 24 of the 96 layers) with every tensor-parallel dimension
+    heaviest stage (embedding + 24 of the 96 layers; --layers sets more per stage) with every tensor-parallel dimension
     halved (48 of the 96 heads x 128, 4h / 2 = 24576 MLP channels, half the vocabulary), built
     at tp=1 with those sliced shapes.  bf16 params / grads, AdamW with the fp32 state fields
     named by SMP_OFFLOAD_OPTIMIZER_FIELDS in pinned host memory (amd_offload_optimizer_state),
@@ -131,7 +131,7 @@ def shard(args):
     host_state = sum(t.numel() * t.element_size() for d in opt.domains for t in (d.master, d.m, d.v)
                      if t is not None and not t.is_cuda)
     rec = {"ok": all(l == l for l in losses), "config": "GPT-3 175B shape, PP=4 x TP=2: one rank's shard "
-           "(embedding + 24 layers, TP-sliced shapes at tp=1)", "layers": args.layers, "hidden": h,
+           f"(embedding + {args.layers} layers, TP-sliced shapes at tp=1)", "layers": args.layers, "hidden": h,
            "heads_local": 96 // tp, "intermediate_local": 4 * h // tp, "vocab_local": vocab, "params": n,
            "offloaded_fields": sorted(opt._offload_fields), "host_state_gb": round(host_state / 1e9, 2),
            "host_peak_rss_gb": round(_host_rss_gb() or 0.0, 2),
