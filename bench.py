@@ -270,7 +270,10 @@ def main():
 
     from smdistributed_modelparallel_amd.parallel.comm_timer import timer as comm_timer
 
+    from smdistributed_modelparallel_amd.ops.attention import FLASH_CALLS
+
     sync()
+    fc0 = dict(FLASH_CALLS)
     comm_timer.reset()
     comm_timer.enabled = True  # two HIP events around each communication wait (no sync)
     t0 = time.perf_counter()
@@ -283,6 +286,10 @@ def main():
     ex = torch.tensor([exposed["dp"], exposed["p2p"]], dtype=torch.float64, device=dev)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+    # flash-attention forward launches in the timed steps, summed over ranks
+    fc = torch.tensor([FLASH_CALLS[k] - fc0[k] for k in ("plain", "key_bias")], dtype=torch.float64, device=dev)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(fc)
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -334,6 +341,7 @@ def main():
             # per-step compute-stream stall on communication (max over ranks): the DP bucket
             # all-reduces left after backward, and pipeline activation / gradient pulls
             "exposed_comm_ms": {"dp": round(float(ex[0]) / args.steps, 2), "p2p": round(float(ex[1]) / args.steps, 2)},
+            "attention_calls": {"plain": int(fc[0]), "key_bias": int(fc[1])},
             "tokens_per_s": round(tokens_per_s, 1),
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),
             "final_loss": round(loss_val, 4),

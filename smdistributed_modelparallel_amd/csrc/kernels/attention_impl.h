@@ -68,6 +68,26 @@ struct MF<f16> {
 };
 
 constexpr float kLog2e = 1.4426950408889634f;
+
+// Compile-time A/B switches (tools/build_kvariant.sh builds a variant .so; defaults = shipped):
+//   SMPK_ATTN_PAIRS     element-wise softmax / dS code of dQ and dK/dV on f32x2 register pairs
+//                       (packed fp32 FMAs) instead of scalar code
+//   SMPK_ATTN_FWD_PAIRS the same for the forward's exponent arguments and row sums
+//   SMPK_ATTN_VPRE      forward D = 64: the tile's V fragments read before the softmax
+//   SMPK_ATTN_FWD_WAVES forward D <= 128: waves-per-SIMD floor given to the register allocator
+//                       (0 = none)
+#ifndef SMPK_ATTN_PAIRS
+#define SMPK_ATTN_PAIRS 1
+#endif
+#ifndef SMPK_ATTN_FWD_PAIRS
+#define SMPK_ATTN_FWD_PAIRS 1
+#endif
+#ifndef SMPK_ATTN_VPRE
+#define SMPK_ATTN_VPRE 1
+#endif
+#ifndef SMPK_ATTN_FWD_WAVES
+#define SMPK_ATTN_FWD_WAVES 0
+#endif
 constexpr int kThreads = 256;
 
 // LDS row stride (elements) for head dim D
@@ -423,25 +443,27 @@ __device__ __forceinline__ E drop_packed(E v, uint32_t f0, uint32_t f1) {
 // ------------------------------------------------------------ stored keep bits
 // The forward hashes each element's dropout decision once and stores it as 1 bit: per (b h,
 // query row q, 64-key tile t, half-wave hh) one uint32 at ((bh * ntiles + t) * sq + q) * 2 + hh
-// whose bit 16 s + reg is the decision of key 64 t + 32 s + acc_row(reg, hh) -- exactly the
-// registers a query-on-lane wave holds, so the forward writes and dQ reads one coalesced
-// dword per lane per tile, and dK/dV stages a block's words through LDS.  The backward then
-// never regenerates the hash (~100 VALU per 64-key tile per lane).
+// holding the decisions of exactly the 32 keys a query-on-lane wave's lane holds (keys
+// 64 t + 32 s + acc_row(reg, hh), at bit drop_bit(s, reg)), so the forward writes and dQ
+// reads one coalesced dword per lane per tile, and dK/dV stages a block's words through LDS.
+// The backward then never regenerates the hash (~100 VALU per 64-key tile per lane).
 __device__ __forceinline__ int64_t bits_index(int64_t bh, int ntiles, int tile, int sq, int q, int hh) {
   return ((bh * ntiles + tile) * static_cast<int64_t>(sq) + q) * 2 + hh;
 }
 
-// 4 keep flags (bits 7, 15, 23, 31 of a keep_flags word) -> a 4-bit nibble in bits 0-3
-__device__ __forceinline__ uint32_t flag_nibble(uint32_t f) { return ((f & 0x80808080u) * 0x00204081u) >> 28; }
-
-// the lane's 32 keep bits of a tile from the 8 keep words of its two 32-key halves
+// The lane's 32 keep bits of a tile from the 8 keep words of its two 32-key halves: word g of
+// half s keeps its flags at bits 7, 15, 23, 31 (element i at 8 i + 7); shifted right by g + 4 s
+// they interleave without overlap, so register reg = 4 g + i of half s is bit
+// drop_bit(s, reg) = 8 i + 7 - g - 4 s (one shift + and-or per word).
+__device__ __forceinline__ constexpr uint32_t drop_bit(int s, int reg) {
+  return static_cast<uint32_t>(8 * (reg & 3) + 7 - (reg >> 2) - 4 * s);
+}
 __device__ __forceinline__ uint32_t pack_keep(const uint32_t (&f0)[4], const uint32_t (&f1)[4]) {
   uint32_t w = 0;
 #pragma unroll
-  for (int g = 0; g < 4; ++g) w |= (flag_nibble(f0[g]) << (4 * g)) | (flag_nibble(f1[g]) << (16 + 4 * g));
+  for (int g = 0; g < 4; ++g) w |= ((f0[g] & 0x80808080u) >> g) | ((f1[g] & 0x80808080u) >> (4 + g));
   return w;
 }
-
 
 // LDS-DMA of one K or V tile (BN rows x D, D = 64 / 128: the LDS image is exactly [BN][D]):
 // each wave-instruction fills 1 KB = 1024 / (2 D) consecutive rows, lane-linear, so the
@@ -496,7 +518,11 @@ struct QInLds {
 // and a per-tile `if (!interior)`, hipcc if-converted the masks into ~100 VALU + ~100 SALU
 // selects executed on every tile -- profiles/r4/attention_isa.md.)
 template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
-__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(AttnParams p) {
+__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
+#if SMPK_ATTN_FWD_WAVES
+    __attribute__((amdgpu_waves_per_eu(D >= 256 ? 1 : SMPK_ATTN_FWD_WAVES)))
+#endif
+    attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr bool QLDS = QInLds<D>::v;
   static_assert(!DMA || (!QLDS && !BIAS && DS == D && (D == 64 || D == 128)), "DMA variant: D 64 / 128, no bias");
@@ -655,7 +681,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
         p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
     }
-    constexpr bool VPRE = D == 64 && !BIAS;
+    constexpr bool VPRE = SMPK_ATTN_VPRE && D == 64 && !BIAS;
     typename MF<T>::e8 vfr[VPRE ? D / 32 : 1][4];
     if constexpr (VPRE) {
 #pragma unroll
@@ -700,6 +726,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
       m_use = mu;
     }
     // p = exp2(S sl2 - m): exponent arguments two at a time (v_pk_fma_f32), packed row sums
+#if SMPK_ATTN_FWD_PAIRS
     const f32x2 sl2v = {sl2, sl2}, nm = {-m_use, -m_use};
     f32x2 rs0 = {0.f, 0.f}, rs1 = {0.f, 0.f};
 #pragma unroll
@@ -718,6 +745,19 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2) attn_fwd_kernel(At
     }
     rs0 += rs1;
     l_i += rs0.x + rs0.y;
+#else
+    float rs0 = 0.f, rs1 = 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float e0 = fast_exp2(fmaf(s0[reg], sl2, -m_use));
+      const float e1 = fast_exp2(fmaf(s1[reg], sl2, -m_use));
+      s0[reg] = e0;
+      s1[reg] = e1;
+      rs0 += e0;
+      rs1 += e1;
+    }
+    l_i += rs0 + rs1;
+#endif
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
       pf[0] = drop_packed(pf[0], f0[0], f0[1]);
@@ -828,14 +868,13 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   const float kbias_raw = BIAS ? load_bias(p, b, krow) : 0.f;
   float kbias = 0.f;
   bool blk_bias = false;  // this wave's 32 keys carry a bias
-  // dropout: the forward's keep bits (kDropBits layout).  This lane's key kr = krow & 31 in
-  // 32-key half s = wave & 1 of 64-key tile kb * 2 + wave / 2 is bit 16 s + 4 (kr >> 3) +
-  // (kr & 3) of the words with half-wave index (kr >> 2) & 1.  Thread t stages word
+  // dropout: the forward's keep bits.  This lane's key kr = krow & 31 in 32-key half s =
+  // wave & 1 of 64-key tile kb * 2 + wave / 2 is register 4 (kr >> 3) + (kr & 3) of the words
+  // with half-wave index (kr >> 2) & 1: bit drop_bit(s, that register).  Thread t stages word
   // (tile half t >> 7, query (t >> 1) & 63, half-wave t & 1) of each Q tile (coalesced 512 B
   // runs) into sBits[(t >> 7) * 2 + (t & 1)][query].
   const int ntiles64 = (sk + 63) >> 6;
-  const uint32_t kbit = 16u * static_cast<uint32_t>(wave & 1) + 4u * static_cast<uint32_t>(r >> 3) +
-                        static_cast<uint32_t>(r & 3);
+  const uint32_t kbit = drop_bit(wave & 1, 4 * (r >> 3) + (r & 3));
   const int bits_row = ((wave >> 1) * 2 + ((r >> 2) & 1)) * BQ;  // this lane's sBits row
   const int st_tile = kb * 2 + static_cast<int>(threadIdx.x >> 7), st_q = (threadIdx.x >> 1) & 63;
   const int st_hh = threadIdx.x & 1;
@@ -956,6 +995,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
       for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(&sBits[bits_row + 32 * sub + 8 * g + 4 * hh]);
     }
+#if SMPK_ATTN_PAIRS
     // element-wise on register pairs (2j, 2j + 1): packed fp32 multiplies / FMAs
     f32x2 po[8], dso[8];
     const f32x2 sl2v = {sl2, sl2};
@@ -989,6 +1029,29 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
     typename MF<T>::e8 pf0 = pack8p<T>(po, 0), pf1 = pack8p<T>(po, 1);
     typename MF<T>::e8 sf0 = pack8p<T>(dso, 0), sf1 = pack8p<T>(dso, 1);
+#else
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      float pv = fast_exp2(s[reg] * sl2);
+      if constexpr (MASK) {
+        const int qq = qs + acc_row(reg, hh);
+        if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win)) pv = 0.f;
+      }
+      if (DROP) {
+        const uint4 w4 = kw[reg >> 2];
+        const uint32_t w = (reg & 3) == 0 ? w4.x : (reg & 3) == 1 ? w4.y : (reg & 3) == 2 ? w4.z : w4.w;
+        const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
+        s[reg] = pv * z;                             // (P o Z) for dV
+        dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
+      } else {
+        s[reg] = pv;
+        dp[reg] *= pv;
+      }
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
+    typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
+    typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
+#endif
 #pragma unroll
     for (int i = 0; i < DO / 32; ++i) {
       const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
@@ -1203,6 +1266,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       if (BIAS && tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       // dS^T = P o (Z o dP - delta), Z = keep / (1 - p) from the forward's bits (one dword per
       // lane per tile) -- element-wise on register pairs (packed fp32 FMAs / multiplies)
+#if SMPK_ATTN_PAIRS
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int reg = 2 * j;
@@ -1218,13 +1282,27 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
         }
         const f32x2 d = {dp[u][reg], dp[u][reg + 1]};
         if (DROP) {
-          const f32x2 z = {__builtin_bit_cast(float, bit_mask(kbits, 16u * u + reg) & rsd_bits),
-                           __builtin_bit_cast(float, bit_mask(kbits, 16u * u + reg + 1) & rsd_bits)};
+          const f32x2 z = {__builtin_bit_cast(float, bit_mask(kbits, drop_bit(u, reg)) & rsd_bits),
+                           __builtin_bit_cast(float, bit_mask(kbits, drop_bit(u, reg + 1)) & rsd_bits)};
           dsp[u][j] = pv * __builtin_elementwise_fma(d, z, ndl2);
         } else {
           dsp[u][j] = pv * (d + ndl2);
         }
       }
+#else
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        float pv = fast_exp2(fmaf(s[u][reg], sl2, -lse2));
+        if constexpr (MASK) {
+          const int kk = kv0 + 32 * u + acc_row(reg, hh);
+          if (qrow >= sq || kk >= sk || (CAUSAL && kk > qrow + diag) || (win > 0 && kk <= qrow + diag - win)) pv = 0.f;
+        }
+        float d = dp[u][reg];
+        if (DROP) d = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, d) & bit_mask(kbits, drop_bit(u, reg)));
+        const float ds = DROP ? pv * fmaf(d, p.drop_rs, -dl) : pv * (d - dl);
+        dsp[u][reg >> 1][reg & 1] = ds;
+      }
+#endif
       if (SEQ) {
         const typename MF<T>::e8 sf0 = pack8p<T>(dsp[u], 0), sf1 = pack8p<T>(dsp[u], 1);
 #pragma unroll

@@ -170,7 +170,7 @@ struct AttnParams {
   uint32_t drop_xr1;   // ... and for thr = drop_thr + 1
   uint32_t drop_c1;
   // keep bits [b * h][ceil(sk / 64)][sq][2] (one uint32 per (row, 64-key tile, half-wave)):
-  // written by the forward, read by dQ / dK-dV (attention_impl.h kDropBits layout)
+  // written by the forward, read by dQ / dK-dV (attention_impl.h drop_bit layout)
   uint32_t* drop_bits;
   uint64_t seed, offset;
 };

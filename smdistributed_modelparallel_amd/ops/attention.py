@@ -128,6 +128,15 @@ def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu")
     return (u >= thr).view(b, h, sq, sk)
 
 
+# forward launches of the flash kernels by variant, for run reports (bench.py "attention_calls":
+# a pipeline stage whose padding masks were decided all-ones launches no key-bias variant)
+FLASH_CALLS = {"plain": 0, "key_bias": 0}
+
+
+def _count_flash(kb):
+    FLASH_CALLS["key_bias" if kb is not None else "plain"] += 1
+
+
 class _FlashAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, causal, window, kb, dropout_p):
@@ -190,6 +199,7 @@ def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, t
     p = dropout_p if training else 0.0
     kbias = key_padding_bias(mask, q.shape[1], q.shape[1], mask_value) if mask is not None else None
     if use_flash and flash_supported(q, p, mask, kbias):
+        _count_flash(kbias)
         return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kbias, float(p))
     return attention(q, qkv[:, :, 1], qkv[:, :, 2], causal=causal, mask=mask, scale=scale, dropout_p=dropout_p,
                      window=window, training=training, use_flash=use_flash, mask_value=mask_value)
@@ -291,5 +301,6 @@ def attention(q, k, v, causal=True, mask=None, scale=None, dropout_p=0.0, window
     if use_flash and not attention_in_fp32 and q.is_cuda:
         kbias = key_padding_bias(mask, q.shape[1], k.shape[1], mask_value) if mask is not None else None
         if flash_supported(q, p, mask, kbias):
+            _count_flash(kbias)
             return _FlashAttention.apply(q, k, v, float(scale), bool(causal), int(window or 0), kbias, float(p))
     return _materialised(q, k, v, scale, causal, mask, dropout_p, window, training, attention_in_fp32)

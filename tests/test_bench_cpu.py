@@ -57,6 +57,9 @@ def _check_audit_fields(rec, world, dp, pp):
     if dp > 1:
         assert ex["dp"] > 0.0  # gloo all-reduces block the host: some wait is always exposed
     assert ex["dp"] + ex["p2p"] <= rec["ms_per_step"] * 1.05
+    # flash launches by variant (CPU runs use the materialised path: none)
+    assert set(rec["attention_calls"]) == {"plain", "key_bias"}
+    assert all(isinstance(v, int) and v >= 0 for v in rec["attention_calls"].values())
 
 
 def test_bench_pp_layout_four_ranks():
