@@ -80,10 +80,10 @@ constexpr float kLog2e = 1.4426950408889634f;
 #define SMPK_ATTN_PAIRS 1
 #endif
 #ifndef SMPK_ATTN_FWD_PAIRS
-#define SMPK_ATTN_FWD_PAIRS 1
+#define SMPK_ATTN_FWD_PAIRS 0
 #endif
 #ifndef SMPK_ATTN_VPRE
-#define SMPK_ATTN_VPRE 1
+#define SMPK_ATTN_VPRE 0
 #endif
 #ifndef SMPK_ATTN_FWD_WAVES
 #define SMPK_ATTN_FWD_WAVES 0

@@ -192,6 +192,218 @@ __global__ void __launch_bounds__(256) ln_fwd_stream(const T* __restrict__ x, co
   }
 }
 
+// Wide rows (more than 64 x 8 16-byte vectors: GPT-NeoX 6144, GPT-3 12288 in bf16): one
+// 256-thread block per row, thread t holding vectors t, t + 256, .. (VB of them) in registers:
+// x read once with 16-byte loads, two block reductions, y written once.  (The streaming
+// fallback this replaces re-read the row three times with 2-byte accesses: ~1 TB/s at 6144.)
+template <typename T, typename W, int VB, typename TO = T>
+__global__ void __launch_bounds__(256) ln_fwd_wide(const T* __restrict__ x, const T* __restrict__ res,
+                                                   T* __restrict__ x_out, const W* __restrict__ w,
+                                                   const W* __restrict__ b, TO* __restrict__ y,
+                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                   int64_t rows, int cols, float eps, DropoutArgs drop) {
+  constexpr int N = Vec16<T>::N;
+  __shared__ float smem[16];
+  const int t = threadIdx.x;
+  const int64_t row = blockIdx.x;
+  const int nvec = cols / N;
+  const uint32_t dkey = drop.thr ? dropout_key(drop) : 0u;
+  float v[VB][N];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    const int vi = t + 256 * k;
+#pragma unroll
+    for (int j = 0; j < N; ++j) v[k][j] = 0.f;
+    if (vi < nvec) {
+      const int64_t off = row * cols + static_cast<int64_t>(vi) * N;
+      Vec16<T> a = load16(x + off);
+      if (res != nullptr) {
+        Vec16<T> r = load16(res + off);
+        float f[N];
+        if (drop.thr) {
+          if constexpr (N == 8) {
+            dropout_factors8(dkey, off, drop, f);
+          } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) f[j] = dropout_factor1(dkey, off + j, drop);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) f[j] = 1.f;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) a.v[j] = from_f32<T>(fmaf(to_f32(a.v[j]), f[j], to_f32(r.v[j])));
+        store16(x_out + off, a);
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        v[k][j] = to_f32(a.v[j]);  // (the rounded sum is what is normalised)
+        sum += v[k][j];
+      }
+    }
+  }
+  const float mean = block_sum(sum, smem) / cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    if (t + 256 * k < nvec) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const float d = v[k][j] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(block_sum(sq, smem) / cols + eps);
+  if (t == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    const int vi = t + 256 * k;
+    if (vi < nvec) {
+      const int c = vi * N;
+      float g[N], bb[N], o[N];
+      if (w) {
+        load_wn<W, N>(w + c, g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) g[j] = 1.f;
+      }
+      if (b) {
+        load_wn<W, N>(b + c, bb);
+      } else {
+#pragma unroll
+        for (int j = 0; j < N; ++j) bb[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < N; ++j) o[j] = (v[k][j] - mean) * rstd * g[j] + bb[j];
+      store_out<TO, T, N>(y + row * cols + c, o);
+    }
+  }
+}
+
+// Wide-row backward: a block per `rows_per_block` rows, thread t owning vectors t + 256 k of
+// every row; the row's x / dy (/ dres) stay in registers as packed 16-byte vectors between
+// the reduction pass and the dx pass, gamma is re-read from L1/L2 per row (instead of VB x N
+// more registers), and dgamma / dbeta accumulate per thread over the block's rows into one fp32
+// partial row per block (parts = the register paths' count: no [rows, cols] partials).
+// ext: the distributed LayerNorm's all-reduced row sums replace the local reduction.
+template <typename T, typename W, int VB>
+__global__ void __launch_bounds__(256) ln_bwd_wide(const T* __restrict__ dy, const T* __restrict__ x,
+                                                   const W* __restrict__ w, const float* __restrict__ mean_in,
+                                                   const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                   float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                   int64_t rows, int cols, const T* __restrict__ dres,
+                                                   int64_t rows_per_block, const float* __restrict__ ext,
+                                                   float ext_n) {
+  constexpr int N = Vec16<T>::N;
+  __shared__ float smem[2][16];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int nvec = cols / N;
+  float dwacc[VB][N], dbacc[VB][N];
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) dwacc[k][j] = dbacc[k][j] = 0.f;
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
+  for (int64_t row = r0; row < r1; ++row) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    Vec16<T> xa[VB], da[VB];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+      const int vi = t + 256 * k;
+      if (vi < nvec) {
+        const int64_t off = row * cols + static_cast<int64_t>(vi) * N;
+        xa[k] = load16(x + off);
+        da[k] = load16(dy + off);
+        float g[N];
+        if (w) {
+          load_wn<W, N>(w + vi * N, g);
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) g[j] = 1.f;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const float dyv = to_f32(da[k].v[j]);
+          const float xh = (to_f32(xa[k].v[j]) - mean) * rstd;
+          const float gg = dyv * g[j];
+          s1 += gg;
+          s2 += gg * xh;
+          dwacc[k][j] += dyv * xh;
+          dbacc[k][j] += dyv;
+        }
+      }
+    }
+    // both row sums in one barrier pair (double-buffered by row parity)
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    float* red = smem[row & 1];
+    if (lane == 0) {
+      red[wid] = s1;
+      red[8 + wid] = s2;
+    }
+    __syncthreads();
+    if (ext != nullptr) {
+      s1 = ext[2 * row] / ext_n;
+      s2 = ext[2 * row + 1] / ext_n;
+    } else {
+      s1 = (red[0] + red[1] + red[2] + red[3]) / cols;
+      s2 = (red[8] + red[9] + red[10] + red[11]) / cols;
+    }
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+      const int vi = t + 256 * k;
+      if (vi < nvec) {
+        const int64_t off = row * cols + static_cast<int64_t>(vi) * N;
+        float g[N];
+        if (w) {
+          load_wn<W, N>(w + vi * N, g);
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) g[j] = 1.f;
+        }
+        Vec16<T> ra;
+        if (dres != nullptr) ra = load16(dres + off);
+        Vec16<T> o;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const float xh = (to_f32(xa[k].v[j]) - mean) * rstd;
+          float vv = rstd * (to_f32(da[k].v[j]) * g[j] - s1 - xh * s2);
+          if (dres != nullptr) vv += to_f32(ra.v[j]);
+          o.v[j] = from_f32<T>(vv);
+        }
+        store16(dx + off, o);
+      }
+    }
+  }
+  if (dw_part == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < VB; ++k) {
+    const int vi = t + 256 * k;
+    if (vi >= nvec) continue;
+    const int64_t c = static_cast<int64_t>(vi) * N;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      dw_part[static_cast<int64_t>(blockIdx.x) * cols + c + j] = dwacc[k][j];
+      if (db_part) db_part[static_cast<int64_t>(blockIdx.x) * cols + c + j] = dbacc[k][j];
+    }
+  }
+}
+
+// vectors per thread of the wide kernels (0: not a wide row): 3 / 4 / 6 x 256 16-byte vectors
+constexpr int kLnWideMaxVB = 6;
+__host__ __device__ inline int ln_wide_vb(int64_t nvec) {
+  if (nvec <= 512 || nvec > 256 * kLnWideMaxVB) return 0;
+  return nvec <= 768 ? 3 : (nvec <= 1024 ? 4 : 6);
+}
+
 template <typename T, typename W, int VPT>
 __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, const T* __restrict__ x,
                                                   const W* __restrict__ w, const float* __restrict__ mean_in,
@@ -521,6 +733,12 @@ void launch_ln_fwd(const void* x, const void* residual, void* x_out, const void*
     ln_fwd_reg<T, W, 4, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
   } else if (aligned && vpt <= 8) {
     ln_fwd_reg<T, W, 8, TO><<<grid, 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && ln_wide_vb(cols / N) == 3) {
+    ln_fwd_wide<T, W, 3, TO><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && ln_wide_vb(cols / N) == 4) {
+    ln_fwd_wide<T, W, 4, TO><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
+  } else if (aligned && ln_wide_vb(cols / N) == 6) {
+    ln_fwd_wide<T, W, 6, TO><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps, drop);
   } else {
     ln_fwd_stream<T, W, TO><<<static_cast<int>(rows), 256, 0, s>>>(xx, rr, xo, ww, bb, yy, mean, rstd, rows, c, eps,
                                                                    drop);
@@ -573,7 +791,8 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
                            (dres == nullptr || vec_ok<T>(dres));
       const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
       const bool reg = aligned && vpt <= 8;
-      const int parts = ln_bwd_parts(rows, cols, reg);
+      const int wide = aligned ? ln_wide_vb(cols / N) : 0;
+      const int parts = ln_bwd_parts(rows, cols, reg || wide > 0);
       if (part_rows != parts) return -2;  // caller must size partials with layernorm_bwd_parts
       const T* dyy = static_cast<const T*>(dy);
       const T* xx = static_cast<const T*>(x);
@@ -597,6 +816,15 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
         ln_bwd_reg<T, W, 4><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else if (reg) {
         ln_bwd_reg<T, W, 8><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
+      } else if (wide == 3) {
+        ln_bwd_wide<T, W, 3><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb,
+                                                   ext_sums, ext_n);
+      } else if (wide == 4) {
+        ln_bwd_wide<T, W, 4><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb,
+                                                   ext_sums, ext_n);
+      } else if (wide == 6) {
+        ln_bwd_wide<T, W, 6><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb,
+                                                   ext_sums, ext_n);
       } else {
         ln_bwd_stream<T, W><<<static_cast<int>(rows), 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part,
                                                                    rows, c, dr, ext_sums, ext_n);
@@ -713,7 +941,8 @@ int layernorm_bwd_local_sums(int dt, const void* dy, const void* x, int wdt, con
 int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned) {
   const int N = dt == F32 ? 4 : 8;
   const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));
-  return ln_bwd_parts(rows, cols, aligned && (cols % N == 0) && vpt <= 8);
+  const bool ok = aligned && (cols % N == 0);
+  return ln_bwd_parts(rows, cols, ok && (vpt <= 8 || ln_wide_vb(cols / N) > 0));
 }
 
 }  // namespace smpk

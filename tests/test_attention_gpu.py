@@ -97,6 +97,40 @@ def test_flash_dropout_matches_host_mask(d, causal, p):
     assert not torch.equal(o.detach(), o2)
 
 
+def test_flash_bench_shape_dropout_fp32():
+    """The bench's attention exactly (GPT-2 XL: 25 heads x 64, s 2048, causal, dropout 0.1),
+    forward and backward against fp32 with the host-rebuilt keep mask (the
+    backward was checked only up to s 1024)."""
+    from smdistributed_modelparallel_amd.ops.attention import _FlashAttentionPacked, flash_dropout_keep_mask
+
+    torch.manual_seed(8)
+    b, s, h, d, p = 2, 2048, 25, 64, 0.1
+    qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    gen = torch.cuda.default_generators[torch.cuda.current_device()]
+    seed, off = gen.initial_seed(), gen.get_offset()
+    o = _FlashAttentionPacked.apply(qkv, 0.125, True, 0, None, p)
+    keep = flash_dropout_keep_mask(b, h, s, s, p, seed & ((1 << 63) - 1), off, device="cuda")
+    qf = qkv.detach().float().requires_grad_()
+    orf = _ref(qf[:, :, 0], qf[:, :, 1], qf[:, :, 2], 0.125, True, keep=keep, p=p)
+    assert (o.float() - orf).abs().max().item() < 3e-2 * max(1.0, orf.abs().max().item())
+    g = torch.randn_like(orf)
+    o.backward(g.to(torch.bfloat16))
+    orf.backward(g)
+    gq, gr = qkv.grad.float(), qf.grad
+    _check_grads((("dq", gq[:, :, 0], gr[:, :, 0]), ("dk", gq[:, :, 1], gr[:, :, 1]), ("dv", gq[:, :, 2], gr[:, :, 2])),
+                 3e-2)
+
+
+def test_gpt2xl_width_step_matches_fp32():
+    """GPT-2 XL width, 2 layers, 16384 tokens through smp.DistributedModel in bf16 -- the
+    bench's kernels incl. the weight-gradient MFMA kernel with fused bias sums -- one step
+    against an fp32 copy (tests/workers/bench_shape.py)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("bench_shape", 1, [], timeout=300, env_extra={"SMP_FORCE_CPU": "0"})
+    assert "OK" in outs[0], outs[0][-3000:]
+
+
 @pytest.mark.parametrize("d", [64, 128, 256])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_key_padding_bias(d, causal):

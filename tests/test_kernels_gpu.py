@@ -22,7 +22,7 @@ def C():
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("cols", [64, 1600, 4096, 1000, 12288])
+@pytest.mark.parametrize("cols", [64, 1600, 4096, 1000, 5000, 6144, 8192, 12288])
 def test_layernorm_fwd_bwd(C, dt, cols):
     from smdistributed_modelparallel_amd.ops.layernorm import layer_norm
 
@@ -44,18 +44,21 @@ def test_layernorm_fwd_bwd(C, dt, cols):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-def test_add_layernorm(C, dt):
+@pytest.mark.parametrize("cols", [1600, 6144])
+def test_add_layernorm(C, dt, cols):
+    """Residual add + LayerNorm in one kernel (register rows; 6144: the wide block-per-row
+    kernels of GPT-NeoX / the 175B shape's TP-sliced widths)."""
     from smdistributed_modelparallel_amd.ops.layernorm import add_layer_norm
 
     torch.manual_seed(1)
-    x = torch.randn(64, 1600, device="cuda", dtype=dt, requires_grad=True)
-    r = torch.randn(64, 1600, device="cuda", dtype=dt, requires_grad=True)
-    w = torch.ones(1600, device="cuda", dtype=dt, requires_grad=True)
-    b = torch.zeros(1600, device="cuda", dtype=dt, requires_grad=True)
+    x = torch.randn(64, cols, device="cuda", dtype=dt, requires_grad=True)
+    r = torch.randn(64, cols, device="cuda", dtype=dt, requires_grad=True)
+    w = torch.ones(cols, device="cuda", dtype=dt, requires_grad=True)
+    b = torch.zeros(cols, device="cuda", dtype=dt, requires_grad=True)
     y, s = add_layer_norm(x, r, w, b)
     xr, rr = x.detach().float().requires_grad_(), r.detach().float().requires_grad_()
     sr = xr + rr
-    yr = torch.nn.functional.layer_norm(sr, (1600,), w.detach().float(), b.detach().float())
+    yr = torch.nn.functional.layer_norm(sr, (cols,), w.detach().float(), b.detach().float())
     tol = _tol(dt) * 4
     assert torch.allclose(s.float(), sr, atol=tol, rtol=tol)
     assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)

@@ -12,7 +12,7 @@ for S in gptj_tp4 neox_pp2tp4; do
   grep '^SHARD' gpurun_out/r4d/$S.log
   timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/r4d/trace_$S -o t -- python3 tools/shard_bench.py $S --mbs 8 \
     --steps 2 --warmup 2 > gpurun_out/r4d/trace_$S.log 2>&1 || { tail -20 gpurun_out/r4d/trace_$S.log; exit 1; }
-  f=$(find gpurun_out/r4d/trace_$S -name "*kernel_trace.csv" | head -1)
+  f=$(find gpurun_out/r4d/trace_$S -name "*.db" | head -1)
   python3 tools/step_kernels.py "$f" > gpurun_out/r4d/kernels_$S.txt && head -25 gpurun_out/r4d/kernels_$S.txt
   rm -f "$f"
 done
@@ -21,4 +21,10 @@ timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 
   --master-port 29513 bench.py --gpus 4 --microbatches 8 --steps 2 --warmup 2 --tunableop off \
   > gpurun_out/r4d/pp4.log 2>&1
 rc=$?; grep '"metric"' gpurun_out/r4d/pp4.log || tail -30 gpurun_out/r4d/pp4.log
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+# the 1-GPU default bench step, kernel-traced (3 steps; the table is the last full step)
+timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/r4d/trace_bench -o t -- python3 bench.py --steps 3 --warmup 2 \
+  > gpurun_out/r4d/trace_bench.log 2>&1 || { tail -20 gpurun_out/r4d/trace_bench.log; exit 1; }
+f=$(find gpurun_out/r4d/trace_bench -name "*.db" | head -1)
+python3 tools/step_kernels.py "$f" > gpurun_out/r4d/kernels_bench.txt && head -30 gpurun_out/r4d/kernels_bench.txt
+rm -f "$f"

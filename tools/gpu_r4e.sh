@@ -6,6 +6,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r4e
+timeout -k 10 600 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_attention_gpu.py -k "bench_shape or gpt2xl_width" > gpurun_out/r4e/pytest.log 2>&1
+rc=$?; grep -E "PASSED|FAILED|Error|assert" gpurun_out/r4e/pytest.log | head -20; [ $rc -le 1 ] || exit $rc
 for b in intree base scalar bwscalar novpre fw3 intree; do
   so=""; [ $b != intree ] && so=abtest/_C_$b.so
   timeout -k 10 120 rocprofv3 --kernel-trace -d gpurun_out/r4e/p_$b -o r -- python3 tools/attn_time.py $so \

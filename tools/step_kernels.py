@@ -4,7 +4,15 @@ import collections
 import csv
 import sys
 
-rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+if sys.argv[1].endswith(".db"):  # rocprofv3's default rocpd SQLite output
+    import sqlite3
+
+    db = sqlite3.connect(sys.argv[1])
+    rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e, "Grid_Size_X": gx, "Workgroup_Size_X": wx}
+            for n, s, e, gx, wx in db.execute("select name, start, end, grid_x, workgroup_x from kernels")]
+else:
+    rows = list(csv.DictReader(open(sys.argv[1])))
+rows = sorted(rows, key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "xent_fwd" in r["Kernel_Name"]]
 last = rows[idx[-2]:idx[-1]]
 t0, t1 = int(last[0]["Start_Timestamp"]), int(rows[idx[-1]]["Start_Timestamp"])
