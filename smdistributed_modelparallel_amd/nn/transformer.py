@@ -362,9 +362,10 @@ class DistributedAttentionLayer(DistributedModule):
                 logger.info("causal attention with an attention mask: the mask is applied together with the causal "
                             "mask (the reference's fused causal softmax ignored it unless fused_softmax=False)")
 
-    def core(self, a, mask=None, cross_states=None, cross_mask=None):
+    def core(self, a, mask=None, cross_states=None, cross_mask=None, reduce=True):
         """a: [B, s, h] (already normalised). Returns the dense output after the TP
-        all-reduce (bias included), [B, s, h]."""
+        all-reduce (bias included), [B, s, h]; reduce=False: the rank's partial sum (the
+        caller reduces it together with another row-parallel output)."""
         if not self.cross_attention:
             self._note_causal_mask(mask)
         if self._mem:
@@ -392,7 +393,7 @@ class DistributedAttentionLayer(DistributedModule):
                     mask=mask, mask_value=getattr(self, "mask_value", -1e4),
                 )
                 out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
-                return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
+                return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
@@ -406,7 +407,7 @@ class DistributedAttentionLayer(DistributedModule):
         )
         ctx = ctx.reshape(B, s, lh * d)
         out = linear(ctx, self.dense_weight, self.dense_bias)
-        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
+        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
 
     def _core_memory(self, a, mask):
         """optimize='memory': a is [B, s, h/tp] (hidden-sharded).  Partial QKV products
@@ -538,7 +539,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
             if self.dense2_bias is not None:
                 self.dense2_bias.zero_()
 
-    def core(self, m):
+    def core(self, m, reduce=True):
         if self._mem:
             # m: [B, s, h/tp]; partial products reduce-scattered on the output channels
             x = linear(m, self.dense1_weight, self.dense1_bias)
@@ -555,7 +556,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
                    dbias_of=self.dense1_bias if fuse_db else None)
         x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu, bias_grad=not fuse_db)
         out = linear(x, self.dense2_weight, self.dense2_bias)
-        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 else out)
+        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
 
     def forward(self, hidden):
         if self._tp > 1 and self.input_layer and not _prescaled():
@@ -605,10 +606,17 @@ class DistributedTransformerLayer(DistributedModule):
         at, out = self.attention, self.output
         if self.parallel_attn_output:
             a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
-            attn = at.core(a, mask)
+            # TP without branch dropout: one all-reduce of the summed row-parallel partials
+            # (both biases live on tp_rank 0) instead of one per branch -- the reference's
+            # parallel-attention layout; half the layer's forward TP traffic
+            one_ar = self._tp > 1 and not self._mem and not at.dropout.active_p() and not out.dropout.active_p()
+            attn = at.core(a, mask, reduce=not one_ar)
             m = a if self.single_pre_layernorm else (out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden)
-            mlp = out.core(m)
-            hidden = hidden + at.dropout(attn) + out.dropout(mlp)
+            mlp = out.core(m, reduce=not one_ar)
+            if one_ar:
+                hidden = hidden + fwd_allreduce_for_tp(attn + mlp, inplace=True)
+            else:
+                hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:
             if at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
                 # hidden feeds LN1 and the residual add: its two gradients meet in the LN kernel

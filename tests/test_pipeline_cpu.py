@@ -104,6 +104,19 @@ def test_pp2_activation_offloading():
     _run(2, 2, 1, 2, extra={"ckpt_layers": True, "cfg": {"offload_activations": True}})
 
 
+@pytest.mark.parametrize("base,model", [
+    ("gptj-6b", {"hidden_size": 64, "num_attention_heads": 4, "attention_head_size": 16, "intermediate_size": 128,
+                 "rotary_dim": 8}),
+    ("gptneox-20b", {"hidden_size": 64, "num_attention_heads": 4, "attention_head_size": 16,
+                     "intermediate_size": 128, "rotary_dim": 4}),
+])
+def test_tp2_parallel_attention_one_allreduce(base, model):
+    """GPT-J / NeoX parallel attention + MLP at TP=2: the two row-parallel partials are summed
+    and all-reduced once per layer (the reference's layout) -- same loss and parameters as the
+    unpartitioned model."""
+    _run(2, 1, 2, 2, extra={"base": base, "model": model})
+
+
 def test_tp2_optimize_memory():
     _run(2, 1, 2, 2, extra={"cfg": {"optimize": "memory"}})
 
