@@ -160,14 +160,16 @@ class IpcP2P {
       it = imports_.end();
     }
     if (it == imports_.end()) {
+      if (imports_.size() >= kMaxImports) evict_lru_locked();
       hipIpcMemHandle_t h;
       std::memcpy(&h, mh.data(), sizeof(h));
       void* p = nullptr;
       hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-      imports_[key] = Mapping{gen, p};
+      imports_[key] = Mapping{gen, p, 0};
       it = imports_.find(key);
       stats_maps_++;
     }
+    it->second.last_use = ++use_clock_;
     hipStream_t s = at::hip::getCurrentHIPStream(device_).stream();
     if (nbytes > 0) {
       hip_check(hipMemcpyAsync(dst.data_ptr(), static_cast<char*>(it->second.ptr) + offset, nbytes,
@@ -176,6 +178,13 @@ class IpcP2P {
     }
     stats_imports_++;
     stats_bytes_in_ += nbytes;
+  }
+
+  // test hook: a small cap makes every pull of a new segment evict (tests/workers/pp_gpu.py)
+  void set_max_imports(int64_t n) {
+    std::lock_guard<std::mutex> g(mu_);
+    TORCH_CHECK(n >= 1, "IpcP2P.set_max_imports: need >= 1");
+    kMaxImports = static_cast<size_t>(n);
   }
 
   void close() {
@@ -195,6 +204,8 @@ class IpcP2P {
     d["segment_exports"] = stats_exports_new_;
     d["imports"] = stats_imports_;
     d["mappings"] = stats_maps_;
+    d["mappings_open"] = static_cast<int64_t>(imports_.size());
+    d["mappings_evicted"] = stats_evicted_;
     d["bytes_out"] = stats_bytes_out_;
     d["bytes_in"] = stats_bytes_in_;
     d["event_slots"] = static_cast<int64_t>(events_.size());
@@ -212,7 +223,26 @@ class IpcP2P {
   struct Mapping {
     int64_t gen;
     void* ptr;
+    uint64_t last_use;
   };
+
+  // A receiver never learns that a sender freed a segment (only a new generation at the same
+  // base replaces a mapping), so under allocator churn mappings of dead segments -- and the
+  // sender memory they pin -- would accumulate.  The import table is bounded: past
+  // kMaxImports mappings the least recently used one is closed, after the pull stream has
+  // drained (a pending copy may still read it; eviction is rare, so the sync is cheap).
+  static constexpr size_t kMaxImportsDefault = 256;
+  size_t kMaxImports = kMaxImportsDefault;
+  void evict_lru_locked() {
+    auto lru = imports_.begin();
+    for (auto i = imports_.begin(); i != imports_.end(); ++i)
+      if (i->second.last_use < lru->second.last_use) lru = i;
+    if (lru == imports_.end()) return;
+    hip_check(hipStreamSynchronize(at::hip::getCurrentHIPStream(device_).stream()), "hipStreamSynchronize");
+    hipIpcCloseMemHandle(lru->second.ptr);
+    imports_.erase(lru);
+    stats_evicted_++;
+  }
 
   int acquire_event_locked() {
     if (free_slots_.empty()) {
@@ -245,7 +275,8 @@ class IpcP2P {
   std::vector<LocalEvent> events_;
   std::vector<int> free_slots_;
   std::map<std::pair<int, int64_t>, Mapping> imports_;
-  int64_t stats_exports_ = 0, stats_exports_new_ = 0, stats_imports_ = 0, stats_maps_ = 0;
+  uint64_t use_clock_ = 0;
+  int64_t stats_exports_ = 0, stats_exports_new_ = 0, stats_imports_ = 0, stats_maps_ = 0, stats_evicted_ = 0;
   int64_t stats_bytes_out_ = 0, stats_bytes_in_ = 0;
 };
 
@@ -258,6 +289,7 @@ void register_ipc_p2p(py::module& m) {
       .def("import_copy", &IpcP2P::import_copy, py::arg("dst"), py::arg("src"), py::arg("base"), py::arg("gen"),
            py::arg("mem_handle"), py::arg("offset"), py::arg("nbytes"))
       .def("release_event", &IpcP2P::release_event)
+      .def("set_max_imports", &IpcP2P::set_max_imports)
       .def("close", &IpcP2P::close)
       .def("stats", &IpcP2P::stats);
 }

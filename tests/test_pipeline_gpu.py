@@ -38,6 +38,13 @@ def test_pp2_simple_pipeline_ipc():
     _run(2, 2, 3, extra={"pipeline": "simple"})
 
 
+def test_pp2_ipc_bounded_mappings():
+    """A receiver's IPC import table is bounded (least recently used mapping closed after the
+    pull stream drains): with a cap of 1 every new sender segment evicts, and training still
+    matches the unpartitioned model."""
+    _run(2, 2, 3, extra={"max_mappings": 1})
+
+
 def test_pp2_bf16_ipc():
     _run(2, 2, 2, dtype="bf16")
 

@@ -35,6 +35,8 @@ def main():
     smp.init(cfg)
     want_mode = extra.get("expect_mode", os.environ.get("SMP_P2P", "ipc"))
     assert smp.state.transport.mode == want_mode, (smp.state.transport.mode, want_mode)
+    if extra.get("max_mappings"):  # bounded IPC import table: evictions under churn
+        smp.state.transport._ipc.set_max_imports(int(extra["max_mappings"]))
     net = build_gpt("gpt2-small", dropout=0.0, **kw)
     net.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
     if not extra.get("auto") and pp > 1:
@@ -88,6 +90,10 @@ def main():
         # every exported activation / gradient was released by its receiver at step end
         assert st["held"] == 0 and st["event_slots_busy"] == 0 and st["release_wait_timeouts"] == 0, st
         assert st["comm_stream"] == (os.environ.get("SMP_P2P_COMM_STREAM", "1") != "0"), st
+    if extra.get("max_mappings"):
+        ist = smp.state.transport._ipc.stats()
+        assert ist["mappings_open"] <= int(extra["max_mappings"]), ist
+        assert ist["mappings_evicted"] > 0, ist  # the churn really went through the eviction path
     print(f"rank {smp.rank()} OK pp={pp} loss={ref_loss.item():.5f} worst_param_diff={worst:.2e} p2p={st}", flush=True)
     smp.barrier()
 

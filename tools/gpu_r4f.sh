@@ -11,7 +11,8 @@ mkdir -p gpurun_out/r4f
 HB=$!
 trap "kill $HB" EXIT
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py \
-  tests/test_attention_gpu.py tests/test_dropout_gpu.py > gpurun_out/r4f/pytest.log 2>&1
+  tests/test_attention_gpu.py tests/test_dropout_gpu.py "tests/test_pipeline_gpu.py::test_pp2_ipc_bounded_mappings" \
+  "tests/test_pipeline_gpu.py::test_pp2_ipc_matches_unpartitioned" > gpurun_out/r4f/pytest.log 2>&1
 rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/r4f/pytest.log | tail -12; [ $rc -le 1 ] || exit $rc
 timeout -k 10 120 python tools/attn_time.py 2>&1 | grep -v "^\[\|amdgpu.ids" || exit 1
 S=neox_pp2tp4
