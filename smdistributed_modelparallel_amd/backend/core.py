@@ -72,6 +72,9 @@ class Watchdog:
         self.step_timeout = float(t) if t else None
         self._step_started = None
         self._stop = False
+        # hang diagnostics: callables returning one line of runtime state each (the pipeline
+        # engine's pending waits, transport holds, mailbox queues), logged with the stacks
+        self.diagnostics = []
         self._thread = threading.Thread(target=self._run, name="smp-watchdog", daemon=True)
 
     def start(self):
@@ -89,12 +92,33 @@ class Watchdog:
 
     def step_started(self):
         self._step_started = time.monotonic()
+        if self.step_timeout is not None:
+            # backstop for a main thread blocked in native code WITH the GIL (the watchdog
+            # thread then cannot run): faulthandler's own C thread dumps every Python stack
+            # without the GIL, 30 s after the watchdog should have fired, and exits
+            try:
+                faulthandler.dump_traceback_later(self.step_timeout + 30.0, exit=True)
+            except Exception:  # pragma: no cover
+                pass
 
     def step_finished(self):
         self._step_started = None
+        if self.step_timeout is not None:
+            try:
+                faulthandler.cancel_dump_traceback_later()
+            except Exception:  # pragma: no cover
+                pass
+
+    def dump_state(self):
+        for fn in list(self.diagnostics):
+            try:
+                logger.error(f"[smp watchdog] rank {self.core._rank} state: {fn()}")
+            except Exception as e:  # state read racing the main thread: report and go on
+                logger.error(f"[smp watchdog] rank {self.core._rank} state unavailable: {e!r}")
 
     def _fatal(self, why):
         logger.error(f"[smp watchdog] rank {self.core._rank}: {why}; dumping stacks and exiting")
+        self.dump_state()
         try:
             faulthandler.dump_traceback(all_threads=True)
         except Exception:  # pragma: no cover
@@ -113,6 +137,7 @@ class Watchdog:
                 return
             if err:
                 logger.error(f"[smp watchdog] rank {self.core._rank}: peer failure: {err}")
+                self.dump_state()  # what this rank was waiting for when the peer gave up
                 deadline = time.monotonic() + self.grace
                 while time.monotonic() < deadline:
                     if self._stop:

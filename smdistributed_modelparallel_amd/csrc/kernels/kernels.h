@@ -218,5 +218,9 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
 // split/merge-axis all-to-all and allgatherv packing).
 int strided_copy4(int elem_bytes, const void* src, void* dst, const int64_t* sizes, const int64_t* src_strides,
                   const int64_t* dst_strides, hipStream_t s);
+// Flat byte copy by a kernel on `s` (16-byte vectors when both ends are 16-byte aligned): the
+// pipeline's IPC pulls use it instead of hipMemcpyAsync, so a pull is an ordinary compute-queue
+// kernel of the pull stream (no copy-engine queue shared with the process's other streams).
+int device_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s);
 
 }  // namespace smpk

@@ -75,4 +75,42 @@ int strided_copy4(int elem_bytes, const void* src, void* dst, const int64_t* siz
   }
 }
 
+namespace {
+// grid-stride copy of n16 16-byte vectors, then the byte tail by the first block
+__global__ void __launch_bounds__(256) device_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          int64_t n16, const uint8_t* __restrict__ tsrc,
+                                                          uint8_t* __restrict__ tdst, int tail) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+  if (blockIdx.x == 0 && static_cast<int>(threadIdx.x) < tail) tdst[threadIdx.x] = tsrc[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) device_copy_bytes_kernel(const uint8_t* __restrict__ src,
+                                                                uint8_t* __restrict__ dst, int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+}  // namespace
+
+int device_copy(void* dst, const void* src, int64_t nbytes, hipStream_t s) {
+  if (nbytes <= 0) return 0;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+  if (aligned) {
+    const int64_t n16 = nbytes / 16;
+    const int tail = static_cast<int>(nbytes - n16 * 16);
+    // enough workgroups to fill the chip (2048 x 256 threads), grid-stride beyond
+    const int64_t want = (n16 + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(want < 1 ? 1 : (want > 2048 ? 2048 : want));
+    device_copy_kernel<<<grid, 256, 0, s>>>(static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16,
+                                            static_cast<const uint8_t*>(src) + n16 * 16,
+                                            static_cast<uint8_t*>(dst) + n16 * 16, tail);
+  } else {
+    const int64_t want = (nbytes + 255) / 256;
+    const unsigned grid = static_cast<unsigned>(want > 2048 ? 2048 : want);
+    device_copy_bytes_kernel<<<grid, 256, 0, s>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst),
+                                                  nbytes);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
 }  // namespace smpk

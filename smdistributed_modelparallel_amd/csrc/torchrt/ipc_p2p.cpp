@@ -26,6 +26,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
+
+#include "../kernels/kernels.h"
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include <torch/extension.h>
@@ -86,12 +88,49 @@ class IpcP2P {
   py::tuple export_tensor(const at::Tensor& t) {
     TORCH_CHECK(t.is_cuda(), "IpcP2P.export: tensor must be on the GPU");
     TORCH_CHECK(t.is_contiguous(), "IpcP2P.export: tensor must be contiguous");
+    int64_t b_out = 0, gen_out = 0, offset = 0, nbytes = 0;
+    hipIpcMemHandle_t handle;
+    {
+      // HIP runtime calls without the GIL (a blocked call must not freeze the process's other
+      // Python threads -- the watchdog among them)
+      py::gil_scoped_release nogil;
+      export_locked_impl(t, b_out, gen_out, handle, offset, nbytes);
+    }
+    return py::make_tuple(b_out, gen_out, py::bytes(reinterpret_cast<const char*>(&handle), sizeof(hipIpcMemHandle_t)),
+                          offset, nbytes);
+  }
+
+  void export_locked_impl(const at::Tensor& t, int64_t& b_out, int64_t& gen_out, hipIpcMemHandle_t& handle,
+                          int64_t& offset_out, int64_t& nbytes_out) {
     std::lock_guard<std::mutex> g(mu_);
     drain_freed_locked();
     char* ptr = static_cast<char*>(t.data_ptr());
     hipDeviceptr_t base = nullptr;
     size_t size = 0;
     hip_check(hipMemGetAddressRange(&base, &size, reinterpret_cast<hipDeviceptr_t>(ptr)), "hipMemGetAddressRange");
+    if (size > kMaxExportSegment) {
+      // the tensor sits in a huge caching-allocator segment (e.g. a freed multi-GB logits
+      // block reused for a gradient): opening such a segment's IPC handle in the peer blocked
+      // indefinitely on this driver (3.5 GB hung, 1 GB worked: tools/ipc_size_probe.py), so
+      // the bytes go out through a pooled, separately allocated staging buffer instead --
+      // one D2D copy on the producer's stream, before the message's readiness event
+      const int64_t nb = static_cast<int64_t>(t.numel() * t.element_size());
+      const int si = acquire_staging_locked(static_cast<size_t>(nb));
+      Staging& st = staging_[si];
+      hip_check(static_cast<hipError_t>(
+                    smpk::device_copy(st.ptr, ptr, nb, at::hip::getCurrentHIPStream(device_).stream())),
+                "device_copy (staging)");
+      staging_pending_.push_back(si);
+      stats_staged_++;
+      stats_exports_++;
+      stats_bytes_out_ += nb;
+      b_out = static_cast<int64_t>(reinterpret_cast<uintptr_t>(st.ptr));
+      gen_out = st.gen;
+      handle = st.handle;
+      offset_out = 0;
+      nbytes_out = nb;
+      return;
+    }
     uintptr_t b = reinterpret_cast<uintptr_t>(base);
     auto it = exports_.find(b);
     if (it == exports_.end() || it->second.size != size) {
@@ -103,13 +142,13 @@ class IpcP2P {
       it = exports_.find(b);
       stats_exports_new_++;
     }
-    const int64_t offset = static_cast<int64_t>(reinterpret_cast<uintptr_t>(ptr) - b);
-    const int64_t nbytes = static_cast<int64_t>(t.numel() * t.element_size());
+    offset_out = static_cast<int64_t>(reinterpret_cast<uintptr_t>(ptr) - b);
+    nbytes_out = static_cast<int64_t>(t.numel() * t.element_size());
     stats_exports_++;
-    stats_bytes_out_ += nbytes;
-    return py::make_tuple(static_cast<int64_t>(b), it->second.gen,
-                          py::bytes(reinterpret_cast<const char*>(&it->second.handle), sizeof(hipIpcMemHandle_t)),
-                          offset, nbytes);
+    stats_bytes_out_ += nbytes_out;
+    b_out = static_cast<int64_t>(b);
+    gen_out = it->second.gen;
+    handle = it->second.handle;
   }
 
   // Sender side: record the readiness event of one control message on the current stream.
@@ -117,6 +156,9 @@ class IpcP2P {
   py::tuple record_event() {
     std::lock_guard<std::mutex> g(mu_);
     int slot = acquire_event_locked();
+    // the staging buffers of this message are free again once its receiver releases the slot
+    staging_by_slot_[slot].swap(staging_pending_);
+    staging_pending_.clear();
     hip_check(hipEventRecord(events_[slot].ev, at::hip::getCurrentHIPStream(device_).stream()), "hipEventRecord");
     return py::make_tuple(slot, static_cast<uint64_t>(reinterpret_cast<uintptr_t>(events_[slot].ev)));
   }
@@ -138,6 +180,11 @@ class IpcP2P {
       events_[slot].busy = false;
       free_slots_.push_back(slot);
     }
+    auto sb = staging_by_slot_.find(slot);
+    if (sb != staging_by_slot_.end()) {
+      for (int si : sb->second) staging_free_.push_back(si);
+      staging_by_slot_.erase(sb);
+    }
   }
 
   // Receiver side: enqueue one D2D pull of nbytes into dst on the current stream.  The
@@ -150,6 +197,7 @@ class IpcP2P {
                 dst.numel() * dst.element_size(), " B, message ", nbytes, " B)");
     std::string mh = mem_handle;
     TORCH_CHECK(mh.size() == sizeof(hipIpcMemHandle_t), "IpcP2P.import: malformed handle");
+    py::gil_scoped_release nogil;  // HIP calls below: no GIL held while they run
     std::lock_guard<std::mutex> g(mu_);
     // ---- mapping of the sender's segment
     auto key = std::make_pair(src, base);
@@ -172,9 +220,12 @@ class IpcP2P {
     it->second.last_use = ++use_clock_;
     hipStream_t s = at::hip::getCurrentHIPStream(device_).stream();
     if (nbytes > 0) {
-      hip_check(hipMemcpyAsync(dst.data_ptr(), static_cast<char*>(it->second.ptr) + offset, nbytes,
-                               hipMemcpyDeviceToDevice, s),
-                "hipMemcpyAsync");
+      // a copy kernel on the pull stream, not hipMemcpyAsync: with four processes time-sharing
+      // one GPU, >= 100 MB hipMemcpyAsync pulls blocked the host thread indefinitely (PP=4
+      // micro-batch 16 rehearsal, tools/gpu_pp_hang.sh); 50 MB pulls did not
+      hip_check(static_cast<hipError_t>(smpk::device_copy(dst.data_ptr(), static_cast<char*>(it->second.ptr) + offset,
+                                                          nbytes, s)),
+                "device_copy");
     }
     stats_imports_++;
     stats_bytes_in_ += nbytes;
@@ -195,17 +246,33 @@ class IpcP2P {
     events_.clear();
     free_slots_.clear();
     exports_.clear();
+    if (!staging_.empty()) {
+      hipDeviceSynchronize();  // a staging copy may still be queued
+      for (auto& st : staging_) hipFree(st.ptr);
+    }
+    staging_.clear();
+    staging_free_.clear();
+    staging_pending_.clear();
+    staging_by_slot_.clear();
   }
 
   py::dict stats() {
-    std::lock_guard<std::mutex> g(mu_);
     py::dict d;
+    // never blocks: the watchdog reads this while the main thread may be stuck inside a HIP
+    // call that holds mu_ (that itself is the diagnostic)
+    std::unique_lock<std::mutex> g(mu_, std::try_to_lock);
+    if (!g.owns_lock()) {
+      d["locked_by_hip_call"] = true;
+      return d;
+    }
     d["exports"] = stats_exports_;
     d["segment_exports"] = stats_exports_new_;
     d["imports"] = stats_imports_;
     d["mappings"] = stats_maps_;
     d["mappings_open"] = static_cast<int64_t>(imports_.size());
     d["mappings_evicted"] = stats_evicted_;
+    d["staged_exports"] = stats_staged_;
+    d["staging_buffers"] = static_cast<int64_t>(staging_.size());
     d["bytes_out"] = stats_bytes_out_;
     d["bytes_in"] = stats_bytes_in_;
     d["event_slots"] = static_cast<int64_t>(events_.size());
@@ -225,6 +292,41 @@ class IpcP2P {
     void* ptr;
     uint64_t last_use;
   };
+
+  // largest caching-allocator segment exported in place
+  static constexpr size_t kMaxExportSegment = size_t(1) << 30;
+  struct Staging {
+    void* ptr;
+    size_t cap;
+    int64_t gen;
+    hipIpcMemHandle_t handle;
+  };
+  // best-fitting free staging buffer, or a new one (2 MB-rounded hipMalloc: its own segment,
+  // exported once -- receivers keep the mapping across steps)
+  int acquire_staging_locked(size_t nbytes) {
+    int best = -1;
+    for (size_t i = 0; i < staging_free_.size(); ++i) {
+      const int si = staging_free_[i];
+      if (staging_[si].cap >= nbytes && (best < 0 || staging_[si].cap < staging_[staging_free_[best]].cap))
+        best = static_cast<int>(i);
+    }
+    if (best >= 0) {
+      const int si = staging_free_[best];
+      staging_free_.erase(staging_free_.begin() + best);
+      return si;
+    }
+    Staging st;
+    st.cap = (nbytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+    hip_check(hipSetDevice(device_), "hipSetDevice");
+    hip_check(hipMalloc(&st.ptr, st.cap), "hipMalloc (IPC staging)");
+    hip_check(hipIpcGetMemHandle(&st.handle, st.ptr), "hipIpcGetMemHandle (IPC staging)");
+    st.gen = ++gen_counter_;
+    staging_.push_back(st);
+    return static_cast<int>(staging_.size()) - 1;
+  }
+  std::vector<Staging> staging_;
+  std::vector<int> staging_free_, staging_pending_;
+  std::map<int, std::vector<int>> staging_by_slot_;
 
   // A receiver never learns that a sender freed a segment (only a new generation at the same
   // base replaces a mapping), so under allocator churn mappings of dead segments -- and the
@@ -277,6 +379,7 @@ class IpcP2P {
   std::map<std::pair<int, int64_t>, Mapping> imports_;
   uint64_t use_clock_ = 0;
   int64_t stats_exports_ = 0, stats_exports_new_ = 0, stats_imports_ = 0, stats_maps_ = 0, stats_evicted_ = 0;
+  int64_t stats_staged_ = 0;
   int64_t stats_bytes_out_ = 0, stats_bytes_in_ = 0;
 };
 

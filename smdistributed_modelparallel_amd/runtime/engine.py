@@ -187,6 +187,23 @@ class PipelineEngine:
         self._recording = None
         self._cur_worker = None
         self.reset_step()
+        wd = getattr(state.core, "watchdog", None) if getattr(state, "core", None) is not None else None
+        if wd is not None:
+            wd.diagnostics.append(self.debug_state)
+
+    def debug_state(self):
+        """One line of what this rank's pipeline is waiting for (the watchdog logs it on a step
+        timeout or a peer failure): microbatch statuses, open wait keys, per-microbatch
+        gradient entries still owed, transport holds."""
+        pl = self.pipeline
+        status = [int(x) for x in pl.status] if pl is not None else None
+        waits = sorted(str(k) for k in list(self.waiting))[:24]
+        owed = {mb: sum(1 for e in list(st.entries.values()) if not e.flushed)
+                for mb, st in list(self.mbstate.items())}
+        tr = self.state.transport
+        ts = tr.stats() if tr is not None and hasattr(tr, "stats") else {}
+        return (f"mb_status={status} active={getattr(pl, 'active_mb', None)} waiting={waits} "
+                f"local_q={len(self._local_q)} entries_owed={owed} transport={ts}")
 
     # ------------------------------------------------------------- plumbing
     @property

@@ -45,6 +45,14 @@ def test_pp2_ipc_bounded_mappings():
     _run(2, 2, 3, extra={"max_mappings": 1})
 
 
+def test_ipc_pull_from_multi_gb_segment():
+    """Tensors inside multi-GB allocator segments (a freed logits block reused for a gradient)
+    go out through a pooled staging buffer: the peer's pull completes and matches (opening
+    the huge segment's handle directly blocked forever: the PP=4 micro-batch-16 hang)."""
+    outs = run_workers("ipc_segment", 2, [3584], timeout=180, env_extra={"SMP_FORCE_CPU": "0"})
+    assert all("OK" in o for o in outs)
+
+
 def test_pp2_bf16_ipc():
     _run(2, 2, 2, dtype="bf16")
 
