@@ -6,6 +6,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/maxp
+( while sleep 50; do echo "heartbeat $(date +%T) $(free -g | awk '/Mem/{print $3}') GB used" >> gpurun_out/maxp/heartbeat.log; done ) &
+HB=$!
+trap "kill $HB" EXIT
 free -g | head -2
 for L in 37 35; do
   SMP_OFFLOAD_OPTIMIZER_FIELDS=m,v SMP_LOG_LEVEL=warning timeout -k 10 900 \
