@@ -1265,8 +1265,10 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
       if (BIAS && tile_bias) add_from_keys(s[u], sB + 32 * u, hh);
       // dS^T = P o (Z o dP - delta), Z = keep / (1 - p) from the forward's bits (one dword per
-      // lane per tile) -- element-wise on register pairs (packed fp32 FMAs / multiplies)
-#if SMPK_ATTN_PAIRS
+      // lane per tile) -- with dropout element-wise on register pairs (packed fp32 FMAs /
+      // multiplies: dQ -7 %); without it the scalar form measured 2 % faster
+      // (profiles/r4/attention_r4c.md)
+      if constexpr (SMPK_ATTN_PAIRS && DROP) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int reg = 2 * j;
@@ -1289,7 +1291,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
           dsp[u][j] = pv * (d + ndl2);
         }
       }
-#else
+      } else {
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         float pv = fast_exp2(fmaf(s[u][reg], sl2, -lse2));
@@ -1302,7 +1304,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
         const float ds = DROP ? pv * fmaf(d, p.drop_rs, -dl) : pv * (d - dl);
         dsp[u][reg >> 1][reg & 1] = ds;
       }
-#endif
+}
       if (SEQ) {
         const typename MF<T>::e8 sf0 = pack8p<T>(dsp[u], 0), sf1 = pack8p<T>(dsp[u], 1);
 #pragma unroll
