@@ -820,7 +820,11 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   __shared__ __attribute__((aligned(16))) uint16_t sdO[BQ * DS];
   __shared__ __attribute__((aligned(16))) float sL[BQ], sDl[BQ];
   // keep bits of the Q tile x the block's 128 keys: [64-key half][word half-wave][query]
-  __shared__ __attribute__((aligned(16))) uint32_t sBits[DROP ? 4 * BQ : 4];
+  // rows padded to 72 words: the 4 rows a wave reads start 8 banks apart (with the 4-word
+  // half-wave offset: 8 distinct 4-bank groups), where a 64-word stride put all four on the
+  // same banks (SQ_LDS_BANK_CONFLICT 7.1e6 per dispatch, profiles/pmc/r4_attention_counters.md)
+  constexpr int BROW = BQ + 8;
+  __shared__ __attribute__((aligned(16))) uint32_t sBits[DROP ? 4 * BROW : 4];
   const AttnParams& p = P.f;
   // wave index as a scalar: every wave-derived tile condition (causal / window / edge) then
   // branches on SGPRs instead of being if-converted into per-lane selects on every tile
@@ -875,7 +879,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
   // runs) into sBits[(t >> 7) * 2 + (t & 1)][query].
   const int ntiles64 = (sk + 63) >> 6;
   const uint32_t kbit = drop_bit(wave & 1, 4 * (r >> 3) + (r & 3));
-  const int bits_row = ((wave >> 1) * 2 + ((r >> 2) & 1)) * BQ;  // this lane's sBits row
+  const int bits_row = ((wave >> 1) * 2 + ((r >> 2) & 1)) * BROW;  // this lane's sBits row
   const int st_tile = kb * 2 + static_cast<int>(threadIdx.x >> 7), st_q = (threadIdx.x >> 1) & 63;
   const int st_hh = threadIdx.x & 1;
   uint32_t bits_stage = 0u;
@@ -930,7 +934,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
       sL[threadIdx.x] = l_stage == -INFINITY ? 0.f : -l_stage * kLog2e * inv_sl2;
       sDl[threadIdx.x] = -d_stage;
     }
-    if (DROP) sBits[((threadIdx.x >> 7) * 2 + (threadIdx.x & 1)) * BQ + ((threadIdx.x >> 1) & 63)] = bits_stage;
+    if (DROP) sBits[((threadIdx.x >> 7) * 2 + (threadIdx.x & 1)) * BROW + ((threadIdx.x >> 1) & 63)] = bits_stage;
     __syncthreads();
     if (BIAS) {
       kbias = kbias_raw * (1.f / p.scale);

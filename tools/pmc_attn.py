@@ -10,9 +10,10 @@ def main(paths, match="attn"):
         agg = collections.defaultdict(lambda: collections.defaultdict(float))
         disp = collections.defaultdict(set)
         for r in rows:
-            k = r["Kernel_Name"].rsplit("(", 1)[0][-50:] + f" grid={r['Grid_Size']}"
-            if match not in k:
+            full = r["Kernel_Name"].rsplit("(", 1)[0]
+            if match not in full:
                 continue
+            k = full[full.find(match):][:70] + f" grid={r['Grid_Size']}"
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[k].add(r["Dispatch_Id"])
         for k, v in agg.items():
