@@ -184,6 +184,20 @@ void axpby_(at::Tensor x, at::Tensor y, double a, double b) {
   check(smpk::axpby(dt_code(x), x.data_ptr(), y.data_ptr(), x.numel(), a, b, stream()), "axpby");
 }
 
+at::Tensor add3(at::Tensor a, at::Tensor b, at::Tensor c) {
+  check_gpu(a, "a");
+  check_gpu(b, "b");
+  check_gpu(c, "c");
+  TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && c.is_contiguous(), "add3: contiguous inputs required");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.sizes() == c.sizes(), "add3: shape mismatch");
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.scalar_type() == c.scalar_type(), "add3: dtype mismatch");
+  for (const at::Tensor* t : {&a, &b, &c})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "add3: 16-B aligned inputs required");
+  auto out = at::empty_like(a, at::MemoryFormat::Contiguous);
+  check(smpk::add3(dt_code(a), a.data_ptr(), b.data_ptr(), c.data_ptr(), out.data_ptr(), a.numel(), stream()), "add3");
+  return out;
+}
+
 void cast_copy_(at::Tensor src, at::Tensor dst, double scale) {
   check_gpu(src, "src");
   check_gpu(dst, "dst");
@@ -779,6 +793,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("db_out") = py::none(), py::arg("ext_sums") = py::none(), py::arg("ext_n") = 0.0);
   m.def("layernorm_local_stats", &layernorm_local_stats);
   m.def("strided_copy_", &strided_copy_);
+  m.def("add3", &add3);
   m.def("layernorm_bwd_local_sums", &layernorm_bwd_local_sums);
   m.def("layernorm_apply_stats", &layernorm_apply_stats);
   m.def("bias_gelu_fwd", &bias_gelu_fwd, py::arg("x"), py::arg("bias"), py::arg("exact") = false);

@@ -56,6 +56,7 @@ int novograd_blend(float* norms, const float* fresh, int64_t nt, float b2, int l
 int nonfinite(int dt, const void* x, int64_t n, float* out, hipStream_t s);
 // y = a * x + b * y (elementwise, same dtype) ; y may equal x.
 int axpby(int dt, const void* x, void* y, int64_t n, float a, float b, hipStream_t s);
+int add3(int dt, const void* a, const void* b, const void* c, void* out, int64_t n, hipStream_t s);
 // copy with cast: dst(dt_dst) = src(dt_src) * scale
 int cast_copy(int dt_src, const void* src, int dt_dst, void* dst, int64_t n, float scale, hipStream_t s);
 

@@ -54,6 +54,13 @@ constexpr int TK = 64;      // tokens per staged tile
 #ifndef SMPK_WGRAD_PRIO
 #define SMPK_WGRAD_PRIO 0
 #endif
+// waves per workgroup: 8 (2 per SIMD, 128 x 64 wave blocks) or 4 (1 per SIMD, 128 x 128 wave
+// blocks -- a third less LDS read traffic per MFMA, accumulators past the 256 arch VGPRs)
+#ifndef SMPK_WGRAD_W
+#define SMPK_WGRAD_W 8
+#endif
+constexpr int kW = SMPK_WGRAD_W;
+constexpr int kWCOLS = 256 / (kW / 2);  // output columns per wave (2 wave rows of 128)
 constexpr int kTK = SMPK_WGRAD_TK;  // tokens per LDS stage of the kernel
 constexpr int kNS = SMPK_WGRAD_NS;  // LDS stages (2 x 64-token operand tiles + 16 KB column sums)
 constexpr int RW = 256;     // LDS row width (elements) of both staged tiles
@@ -170,7 +177,7 @@ struct WMF16<f16> {
 };
 
 // the idle-wave column-sum mode applies: the last 256-wide K tile leaves a 64-wide wave column free
-__host__ __device__ __forceinline__ bool wgrad_cs_idle(int K) { return K % 256 != 0 && K % 256 <= 192; }
+__host__ __device__ __forceinline__ bool wgrad_cs_idle(int K) { return K % 256 != 0 && K % 256 <= 256 - kWCOLS; }
 
 template <typename T>
 __device__ __forceinline__ typename WMF16<T>::e8 ld_tr16(const uint16_t* tile, int off_lo, int off_hi) {
@@ -206,11 +213,12 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
                                                int64_t t_begin, int64_t ntiles, float* __restrict__ out,
                                                int64_t ldo, int nb0, int kb0, float* __restrict__ cso, bool colsum,
                                                int cs_mod, int cs_rem, bool cs_idle) {
-  constexpr int W = 8, WCOLS = 64, NI = 8, NJ = 4;  // wave block 128 x 64 = 8 x 4 tiles of 16 x 16
+  // wave block 128 x WCOLS = 8 x NJ tiles of 16 x 16; waves in 2 rows x (W / 2) columns
+  constexpr int W = kW, WCOLS = kWCOLS, NI = 8, NJ = WCOLS / 16, RG = W * 2;
   constexpr int L = 2 * (TKS / W / 2);
   const int n0 = tn * TM, k0 = tk * TN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / 4, wn = wave % 4;
+  const int wm = wave / (W / 2), wn = wave % (W / 2);
   if (SMPK_WGRAD_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half
   // transposed-read offsets for k-step 0: row 8 (l / 16) + q (+4), column block base + 4 p
   int aLo[NI], aHi[NI], bLo[NJ], bHi[NJ];
@@ -247,7 +255,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = 1.0f;
   // column-sum accumulators in LDS after the operand ring (no registers held across the
-  // loop: the kernel is at its VGPR limit): thread (row group t >> 5, chunk t & 31) owns
+  // loop: the kernel is at its VGPR limit): thread (row group t >> 5 of RG, chunk t & 31) owns
   // floats [(t >> 5) * 256 + (t & 31) * 8, +8)
   float* csl = reinterpret_cast<float*>(smem + NS * STAGE) + (threadIdx.x >> 5) * 256 + (threadIdx.x & 31) * 8;
   if (colsum) {
@@ -283,8 +291,8 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
       const int ch = threadIdx.x & 31;
       f32x4 c0 = *reinterpret_cast<const f32x4*>(csl), c1 = *reinterpret_cast<const f32x4*>(csl + 4);
 #pragma unroll
-      for (int i = 0; i < TKS / 16; ++i) {
-        const int row = (threadIdx.x >> 5) + 16 * i;
+      for (int i = 0; i < TKS / RG; ++i) {
+        const int row = (threadIdx.x >> 5) + RG * i;
         const u32x4 v = *reinterpret_cast<const u32x4*>(sA + swz(row, ch));
         c0[0] += __uint_as_float(v[0] << 16);
         c0[1] += __uint_as_float(v[0] & 0xffff0000u);
@@ -325,13 +333,13 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
     }
   }
   if (colsum) {
-    // the 16 row groups' sums of each of the 256 columns
+    // the RG row groups' sums of each of the 256 columns
     __syncthreads();
     const float* red = reinterpret_cast<const float*>(smem + NS * STAGE);
     if (threadIdx.x < 256 && n0 + static_cast<int>(threadIdx.x) < N) {
       float a = 0.f;
 #pragma unroll
-      for (int g = 0; g < 16; ++g) a += red[g * 256 + threadIdx.x];
+      for (int g = 0; g < RG; ++g) a += red[g * 256 + threadIdx.x];
       cso[n0 + threadIdx.x - nb0] = a;
     }
   }
@@ -362,7 +370,7 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
 }
 
 template <typename T, int TKS, int NS>
-__global__ __launch_bounds__(512, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
+__global__ __launch_bounds__(64 * kW, 1) void wgrad_glds16_kernel(const uint16_t* __restrict__ A,
                                                              const uint16_t* __restrict__ B, float* __restrict__ ws,
                                                              int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
                                                              int64_t t_split, int group, float* __restrict__ cs) {
@@ -391,7 +399,7 @@ int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tok
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
     attr_set = true;
   }
-  wgrad_glds16_kernel<T, TKS, NS><<<grid, 512, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
+  wgrad_glds16_kernel<T, TKS, NS><<<grid, 64 * kW, lds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split,
                                                                  kWgradGroup, cs);
   return 0;
 }

@@ -36,6 +36,7 @@ from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
 from ..ops.cross_entropy import cross_entropy
+from ..ops.dropout import add3
 from ..ops.dropout import dropout_add as _dropout_add
 from ..ops import linear as _lin
 from ..ops.gelu import bias_gelu
@@ -605,7 +606,12 @@ class DistributedTransformerLayer(DistributedModule):
             mask = _gather_mask(mask)
         at, out = self.attention, self.output
         if self.parallel_attn_output:
-            a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
+            fuse = os.environ.get("SMP_FUSE_PARALLEL_RESIDUAL", "1") != "0"
+            if fuse and at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
+                # the residual gradient meets the LN-input gradient inside the LN backward kernel
+                a, hidden = at.pre_layernorm_module.forward_passthrough(hidden)
+            else:
+                a = at.pre_layernorm_module(hidden) if at.pre_layernorm else hidden
             # TP without branch dropout: one all-reduce of the summed row-parallel partials
             # (both biases live on tp_rank 0) instead of one per branch -- the reference's
             # parallel-attention layout; half the layer's forward TP traffic
@@ -615,6 +621,8 @@ class DistributedTransformerLayer(DistributedModule):
             mlp = out.core(m, reduce=not one_ar)
             if one_ar:
                 hidden = hidden + fwd_allreduce_for_tp(attn + mlp, inplace=True)
+            elif fuse and not at.dropout.active_p() and not out.dropout.active_p():
+                hidden = add3(hidden, attn, mlp)
             else:
                 hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:

@@ -9,6 +9,7 @@ generator like a philox consumer: ``torch.manual_seed``, the TP-consistent RNG f
 
 Fused forms used by the transformer (reference `smp/torch/nn/transformer.py:449,1143,1524`):
 * ``dropout_add(x, residual, p)``: residual + dropout(x) in one pass;
+* ``add3(a, b, c)``: the dropout-free parallel-attention residual sum in one pass;
 * ``add_layer_norm(..., dropout_p)`` (ops/layernorm.py): the attention-branch dropout and
   residual add run inside the LayerNorm kernel that follows them.
 CPU tensors use ``torch.nn.functional.dropout``.
@@ -66,6 +67,28 @@ def dropout_add(x, residual, p, training=True):
         y = torch.nn.functional.dropout(x, p, True)
         return y if residual is None else y + residual
     return _DropoutAdd.apply(x, residual, float(p))
+
+
+class _Add3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, c):
+        return ext().add3(a, b, c)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return dy, dy, dy
+
+
+def add3(a, b, c):
+    """a + b + c in one pass over HBM (3 reads + 1 write instead of two adds' 4 reads + 2
+    writes): the parallel-attention residual sum hidden + attn + mlp (GPT-J / NeoX layers,
+    reference `smp/torch/nn/transformer.py` parallel_attention path).  Falls back to two adds
+    for CPU tensors, mixed dtypes/shapes or non-contiguous / unaligned inputs."""
+    ts = (a, b, c)
+    if (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16, torch.float32)
+            and all(t.dtype == a.dtype and t.shape == a.shape and t.is_contiguous() and _aligned(t) for t in ts)):
+        return _Add3.apply(a, b, c)
+    return a + b + c
 
 
 def dropout(x, p, training=True):

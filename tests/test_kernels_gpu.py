@@ -193,6 +193,24 @@ def test_fused_adam(C, pdt):
         assert torch.allclose(low.float(), master, atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("n", [1, 4097, 16384 * 4096 // 64 + 3])
+def test_add3(C, dt, n):
+    from smdistributed_modelparallel_amd.ops.dropout import add3
+
+    a, b, c = (torch.randn(n, device="cuda", dtype=dt, requires_grad=True) for _ in range(3))
+    y = add3(a, b, c)
+    ref = a.detach().float() + b.detach().float() + c.detach().float()
+    torch.testing.assert_close(y.float(), ref, rtol=_tol(dt), atol=_tol(dt))
+    g = torch.randn_like(y)
+    y.backward(g)
+    for t in (a, b, c):
+        assert torch.equal(t.grad, g)
+    # unaligned views take the two-add fallback
+    z = add3(a.detach()[1:], b.detach()[1:], c.detach()[1:])
+    torch.testing.assert_close(z.float(), ref[1:], rtol=_tol(dt), atol=_tol(dt))
+
+
 def test_sumsq_nonfinite(C):
     from smdistributed_modelparallel_amd.ops.multi_tensor import nonfinite_flag, sumsq
 

@@ -56,7 +56,19 @@ if len(sys.argv) == 3 and sys.argv[1] == "--child":
         g = torch.zeros(n, k, device="cuda", dtype=torch.bfloat16)
         bias = torch.zeros(n, device="cuda", dtype=torch.bfloat16) if db else None
         ops[name] = (dy, x, g, bias, sp, 2.0 * T * n * k)
-    print("RESULT " + json.dumps(time_build(load(sys.argv[2]))), flush=True)
+    C = load(sys.argv[2])
+    res = time_build(C)
+    for name, (dy, x, g, bias, sp, fl) in ops.items():  # numerics of one launch vs fp32
+        g.zero_()
+        if bias is not None:
+            bias.zero_()
+        C.wgrad_(g, dy, x, True, sp, bias, True)
+        ref = dy.float().t() @ x.float()
+        res[name + "_relerr"] = float((g.float() - ref).norm() / ref.norm())
+        if bias is not None:
+            rb = dy.float().sum(0)
+            res[name + "_bias_relerr"] = float((bias.float() - rb).norm() / rb.norm())
+    print("RESULT " + json.dumps(res), flush=True)
     sys.exit(0)
 
 builds = sys.argv[1:] or ["intree"]
@@ -74,6 +86,6 @@ for rnd in range(3):
 for b in builds:
     tot = best[b]["qkv"] + best[b]["proj"] + best[b]["fc1"]
     fl = {name: 2.0 * T * n * k for name, (n, k, _, _) in SHAPES.items()}
-    print(json.dumps({"build": b, **{k: round(v, 1) for k, v in best[b].items()},
-                      "tflops": {k: round(fl[k] / v / 1e6, 1) for k, v in best[b].items()},
+    print(json.dumps({"build": b, **{k: (round(v, 1) if k in fl else v) for k, v in best[b].items()},
+                      "tflops": {k: round(fl[k] / v / 1e6, 1) for k, v in best[b].items() if k in fl},
                       "qkv+proj+fc1_us": round(tot, 1)}), flush=True)
