@@ -976,15 +976,20 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     // dO^T / Q^T fragments of the dV / dK MFMAs now (independent of the exp / dS work below),
     // so those MFMAs issue back to back instead of each waiting on its own LDS reads
     constexpr bool TPRE = D <= 128 && !BIAS && !DROP && CAUSAL;  // (others: spills)
-    typename MF<T>::e8 tdo[TPRE ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
-    if constexpr (TPRE) {
+    // with dropout (D = 64) the dO^T fragments only: dK/dV -4.5 %; both spill 60 B and lose
+    // 10 % (profiles/r4/attention_r4c.md)
+    constexpr bool TPRE_DO = TPRE || (D == 64 && !BIAS && DROP && CAUSAL);
+    typename MF<T>::e8 tdo[TPRE_DO ? DO / 32 : 1][2], tq[TPRE ? DO / 32 : 1][2];
+    if constexpr (TPRE_DO) {
       const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
 #pragma unroll
       for (int i = 0; i < DO / 32; ++i) {
         tdo[i][0] = ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0);
         tdo[i][1] = ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1);
-        tq[i][0] = ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0);
-        tq[i][1] = ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1);
+        if constexpr (TPRE) {
+          tq[i][0] = ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0);
+          tq[i][1] = ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1064,6 +1069,11 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
         dv[i] = MF<T>::mma(tdo[i][1], pf1, dv[i]);
         dk[i] = MF<T>::mma(tq[i][0], sf0, dk[i]);
         dk[i] = MF<T>::mma(tq[i][1], sf1, dk[i]);
+      } else if constexpr (TPRE_DO) {
+        dv[i] = MF<T>::mma(tdo[i][0], pf0, dv[i]);
+        dv[i] = MF<T>::mma(tdo[i][1], pf1, dv[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a0, tro.hi[i] + a0), sf0, dk[i]);
+        dk[i] = MF<T>::mma(ld_tr<T>(sQ, tro.lo[i] + a1, tro.hi[i] + a1), sf1, dk[i]);
       } else {
         dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a0, tro.hi[i] + a0), pf0, dv[i]);
         dv[i] = MF<T>::mma(ld_tr<T>(sdO, tro.lo[i] + a1, tro.hi[i] + a1), pf1, dv[i]);
@@ -1248,7 +1258,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     // S / dP accumulators are live next to the 16 Q / dO fragments.
     constexpr bool SEQ = D >= 256;
     // K^T fragments of the dQ MFMAs (independent of the softmax work): read up front
-    constexpr bool KPRE = !SEQ && !BIAS && !DROP;
+    constexpr bool KPRE = !SEQ && !BIAS && !DROP;  // (with dropout: no gain, r4 notes)
     typename MF<T>::e8 ktf[KPRE ? DO / 32 : 1][4];
     if constexpr (KPRE) {
 #pragma unroll
