@@ -1232,8 +1232,18 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv_begin + threadIdx.x);
   }
   bool tile_bias = false;
+  // keep bits of the next visible tile, loaded one tile ahead and BEFORE that tile's K / V
+  // staging loads: the in-order vmcnt then retires them without draining the K / V prefetch
+  // (read in the body they sat behind it: dQ with dropout waited on the next tile's K / V)
+  const bool bits_row_ok = DROP && qrow < sq;
+  auto bits_at = [&](int t) -> uint32_t {
+    return P.f.drop_bits[bits_index(bh, ntiles64, (kv_begin + t * BN) >> 6, sq, qrow, hh)];
+  };
+  uint32_t kb_cur = 0u, kb_nxt = 0u;
+  if (bits_row_ok && tv0 < tv1 && tv0 == 0) kb_nxt = bits_at(0);
   auto sync = [&](int t) {
     const int kv0 = kv_begin + t * BN;
+    kb_cur = kb_nxt;
     __syncthreads();
     stK.store(sK);
     stV.store(sV);
@@ -1244,6 +1254,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
     __syncthreads();
     tile_bias = BIAS && sFlag != 0;
     if (t + 1 < nt) {
+      if (bits_row_ok && t + 1 >= tv0 && t + 1 < tv1) kb_nxt = bits_at(t + 1);
       stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
       stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
       if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
@@ -1252,7 +1263,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
   auto body = [&](int t, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
     const int kv0 = kv_begin + t * BN;
-    const uint32_t kbits = DROP && qrow < sq ? P.f.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] : 0u;
+    const uint32_t kbits = kb_cur;
     // D <= 128: both 32-key halves' dS^T, then the dQ MFMAs (the two halves' MFMA chains
     // overlap each other's softmax VALU work).  D = 256: half by half, so only one half's
     // S / dP accumulators are live next to the 16 Q / dO fragments.
