@@ -161,6 +161,20 @@ def p2p_selfcheck():
     return SELFCHECK["verdict"]
 
 
+def p2p_record(smp, args):
+    """Pipeline transport facts for the record: mode, the init-time IPC self-check, and -- for
+    IPC pulls -- the pull engine actually used (SDMA copies between distinct GPUs, a copy
+    kernel within one) and how many exports went through the >1 GB staging pool."""
+    tr = smp.state.transport if args.pp > 1 else None
+    rec = {"mode": tr.mode if tr is not None else None, "ipc_selfcheck": p2p_selfcheck()}
+    if tr is not None:
+        st = tr.stats()
+        for k in ("pull_engine", "pulls_sdma", "pulls_kernel", "mappings_remote_gpu", "staged_exports"):
+            if k in st:
+                rec[k] = st[k]
+    return rec
+
+
 def main():
     args = parse()
     import smdistributed_modelparallel_amd.torch as smp
@@ -283,7 +297,7 @@ def main():
     dt = time.perf_counter() - t0
     comm_timer.enabled = False
     exposed = comm_timer.collect()
-    ex = torch.tensor([exposed["dp"], exposed["p2p"]], dtype=torch.float64, device=dev)
+    ex = torch.tensor([exposed["dp"], exposed["p2p"], exposed["tp"]], dtype=torch.float64, device=dev)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(ex, op=dist.ReduceOp.MAX)
     # flash-attention forward launches in the timed steps, summed over ranks
@@ -336,11 +350,12 @@ def main():
             "groups": {name: (dist.get_world_size(g) if g is not None else 1)
                        for name, g in (("world", smp.state.pgs.world), ("dp", smp.state.pgs.dp),
                                        ("pp", smp.state.pgs.pp), ("tp", smp.state.pgs.tp))},
-            "p2p": {"mode": smp.state.transport.mode if args.pp > 1 else None,
-                    "ipc_selfcheck": p2p_selfcheck()},
+            "p2p": p2p_record(smp, args),
             # per-step compute-stream stall on communication (max over ranks): the DP bucket
-            # all-reduces left after backward, and pipeline activation / gradient pulls
-            "exposed_comm_ms": {"dp": round(float(ex[0]) / args.steps, 2), "p2p": round(float(ex[1]) / args.steps, 2)},
+            # all-reduces left after backward, pipeline activation / gradient pulls, and the
+            # tensor-parallel collectives (the asynchronous dX all-reduce: its final wait only)
+            "exposed_comm_ms": {"dp": round(float(ex[0]) / args.steps, 2), "p2p": round(float(ex[1]) / args.steps, 2),
+                                "tp": round(float(ex[2]) / args.steps, 2)},
             "attention_calls": {"plain": int(fc[0]), "key_bias": int(fc[1])},
             "tokens_per_s": round(tokens_per_s, 1),
             "model_tflops_per_gpu": round(flops / world / 1e12, 1),

@@ -419,7 +419,7 @@ at::Tensor bias_gelu_bwd(at::Tensor dy, at::Tensor x, c10::optional<at::Tensor> 
 // dbias given (bf16 operands): dbias (+)= sum over tokens of dy from the same kernel pass
 // (dbias_accumulate: add into it, else overwrite).
 void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t splits,
-            c10::optional<at::Tensor> dbias_opt, bool dbias_accumulate) {
+            c10::optional<at::Tensor> dbias_opt, bool dbias_accumulate, int64_t impl) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && c.is_cuda(), "wgrad_: GPU tensors required");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && c.dim() == 2, "wgrad_: 2-D operands required");
   TORCH_CHECK(dy.size(0) == x.size(0), "wgrad_: token counts differ");
@@ -454,7 +454,8 @@ void wgrad_(at::Tensor c, at::Tensor dy, at::Tensor x, bool accumulate, int64_t 
     check(smpk::wgrad(dt_code(dy), dy.data_ptr(), x.data_ptr(), dt_code(c), c.data_ptr(), ws.data_ptr<float>(), main_t,
                       static_cast<int>(n), static_cast<int>(k), dy.stride(0), x.stride(0), static_cast<int>(splits),
                       accumulate ? 1 : 0, stream(), dbias.defined() ? dt_code(dbias) : 0,
-                      dbias.defined() ? dbias.data_ptr() : nullptr, cs, dbias_accumulate ? 1 : 0),
+                      dbias.defined() ? dbias.data_ptr() : nullptr, cs, dbias_accumulate ? 1 : 0,
+                      static_cast<int>(impl)),
           "wgrad");
   }
   if (tail > 0) {
@@ -801,7 +802,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_into", &transpose_into);
   m.def("col_sum", &col_sum, py::arg("x"), py::arg("out") = py::none());
   m.def("wgrad_", &wgrad_, py::arg("c"), py::arg("dy"), py::arg("x"), py::arg("accumulate") = true,
-        py::arg("splits") = 0, py::arg("dbias") = py::none(), py::arg("dbias_accumulate") = true);
+        py::arg("splits") = 0, py::arg("dbias") = py::none(), py::arg("dbias_accumulate") = true,
+        py::arg("impl") = -1);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("rope_apply", &rope_apply);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),

@@ -210,9 +210,10 @@ int xent_bwd(int dt, const void* logits, const int64_t* target, const float* row
 int wgrad_splits(int64_t tokens, int n, int k, int num_cus);
 // bias != nullptr (bf16 operands): bias (+)= sum over tokens of A, computed by the same kernel
 // from its staged A tiles (cs: [splits * ceil(k / 256)][n] fp32 workspace, wgrad.hip).
+// impl: 1 = ping-pong kernel, 0 = one-barrier-per-tile kernel, -1 = SMP_WGRAD_IMPL / default.
 int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
           int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s, int bias_dt = 0, void* bias = nullptr,
-          float* cs = nullptr, int bias_accumulate = 1);
+          float* cs = nullptr, int bias_accumulate = 1, int impl = -1);
 
 // ---------------------------------------------------------------- pack / unpack (pack.hip)
 // Generic strided 4-D copy: dst[i0,i1,i2,i3] = src[...] with element strides (for the

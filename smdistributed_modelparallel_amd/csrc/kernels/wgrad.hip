@@ -30,6 +30,9 @@
 // waves and 2-5 stages (750-900), a phased ping-pong 8-wave variant, DMA issue spread over the
 // k-steps (no gain), and a stream-K schedule (10-35 % slower: workgroups sharing a tile then
 // read disjoint token ranges and stop sharing A / B strips in L2).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -404,6 +407,289 @@ int launch_glds16(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tok
   return 0;
 }
 
+// ------------------------------------------------------------ ping-pong kernel (round 5)
+// Same problem, same 256 x 256 output tile and split-K partials, restructured as the
+// phased two-row schedule of the fast CDNA4 GEMM template (cdna_hip_programming.md §5,
+// "The 256² 8-phase template"; T3/T4/T5): every 64-token K-tile is FOUR phases, one per
+// 64 x 32 quadrant of a wave's output (16 MFMAs each), and every phase is
+//     load segment: LDS transpose reads of the fragments this phase needs, 2 LDS-DMA
+//                   pieces of the NEXT tile, a COUNTED vmcnt, barrier
+//     MFMA segment: 16 v_mfma_f32_16x16x32 at raised priority, barrier.
+// Wave row 1 starts one barrier late, so on every SIMD the row-0 wave's MFMA segment runs
+// beside the row-1 wave's load segment and vice versa (ping-pong): the matrix pipe never
+// waits for an LDS read burst, and the DMA of tile t+1 stays in flight for 2-3 phases
+// (vmcnt never drains to 0 in the loop).
+//
+// LDS: 8 half-tile slots of 16 KB (two tiles in flight).  A K-tile is four half-tiles --
+// A columns [0,128) / [128,256) and B columns [0,128) / [128,256) -- and wave (wm, wn) owns
+// output rows {qa*128 + wm*64 + [0,64)} x columns {qb*128 + wn*32 + [0,32)}, qa, qb in {0,1},
+// so quadrant (qa, qb) reads exactly A half qa and B half qb.  Phase order (0,0) (0,1) (1,1)
+// (1,0): a phase needs at most one half-tile it has not read before, and the next tile's
+// halves are staged in that order, one per phase.
+//
+// Half-tile image: [token quad 16][16-column block 8][4 tokens][16 columns], 128 B per
+// block, block index XOR (quad & 1).  One LDS-DMA wave instruction (1 KiB, lane-linear) is
+// one token quad; the XOR is applied on the SOURCE columns (rule 21).  ds_read_b64_tr_b16:
+// 16-lane group g reads token quad 8s + 4r + g (r = 0, 1 -> fragment elements 4r .. 4r + 3)
+// of the k-step s; the two groups of a 32-lane half read quads of opposite parity, i.e.
+// opposite 128-B halves of a bank row: conflict-free.  The A and B fragments use the same
+// (group, element) -> token permutation, so the MFMA k-sums are exact.
+namespace pp {
+constexpr int kBK = 64;                        // tokens per K-tile
+constexpr int kHalfElems = 64 * 128;           // one half-tile image (16 KB)
+constexpr size_t kLds = 8 * kHalfElems * 2;    // 128 KB
+
+typedef WMF16<bf16>::e8 e8b;
+
+template <typename T>
+struct Regs {
+  f32x4 acc[2][2][4][2];                       // [qa][qb][i][j]
+  typename WMF16<T>::e8 fa[4][2];              // A fragments of the current qa: [i][k-step]
+  typename WMF16<T>::e8 fb[2][2][2];           // B fragments: [qb][j][k-step]
+};
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// fragment (8 elements) from two transposed reads r = 0, 1 at element offsets off, off + 2048
+template <typename T>
+__device__ __forceinline__ typename WMF16<T>::e8 frag(const uint16_t* base) {
+  return ld_tr16<T>(base, 0, 2048);
+}
+
+struct Geo {
+  int lbA[2], lbB[2];    // per-lane element offsets of the transposed reads, by block parity
+  uint32_t vA[2][2];     // staging byte offsets [half qa][quad u] relative to the tile's first token row
+  uint32_t vB[2][2];
+};
+
+// MFMAs of quadrant (QA, QB): 2 k-steps x 4 i x 2 j
+template <typename T, int QA, int QB>
+__device__ __forceinline__ void mfma_quadrant(Regs<T>& R, bool act, bool cs_quad,
+                                              const typename WMF16<T>::e8& ones) {
+  if (act) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          R.acc[QA][QB][i][j] = WMF16<T>::mma(R.fa[i][s], R.fb[QB][j][s], R.acc[QA][QB][i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  } else if (cs_quad) {
+    // bias-gradient quadrant: B = ones -> every column of acc[QA][QB][i][0] = sum over tokens of A
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) R.acc[QA][QB][i][0] = WMF16<T>::mma(R.fa[i][s], ones, R.acc[QA][QB][i][0]);
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+// One phase P (0..3) of a tile whose slots are set PAR (0, 1).  ISSUE: stage half-tile P of
+// the next tile into set PAR ^ 1.  VM: the counted wait ending the load segment.
+template <typename T, bool CS, int P, int PAR, int VM_ISSUE, int VM_LAST>
+__device__ __forceinline__ void phase(Regs<T>& R, const Geo& G, const uint16_t* smem, const uint16_t* nxtA,
+                                      const uint16_t* nxtB, bool issue, int wave, const bool (&act)[2][2],
+                                      bool cs_q1, const typename WMF16<T>::e8& ones) {
+  constexpr int QA = (P == 0 || P == 1) ? 0 : 1;
+  constexpr int QB = (P == 0 || P == 3) ? 0 : 1;
+  const uint16_t* set = smem + PAR * 4 * kHalfElems;
+  // ---- load segment
+  if (P == 0 || P == 2) {  // A half QA: 4 m-tiles x 2 k-steps
+    const uint16_t* sa = set + (P == 0 ? 0 : 3) * kHalfElems;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) R.fa[i][s] = frag<T>(sa + G.lbA[i & 1] + s * 4096 + i * 64);
+  }
+  if (P == 0 || P == 1) {  // B half QB: 2 n-tiles x 2 k-steps (qb 0 is kept for phase 3)
+    const uint16_t* sb = set + (P == 0 ? 1 : 2) * kHalfElems;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) R.fb[QB][j][s] = frag<T>(sb + G.lbB[j & 1] + s * 4096 + j * 64);
+  }
+  if (issue) {
+    uint16_t* dst = const_cast<uint16_t*>(smem) + ((PAR ^ 1) * 4 + P) * kHalfElems + (2 * wave) * 512;
+    const uint16_t* src = (P == 0 || P == 3) ? nxtA : nxtB;
+    const uint32_t v0 = P == 0 ? G.vA[0][0] : P == 3 ? G.vA[1][0] : P == 1 ? G.vB[0][0] : G.vB[1][0];
+    const uint32_t v1 = P == 0 ? G.vA[0][1] : P == 3 ? G.vA[1][1] : P == 1 ? G.vB[0][1] : G.vB[1][1];
+    lds_dma16_sv(src, v0, dst);
+    lds_dma16_sv(src, v1, dst + 512);
+  }
+  if (issue)
+    wait_vm<VM_ISSUE>();
+  else
+    wait_vm<VM_LAST>();
+  bar();
+  // ---- MFMA segment
+  mfma_quadrant<T, QA, QB>(R, act[QA][QB], CS && QB == 1 && cs_q1 && act[QA][0], ones);
+  bar();
+}
+
+// a whole tile; issue: there is a next tile to stage (else this is the last tile)
+template <typename T, bool CS, int PAR>
+__device__ __forceinline__ void tile(Regs<T>& R, const Geo& G, const uint16_t* smem, const uint16_t* nxtA,
+                                     const uint16_t* nxtB, bool issue, int wave, const bool (&act)[2][2],
+                                     bool cs_q1, const typename WMF16<T>::e8& ones) {
+  // counted waits (2 LDS-DMA pieces per wave per phase): what the NEXT phase reads must have
+  // landed, the youngest issues may stay in flight
+  phase<T, CS, 0, PAR, 4, 2>(R, G, smem, nxtA, nxtB, issue, wave, act, cs_q1, ones);
+  phase<T, CS, 1, PAR, 4, 0>(R, G, smem, nxtA, nxtB, issue, wave, act, cs_q1, ones);
+  phase<T, CS, 2, PAR, 6, 0>(R, G, smem, nxtA, nxtB, issue, wave, act, cs_q1, ones);
+  phase<T, CS, 3, PAR, 4, 0>(R, G, smem, nxtA, nxtB, issue, wave, act, cs_q1, ones);
+}
+}  // namespace pp
+
+template <typename T, bool CS>
+__global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __restrict__ A,
+                                                          const uint16_t* __restrict__ B, float* __restrict__ ws,
+                                                          int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
+                                                          int64_t t_split, float* __restrict__ cs) {
+  using namespace pp;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tiles_n = (N + TM - 1) / TM, tiles_k = (K + TN - 1) / TN;
+  int split, tn, tk;
+  wg_map(tiles_n, tiles_k, 1, split, tn, tk);
+  const int64_t t_begin = split * t_split;
+  const int64_t t_end = t_begin + t_split < Tn ? t_begin + t_split : Tn;
+  const int64_t ntiles = t_end > t_begin ? (t_end - t_begin) / kBK : 0;
+  const int n0 = tn * TM, k0 = tk * TN;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  Geo G;
+  {
+    // transposed reads: lane 4q + p of group g -> token row q of quad (.. + g), columns 4p..4p+3
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, gb = g & 1;
+    const int common = g * 1024 + q * 32 + p * 8;  // bytes
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int adj = gb ? (par ? -128 : 128) : 0;  // block index XOR (quad & 1)
+      G.lbA[par] = (wm * 4 * 128 + adj + common) / 2;
+      G.lbB[par] = (wn * 2 * 128 + adj + common) / 2;
+    }
+    // staging: lane -> (physical block b, token tq, 8-column piece ch) of quad 2 * wave + u
+    const int b = lane >> 3, tq = (lane >> 1) & 3, ch = lane & 1;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int row = (2 * wave + u) * 4 + tq;
+      const int col = ((b ^ u) * 16 + ch * 8);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ca = min(n0 + h * 128 + col, N - 8);
+        const int cb = min(k0 + h * 128 + col, K - 8);
+        G.vA[h][u] = static_cast<uint32_t>((row * static_cast<int64_t>(lda) + ca) * 2);
+        G.vB[h][u] = static_cast<uint32_t>((row * static_cast<int64_t>(ldb) + cb) * 2);
+      }
+    }
+  }
+  bool act[2][2];
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) act[qa][qb] = (n0 + qa * 128 + wm * 64 < N) && (k0 + qb * 128 + wn * 32 < K);
+  // bias-gradient quadrant: the last K tile with no valid column past 128 -> wave column 0
+  // turns its (qa, 1) quadrants into row sums of A
+  const bool cs_q1 = CS && wn == 0 && tk == tiles_k - 1 && K - k0 <= 128;
+
+  Regs<T> R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) R.acc[a][b2][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typename WMF16<T>::e8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = 1.0f;
+
+  if (ntiles > 0) {
+    const uint16_t* a0 = A + t_begin * lda;
+    const uint16_t* b0 = B + t_begin * ldb;
+    const int64_t stepA = kBK * lda, stepB = kBK * ldb;
+    // prologue: tile 0's four halves into set 0; halves 0 and 1 (read first) must land
+    {
+      uint16_t* s0 = smem + (2 * wave) * 512;
+      lds_dma16_sv(a0, G.vA[0][0], s0);
+      lds_dma16_sv(a0, G.vA[0][1], s0 + 512);
+      lds_dma16_sv(b0, G.vB[0][0], s0 + kHalfElems);
+      lds_dma16_sv(b0, G.vB[0][1], s0 + kHalfElems + 512);
+      lds_dma16_sv(b0, G.vB[1][0], s0 + 2 * kHalfElems);
+      lds_dma16_sv(b0, G.vB[1][1], s0 + 2 * kHalfElems + 512);
+      lds_dma16_sv(a0, G.vA[1][0], s0 + 3 * kHalfElems);
+      lds_dma16_sv(a0, G.vA[1][1], s0 + 3 * kHalfElems + 512);
+      wait_vm<4>();
+    }
+    bar();
+    if (wm == 1) bar();  // row 1 runs one barrier behind row 0
+    for (int64_t t = 0; t < ntiles; t += 2) {
+      tile<T, CS, 0>(R, G, smem, a0 + (t + 1) * stepA, b0 + (t + 1) * stepB, t + 1 < ntiles, wave, act, cs_q1,
+                     ones);
+      if (t + 1 < ntiles)
+        tile<T, CS, 1>(R, G, smem, a0 + (t + 2) * stepA, b0 + (t + 2) * stepB, t + 2 < ntiles, wave, act, cs_q1,
+                       ones);
+    }
+    if (wm == 0) bar();  // balance row 1's extra barrier
+  }
+
+  // fp32 partial tile of this split; lane l holds C[4 (l / 16) + r][l % 16] of each 16 x 16 tile
+  float* out = ws + static_cast<int64_t>(split) * N * K;
+  const int col_l = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = k0 + qb * 128 + wn * 32 + j * 16 + col_l;
+        if (k >= K) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int nb = n0 + qa * 128 + wm * 64 + i * 16 + rq;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (nb + r < N) out[static_cast<int64_t>(nb + r) * K + k] = R.acc[qa][qb][i][j][r];
+        }
+      }
+  if (CS && cs_q1 && col_l == 0) {
+    float* cso = cs + static_cast<int64_t>(split) * N;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int nb = n0 + qa * 128 + wm * 64 + i * 16 + rq;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nb + r < N) cso[nb + r] = R.acc[qa][1][i][0][r];
+      }
+  }
+}
+
+template <typename T, bool CS>
+int launch_pp(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
+              int64_t ldb, int64_t t_split, int grid, hipStream_t s, float* cs) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_pp_kernel<T, CS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(pp::kLds));
+    attr_set = true;
+  }
+  wgrad_pp_kernel<T, CS><<<grid, 512, pp::kLds, s>>>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, cs);
+  return 0;
+}
+
+// the ping-pong kernel's bias-gradient quadrant exists for this K
+__host__ __device__ __forceinline__ bool wgrad_pp_cs_ok(int K) { return K % 256 != 0 && K % 256 <= 128; }
+
 // C (+)= sum over splits of ws, 4 elements per thread
 template <typename TO>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, TO* __restrict__ c,
@@ -463,7 +749,7 @@ int wgrad_splits(int64_t tokens, int n, int k, int num_cus) {
 
 int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, int64_t tokens, int n, int k,
           int64_t lda, int64_t ldb, int splits, int accumulate, hipStream_t s, int bias_dt, void* bias, float* cs,
-          int bias_accumulate) {
+          int bias_accumulate, int impl) {
   // whole 64-token tiles only (the caller adds the token remainder)
   if (n % 8 != 0 || k % 8 != 0 || lda % 8 != 0 || ldb % 8 != 0 || splits < 1 || tokens % TK != 0) return -1;
   if (bias != nullptr && (dt != BF16 || cs == nullptr)) return -3;  // column sums: bf16 operands
@@ -473,7 +759,24 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   const int grid = tiles * splits;
   const auto* pa = static_cast<const uint16_t*>(a);
   const auto* pb = static_cast<const uint16_t*>(b);
-  if (bias != nullptr || dt == BF16)
+  // SMP_WGRAD_IMPL=glds keeps the round-4 one-barrier-per-tile kernel (A/B); the ping-pong
+  // kernel needs 32-bit staging offsets and, for a fused bias gradient, its ones quadrant
+  static const bool env_glds = [] {
+    const char* e = getenv("SMP_WGRAD_IMPL");
+    return e != nullptr && strcmp(e, "glds") == 0;
+  }();
+  const bool use_glds = impl == 0 || (impl < 0 && env_glds);
+  const bool pp_ok = !use_glds && lda < (1 << 24) && ldb < (1 << 24) && (bias == nullptr || wgrad_pp_cs_ok(k));
+  if (pp_ok) {
+    if (bias != nullptr)
+      launch_pp<bf16, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
+    else if (dt == BF16)
+      launch_pp<bf16, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
+    else if (dt == F16)
+      launch_pp<f16, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
+    else
+      return -2;
+  } else if (bias != nullptr || dt == BF16)
     launch_glds16<bf16, kTK, kNS>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
   else if (dt == F16)
     launch_glds16<f16, kTK, kNS>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s);
@@ -492,7 +795,7 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
   else
     return -2;
   if (bias != nullptr) {
-    const int parts = splits * (wgrad_cs_idle(k) ? 1 : (k + TN - 1) / TN);
+    const int parts = splits * ((pp_ok || wgrad_cs_idle(k)) ? 1 : (k + TN - 1) / TN);
     const unsigned g = static_cast<unsigned>((n + 255) / 256);
     if (bias_dt == F32)
       colsum_reduce_kernel<float><<<g, 256, 0, s>>>(cs, static_cast<float*>(bias), n, parts, bias_accumulate);

@@ -20,6 +20,12 @@
 //    share one) and pulls the bytes with one hipMemcpyAsync D2D on its current stream (the
 //    transport's communication stream).  No receive pool is needed because the destination
 //    is an ordinary caching-allocator tensor of the receiver.
+//  * pull engine, chosen per mapping (SMP_P2P_PULL_ENGINE = auto | kernel | sdma): when the
+//    mapped segment lives on ANOTHER GPU (hipPointerGetAttributes), hipMemcpyAsync -- the
+//    copy engines (SDMA) move the bytes over xGMI and no CU is taken from the compute kernels
+//    the pull overlaps; when both stages share ONE GPU, a copy kernel (smpk::device_copy):
+//    there, >= 100 MB hipMemcpyAsync pulls blocked the host thread with four processes
+//    time-sharing the GPU (profiles/r4/pp4_hang_root_cause.md).
 //  * lifetime: the sender keeps the source tensors and the event slot until the receiver
 //    reports (release message, Python side) that its copy has completed.
 #include <ATen/ATen.h>
@@ -32,6 +38,7 @@
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -213,19 +220,30 @@ class IpcP2P {
       std::memcpy(&h, mh.data(), sizeof(h));
       void* p = nullptr;
       hip_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-      imports_[key] = Mapping{gen, p, 0};
+      bool remote = false;
+      hipPointerAttribute_t attr;
+      if (hipPointerGetAttributes(&attr, p) == hipSuccess) remote = attr.device >= 0 && attr.device != device_;
+      (void)hipGetLastError();
+      imports_[key] = Mapping{gen, p, 0, remote};
       it = imports_.find(key);
       stats_maps_++;
     }
     it->second.last_use = ++use_clock_;
     hipStream_t s = at::hip::getCurrentHIPStream(device_).stream();
     if (nbytes > 0) {
-      // a copy kernel on the pull stream, not hipMemcpyAsync: with four processes time-sharing
-      // one GPU, >= 100 MB hipMemcpyAsync pulls blocked the host thread indefinitely (PP=4
-      // micro-batch 16 rehearsal, tools/gpu_pp_hang.sh); 50 MB pulls did not
-      hip_check(static_cast<hipError_t>(smpk::device_copy(dst.data_ptr(), static_cast<char*>(it->second.ptr) + offset,
-                                                          nbytes, s)),
-                "device_copy");
+      const char* srcp = static_cast<char*>(it->second.ptr) + offset;
+      const bool sdma = engine_ == kEngineSdma || (engine_ == kEngineAuto && it->second.remote);
+      if (sdma) {
+        hip_check(hipMemcpyAsync(dst.data_ptr(), srcp, static_cast<size_t>(nbytes), hipMemcpyDeviceToDevice, s),
+                  "hipMemcpyAsync (pull)");
+        stats_pulls_sdma_++;
+      } else {
+        // same GPU: a copy kernel on the pull stream, not hipMemcpyAsync -- with four processes
+        // time-sharing one GPU, >= 100 MB hipMemcpyAsync pulls blocked the host thread
+        // indefinitely (PP=4 micro-batch 16 rehearsal, tools/gpu_pp_hang.sh)
+        hip_check(static_cast<hipError_t>(smpk::device_copy(dst.data_ptr(), srcp, nbytes, s)), "device_copy");
+        stats_pulls_kernel_++;
+      }
     }
     stats_imports_++;
     stats_bytes_in_ += nbytes;
@@ -272,6 +290,12 @@ class IpcP2P {
     d["mappings_open"] = static_cast<int64_t>(imports_.size());
     d["mappings_evicted"] = stats_evicted_;
     d["staged_exports"] = stats_staged_;
+    d["pull_engine"] = engine_ == kEngineSdma ? "sdma" : engine_ == kEngineKernel ? "kernel" : "auto";
+    d["pulls_sdma"] = stats_pulls_sdma_;
+    d["pulls_kernel"] = stats_pulls_kernel_;
+    int64_t remote_maps = 0;
+    for (auto& kv : imports_) remote_maps += kv.second.remote ? 1 : 0;
+    d["mappings_remote_gpu"] = remote_maps;
     d["staging_buffers"] = static_cast<int64_t>(staging_.size());
     d["bytes_out"] = stats_bytes_out_;
     d["bytes_in"] = stats_bytes_in_;
@@ -291,7 +315,17 @@ class IpcP2P {
     int64_t gen;
     void* ptr;
     uint64_t last_use;
+    bool remote;  // the segment lives on another GPU (pull over xGMI)
   };
+  static constexpr int kEngineAuto = 0, kEngineKernel = 1, kEngineSdma = 2;
+  static int engine_from_env() {
+    const char* e = getenv("SMP_P2P_PULL_ENGINE");
+    if (e == nullptr) return kEngineAuto;
+    if (strcmp(e, "kernel") == 0) return kEngineKernel;
+    if (strcmp(e, "sdma") == 0) return kEngineSdma;
+    return kEngineAuto;
+  }
+  int engine_ = engine_from_env();
 
   // largest caching-allocator segment exported in place
   static constexpr size_t kMaxExportSegment = size_t(1) << 30;
@@ -379,7 +413,7 @@ class IpcP2P {
   std::map<std::pair<int, int64_t>, Mapping> imports_;
   uint64_t use_clock_ = 0;
   int64_t stats_exports_ = 0, stats_exports_new_ = 0, stats_imports_ = 0, stats_maps_ = 0, stats_evicted_ = 0;
-  int64_t stats_staged_ = 0;
+  int64_t stats_staged_ = 0, stats_pulls_sdma_ = 0, stats_pulls_kernel_ = 0;
   int64_t stats_bytes_out_ = 0, stats_bytes_in_ = 0;
 };
 

@@ -22,6 +22,7 @@ from ..torch.state_mod import state
 from ..ops.pack import strided_copy_
 from ..parallel.throttle import throttler
 from ..parallel import oneshot
+from ..parallel.comm_timer import timer as _comm_timer
 
 
 # --------------------------------------------------------------------- topology
@@ -81,7 +82,7 @@ def _allgather(x, dim, sizes=None):
     out_shape[dim] = sum(sizes)
     if dim == 0 and even:  # rank blocks are already the final layout
         out = x.new_empty(out_shape)
-        with throttler().throttle(x):
+        with throttler().throttle(x), _comm_timer.region("tp", x.device):
             dist.all_gather_into_tensor(out, x, group=group)
         return out
     x3 = _split3(x, dim)  # [A, n, B]
@@ -89,7 +90,7 @@ def _allgather(x, dim, sizes=None):
     send = x.new_empty((mx, A, B))
     strided_copy_(send[: x3.shape[1]], x3.permute(1, 0, 2))
     recv = x.new_empty((ws, mx, A, B))
-    with throttler().throttle(send):
+    with throttler().throttle(send), _comm_timer.region("tp", send.device):
         dist.all_gather_into_tensor(recv.view(ws * mx, A, B), send, group=group)
     out = x.new_empty(out_shape)
     o3 = out.view(A, sum(sizes), B)
@@ -120,7 +121,7 @@ def _reduce_scatter(x, dim, sizes=None):
     if dim == 0 and even:
         x = x.contiguous()
         out = x.new_empty(out_shape)
-        with throttler().throttle(x):
+        with throttler().throttle(x), _comm_timer.region("tp", x.device):
             dist.reduce_scatter_tensor(out, x, group=group)
         return out
     x3 = _split3(x, dim)
@@ -134,7 +135,7 @@ def _reduce_scatter(x, dim, sizes=None):
             strided_copy_(inp[r, :n], x3[:, off:off + n].permute(1, 0, 2))
             off += n
     red = x.new_empty((mx, A, B))
-    with throttler().throttle(inp):
+    with throttler().throttle(inp), _comm_timer.region("tp", inp.device):
         dist.reduce_scatter_tensor(red, inp.view(ws * mx, A, B), group=group)
     out = x.new_empty(out_shape)
     strided_copy_(out.view(A, sizes[me], B).permute(1, 0, 2), red[: sizes[me]])
@@ -149,7 +150,7 @@ def _allreduce(x, inplace=False):
         return x
     if not inplace or not x.is_contiguous():
         x = x.clone(memory_format=torch.contiguous_format)
-    with throttler().throttle(x):
+    with throttler().throttle(x), _comm_timer.region("tp", x.device):
         oneshot.all_reduce(x, group=tp_group())
     return x
 
@@ -194,7 +195,7 @@ def _all_to_all(x, split_dim, merge_dim, split_sizes=None, merge_sizes=None):
             off += n
         rn = [int(torch.Size(s).numel()) for s in out_shapes]
         recv = x.new_empty(sum(rn))
-        with throttler().throttle(x):
+        with throttler().throttle(x), _comm_timer.region("tp", x.device):
             dist.all_to_all_single(recv, send, output_split_sizes=rn, input_split_sizes=numels, group=group)
         out = x.new_empty(out_shape)
         off, moff = 0, 0

@@ -151,7 +151,9 @@ def _wgrad_native_ok(g, dy2, x2):
 # GPT-2 XL (T = 65536, profiles/r2/session4_wgrad_pick_ab.md, profiles/r3/wgrad_variants.md);
 # (4800, 1600): s7 in the b32 step with the fused bias sums (1092-1099 us vs s5 1131, s8 1167).
 # BASELINE config 3-5 rank shapes (scaled-batch TP): tools/wgrad_table.py, profiles/r4/.
-_WGRAD_STATIC = {(1600, 6400): 0, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7,
+# Round 5 (ping-pong kernel, tools/wgrad_pp_ab.py, profiles/r5/wgrad_pp.md): the kernel now wins
+# every GPT-2 XL shape, fc2's (1600, 6400) included (s4 1325 us vs library 1891 us isolated).
+_WGRAD_STATIC = {(1600, 6400): 4, (6400, 1600): 4, (1600, 1600): 5, (4800, 1600): 7,
                  # GPT-J TP4 attention output (T = 16384): s4 137 us vs library 168 us; GPT-NeoX
                  # TP4 QKV: s1 959 vs 1034 us; the other config 3-5 shapes measured library-best
                  (4096, 1024): 4, (4608, 6144): 1}
@@ -349,7 +351,10 @@ class _LinearWGradAccum(torch.autograd.Function):
             if btarget is not bparam.grad:
                 grads[bidx] = btarget.to(bparam.dtype)
         if work is not None:
-            work.wait()
+            from ..parallel.comm_timer import timer as _comm_timer
+
+            with _comm_timer.region("tp", dy.device):
+                work.wait()
             if TRACE_TP_OVERLAP:
                 TP_OVERLAP_TRACE.append("dx_allreduce_wait")
         return dx, dw, grads[2], None, grads[4]

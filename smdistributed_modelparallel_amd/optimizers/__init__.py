@@ -103,6 +103,17 @@ def _pp_sum_(x):
     return x
 
 
+def _any_device(opt):
+    """A device for this optimizer's collectives when it holds no gradient: a parameter's, else
+    the current GPU, else the CPU."""
+    for g in opt.param_groups:
+        for p in g["params"]:
+            return p.device
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 class FusedLAMB(torch.optim.Optimizer):
     """LAMB (apex FusedLAMB + the reference's PP-global gradient norm): the gradient is divided
     by max(1, ||g||_global / max_grad_norm), stage 1 forms the Adam direction (+ decoupled or
@@ -130,6 +141,10 @@ class FusedLAMB(torch.optim.Optimizer):
         groups = [(gi, g, _lists(self, g, ("exp_avg", "exp_avg_sq"))) for gi, g in enumerate(self.param_groups)]
         dev = next((b["grad"][0].device for _, _, bs in groups for b in bs.values()), None)
         if dev is None:
+            # no local gradient (e.g. a pipeline stage whose parameters all went unused): still
+            # join the pipeline-group norm all-reduce with a zero, as the reference's all-gather
+            # does (`optimizers/fused_lamb.py:34-53`) -- the other stages are waiting in it
+            _pp_sum_(torch.zeros(1, dtype=torch.float32, device=_any_device(self)))
             return loss
         # global gradient norm: every group, every dtype, then over the pipeline stages
         gsq = torch.zeros(1, dtype=torch.float32, device=dev)

@@ -2,8 +2,11 @@
 
 Every point where the compute stream has to wait for communication -- the data-parallel
 reducer's final ``synchronize()`` over the bucket all-reduces (reference `ddp_model.py:605-632`
-pre/post DDP step) and the pipeline transport's wait on a pulled activation / gradient
-(reference `server_comm.py:260-302`) -- is bracketed by two HIP events on the compute stream
+pre/post DDP step), the pipeline transport's wait on a pulled activation / gradient
+(reference `server_comm.py:260-302`) and every tensor-parallel collective the compute stream
+waits for (the forward / backward TP all-reduces, all-gathers, reduce-scatters and
+all-to-alls of `nn/utils.py`, reference `torch/nn/utils.py:548,570`; for the asynchronous
+input-gradient all-reduce only its final wait) -- is bracketed by two HIP events on the compute stream
 while the timer is enabled.  The time between them on the GPU is exactly how long compute
 stood still for communication: the collective's overlapped part (it ran beside backward
 kernels) does not appear.  On CPU (gloo) the waits block the host, so wall time is used.
@@ -18,7 +21,7 @@ import torch
 
 
 class ExposedCommTimer:
-    KINDS = ("dp", "p2p")
+    KINDS = ("dp", "p2p", "tp")
 
     def __init__(self):
         self.enabled = False

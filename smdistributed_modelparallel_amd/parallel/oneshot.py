@@ -24,9 +24,10 @@ Failures after set-up are never silent: a kernel that waits longer than
 peer -- a rank skipped a call, died, or drifted away -- writes NaN instead of reducing stale
 slots, raises the instance's host-mapped error word and pushes an abort into every peer's
 flag array, so the peers' kernels fail too.  ``check_errors()`` (called by
-``DistributedModel`` at the end of every step, before the optimizer update: waits for the
-step's kernels, then the TP ranks agree on the verdict) raises ``OneShotAllReduceError`` on
-every rank of the group in the same step, and the failed instance refuses all later calls.
+``DistributedModel`` at the end of every step: reads the error words behind the previous
+step's end event, then the TP ranks agree on the verdict) raises ``OneShotAllReduceError`` on
+every rank of the group in the same step, and the failed instance refuses all later calls;
+checkpoint saves check with a full synchronisation first.
 """
 import os
 import socket
@@ -58,6 +59,7 @@ def _key(group):
 
 
 def reset():
+    _pending.clear()
     for inst in _instances.values():
         if inst is not None:
             try:
@@ -176,20 +178,34 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None, async_op=False):
     return x
 
 
-def check_errors(group=None):
+_pending = []  # [event recorded at the end of the previous checked step]
+
+
+def check_errors(group=None, sync=False):
     """Raise ``OneShotAllReduceError`` if a one-shot all-reduce of any group failed (own
     timeout, or a peer's abort) -- on every rank of `group` (the TP group's gloo twin) in the
-    SAME step, before the optimizer update: the step's kernels are waited for before the
-    host-mapped error words are read, and the ranks agree on the verdict (a MAX over
-    `group`).  Without the wait and the agreement, a peer whose poisoned kernel was still
-    running passed the check and applied NaN gradients.  Costs one stream
-    synchronisation and one 4-byte gloo all-reduce per step, only while one-shot instances
-    exist.  The failed instance stays disabled."""
+    SAME step: the ranks agree on the verdict (a MAX over `group`), so a peer whose poisoned
+    kernel was still running cannot pass the check alone.
+
+    No full stream synchronisation per step: the error words are read after
+    the event recorded at the end of the PREVIOUS checked step -- a step whose kernels have
+    normally finished long ago, so the host does not stall and keeps at most one step of
+    run-ahead -- and a fresh event is recorded for the next check.  A failure is therefore
+    raised at the end of the step in which it happened or of the next one, on every rank of
+    the group at once.  ``sync=True`` (checkpoint saves, teardown) waits for the current
+    stream first, so nothing unchecked is persisted.  Costs one 4-byte gloo all-reduce per
+    step, only while one-shot instances exist.  The failed instance stays disabled."""
     active = [(k, inst) for k, inst in _instances.items() if inst is not None]
     if not active and not _failed:
         return
     if torch.cuda.is_available():
-        torch.cuda.current_stream().synchronize()
+        if sync:
+            torch.cuda.current_stream().synchronize()
+        elif _pending:
+            _pending[0].synchronize()
+        ev = torch.cuda.Event()
+        ev.record()
+        _pending[:] = [ev]
     for k, inst in active:
         if k in _failed or inst.error(False):
             _failed.add(k)

@@ -7,7 +7,9 @@ same steps and keep the same scale:
 * a stage that never calls ``scale()`` (every pp_rank but the loss stage) initialises its
   scale lazily at ``unscale_``/``step`` (reference `:164-165`);
 * a stage without local parameters records a zero found-inf instead of torch's "No inf
-  checks were recorded" error (reference `:169-183`), and skips ``optimizer.step()``;
+  checks were recorded" error (reference `:169-183`), and still calls ``optimizer.step()``
+  when no rank found an inf: the step can itself run collectives (the fp16 overflow check,
+  sharded-DP clipping, FusedLAMB's pipeline norm) that every stage must join;
 * the collective count is fixed -- exactly one MAX all-reduce of a one-element device tensor
   per ``step()`` and one per ``update()``, whatever number of devices or optimizers recorded
   checks -- so ranks with different local state never issue mismatched collectives (the
@@ -43,11 +45,6 @@ class GradScaler(torch.amp.GradScaler):
             dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=state.pgs.mp)
         return flag
 
-    @staticmethod
-    def _has_local_params():
-        model = state.model if state.initialized else None
-        return model is None or any(True for _ in model.local_parameters())
-
     def unscale_(self, optimizer):
         if not self._enabled:
             return
@@ -71,7 +68,7 @@ class GradScaler(torch.amp.GradScaler):
         local = sum(v.to(self._dev()).float().sum() for v in st["found_inf_per_device"].values())
         found = self._combine(torch.as_tensor(local))
         retval = None
-        if found.item() == 0 and self._has_local_params():
+        if found.item() == 0:
             retval = optimizer.step(*args, **kwargs)
         st["stage"] = OptState.STEPPED
         return retval

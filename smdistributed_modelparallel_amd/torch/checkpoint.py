@@ -110,6 +110,10 @@ def save_checkpoint(path, tag, partial=True, model=None, optimizer=None, user_co
         logger.warning("sharded data parallelism saves partial checkpoints only")
         partial = True
     _check_tag(tag)
+    # the per-step one-shot all-reduce check runs one step behind; nothing unchecked is persisted
+    from ..parallel import oneshot
+
+    oneshot.check_errors(state.pgs.cpu_tp if state.pgs is not None else None, sync=True)
     if partial:
         tag = f"{tag}_partial"
         os.makedirs(os.path.join(path, tag), exist_ok=True)

@@ -48,7 +48,14 @@ def _decide_all_ones(args, kwargs):
              if getattr(t, "_smp_all_ones", (None,))[0] != t._version]
     if not cands:
         return
-    flags = torch.stack([(t != 0).all() for t in cands]).tolist()
+    # one batched reduction per device (CPU labels beside a GPU mask must not meet in a stack)
+    by_dev = {}
+    for i, t in enumerate(cands):
+        by_dev.setdefault(t.device, []).append(i)
+    flags = [False] * len(cands)
+    for idx in by_dev.values():
+        for i, f in zip(idx, torch.stack([(cands[i] != 0).all() for i in idx]).tolist()):
+            flags[i] = f
     for t, f in zip(cands, flags):
         try:
             t._smp_all_ones = (t._version, bool(f))

@@ -301,6 +301,13 @@ def test_amp_grad_scaler_pp2_stage_without_params():
     assert "local_params=0" in outs[1]
 
 
+def test_fused_lamb_pp2_stage_without_grads():
+    """FusedLAMB joins the pipeline-group norm all-reduce on a stage with no gradients
+    (an early return there hung the other stage)."""
+    outs = run_workers("lamb_pp", 2, [], timeout=200)
+    assert all("OK" in o for o in outs), outs
+
+
 @pytest.mark.parametrize("pp", [1, 2])
 def test_ddp_buffers_follow_rank0_every_step(pp):
     """Per-step buffer broadcast from DP rank 0 (reference ddp_model.py:518-540,605-607)."""

@@ -111,3 +111,17 @@ def test_optimizer_state_offload_matches_resident(tmp_path):
         for n in a["params"]:
             assert torch.equal(a["params"][n], b["params"][n]), n
         assert torch.equal(a["m0"], b["m0"])
+
+
+def test_all_ones_decision_mixed_devices():
+    """The pipeline's once-per-step all-ones mask decision groups its candidates by device:
+    a GPU padding mask beside CPU labels / position ids (one torch.stack over both
+    raised)."""
+    from smdistributed_modelparallel_amd.torch.step import _decide_all_ones
+
+    mask = torch.ones(4, 16, dtype=torch.int64, device="cuda")
+    labels = torch.randint(1, 50, (4, 16))
+    pos = torch.zeros(4, 16, dtype=torch.int64, device="cuda")
+    _decide_all_ones((mask, labels), {"position_ids": pos})
+    assert mask._smp_all_ones[1] is True and labels._smp_all_ones[1] is True
+    assert pos._smp_all_ones[1] is False

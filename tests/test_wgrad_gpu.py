@@ -178,3 +178,46 @@ def test_mlp_dense1_bias_grad_through_wgrad_kernel(monkeypatch):
         err = (g - want).abs().max().item() / scale
         assert err < 3e-2, (fused, err)
     assert (grads[True] - grads[False]).abs().max().item() / scale < 3e-2
+
+
+@pytest.mark.parametrize("shape", [(64, 256, 256), (192, 520, 264), (4160, 1040, 1000), (8192, 4800, 1600),
+                                   (12288, 1600, 6400), (2048, 264, 1032)])
+@pytest.mark.parametrize("impl", [0, 1])
+def test_wgrad_impls_match_fp32(shape, impl):
+    """Both kernels of csrc/kernels/wgrad.hip (1 = ping-pong, 0 = one barrier per tile) against
+    fp32 torch by relative norm: 1-3 token tiles (prologue / tail paths), odd tile counts,
+    split counts that leave a split with no tokens, edge row / column tiles."""
+    from smdistributed_modelparallel_amd.ops._ext import ext
+
+    T, N, K = shape
+    g0 = torch.Generator(device="cuda").manual_seed(11)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    ref = dy.float().t() @ x.float()
+    for splits in (1, 2, 3, 7):
+        h = torch.full((N, K), float("nan"), device="cuda", dtype=torch.float32)
+        ext().wgrad_(h, dy, x, False, splits, impl=impl)
+        rel = ((h - ref).norm() / ref.norm()).item()
+        assert rel < 1e-5, (splits, rel)
+
+
+@pytest.mark.parametrize("shape", [(4096, 1600, 1600), (8256, 4800, 1600), (5000, 392, 1048), (4160, 1040, 1000)])
+def test_wgrad_pp_bias_quadrant(shape):
+    """The ping-pong kernel's bias-gradient quadrant (K % 256 in [1, 128]: B fragment = ones in
+    the idle qb = 1 quadrant of the last K tile) against fp32 column sums, beside the
+    round-4 kernel's modes (K % 256 > 128: LDS column sums) on the same call API."""
+    from smdistributed_modelparallel_amd.ops._ext import ext
+
+    T, N, K = shape
+    g0 = torch.Generator(device="cuda").manual_seed(12)
+    dy = torch.randn(T, N, device="cuda", dtype=torch.bfloat16, generator=g0)
+    x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
+    ref_g = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    for impl in (1, 0):
+        for splits in (1, 4):
+            g = torch.zeros(N, K, device="cuda", dtype=torch.float32)
+            b = torch.zeros(N, device="cuda", dtype=torch.float32)
+            ext().wgrad_(g, dy, x, True, splits, b, True, impl=impl)
+            assert ((g - ref_g).norm() / ref_g.norm()).item() < 1e-5
+            assert ((b - ref_b).norm() / ref_b.norm()).item() < 1e-5, (impl, splits)
