@@ -284,18 +284,24 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
                                       at::Tensor rstd, bool need_wgrad, bool need_bgrad,
                                       c10::optional<at::Tensor> dres, c10::optional<at::Tensor> dw_out,
                                       c10::optional<at::Tensor> db_out, c10::optional<at::Tensor> ext_sums,
-                                      double ext_n) {
+                                      double ext_n, double dropout_p, int64_t seed, int64_t offset) {
   check_gpu(dy, "dy");
   check_gpu(x, "x");
   const int64_t cols = x.size(-1);
   const int64_t rows = x.numel() / cols;
   auto dx = at::empty_like(x);
+  // dropout_p > 0: also dxd = dropout backward of dx (the residual-branch dropout of a fused
+  // add + LayerNorm) from the same kernel when the block kernels serve this width
+  at::Tensor dxd;
+  smpk::DropoutArgs drop = dropout_args(dropout_p, seed, offset);
   const bool aligned = ((reinterpret_cast<uintptr_t>(x.data_ptr()) | reinterpret_cast<uintptr_t>(dy.data_ptr()) |
                          reinterpret_cast<uintptr_t>(dx.data_ptr()) |
                          (dres.has_value() ? reinterpret_cast<uintptr_t>(dres->data_ptr()) : 0) |
                          (w.has_value() ? reinterpret_cast<uintptr_t>(w->data_ptr()) : 0)) &
                         15) == 0;
   const int parts = smpk::layernorm_bwd_num_parts(dt_code(x), rows, cols, aligned);
+  if (drop.thr != 0 && !ext_sums.has_value() && smpk::layernorm_bwd_dropout_fusable(dt_code(x), cols, aligned))
+    dxd = at::empty_like(x);
   at::Tensor dwp, dbp, dw, db;
   int wdt = w.has_value() ? dt_code(*w) : dt_code(x);
   if (need_wgrad || need_bgrad) {
@@ -311,7 +317,7 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
                             rstd.data_ptr<float>(), dx.data_ptr(), dwp.defined() ? dwp.data_ptr<float>() : nullptr,
                             dbp.defined() ? dbp.data_ptr<float>() : nullptr, rows, cols, parts, opt_ptr(dres),
                             stream(), ext_sums.has_value() ? ext_sums->data_ptr<float>() : nullptr,
-                            static_cast<float>(ext_n)),
+                            static_cast<float>(ext_n), dxd.defined() ? dxd.data_ptr() : nullptr, &drop),
         "layernorm_bwd");
   if (dwp.defined()) {
     auto wo = w.has_value() ? w->options() : x.options();
@@ -331,6 +337,7 @@ std::vector<at::Tensor> layernorm_bwd(at::Tensor dy, at::Tensor x, c10::optional
                                      parts, cols, work.data_ptr<float>(), stream(), acc),
           "layernorm_bwd_reduce");
   }
+  if (dxd.defined()) return {dx, dw, db, dxd};
   return {dx, dw, db};
 }
 
@@ -726,7 +733,8 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
 void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
                         at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window,
                         c10::optional<at::Tensor> kbias, double dropout_p,
-                        int64_t seed, int64_t offset, c10::optional<at::Tensor> drop_bits) {
+                        int64_t seed, int64_t offset, c10::optional<at::Tensor> drop_bits, int64_t fused,
+                        c10::optional<at::Tensor> err_out) {
   smpk::AttnBwdParams P{};
   P.f = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   if (P.f.drop_on) {
@@ -759,7 +767,22 @@ void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor 
   auto delta = at::empty({P.f.b, P.f.h, P.f.sq}, q.options().dtype(at::kFloat));
   P.delta = delta.data_ptr<float>();
   P.dq_acc = nullptr;
+  P.dq_flags = P.dq_err = nullptr;
+  P.fused = 0;
+  at::Tensor acc, flags;
+  if (fused != 0 && smpk::attention_bwd_fused_ok(P)) {
+    // fused backward: fp32 dQ partials (one 16 KB slot per (b h, 64-query tile)) and the
+    // hand-off flags + error word, zeroed on the stream ahead of the kernel
+    const int64_t ntq = (P.f.sq + 63) / 64;
+    acc = at::empty({P.f.b * P.f.h * ntq * 4096}, q.options().dtype(at::kFloat));
+    flags = at::zeros({P.f.b * P.f.h * ntq + 4}, q.options().dtype(at::kInt));
+    P.dq_acc = acc.data_ptr<float>();
+    P.dq_flags = flags.data_ptr<int32_t>();
+    P.dq_err = P.dq_flags + P.f.b * P.f.h * ntq;
+    P.fused = 1;
+  }
   check(smpk::attention_bwd(dt_code(q), P, stream()), "attention_bwd");
+  if (err_out.has_value() && err_out->defined() && flags.defined()) err_out->copy_(flags.narrow(0, flags.numel() - 4, 1));
 }
 
 }  // namespace
@@ -791,7 +814,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_bwd", &dropout_bwd, py::arg("dy"), py::arg("p"), py::arg("seed"), py::arg("offset"));
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
         py::arg("need_wgrad"), py::arg("need_bgrad"), py::arg("dres"), py::arg("dw_out") = py::none(),
-        py::arg("db_out") = py::none(), py::arg("ext_sums") = py::none(), py::arg("ext_n") = 0.0);
+        py::arg("db_out") = py::none(), py::arg("ext_sums") = py::none(), py::arg("ext_n") = 0.0,
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
   m.def("layernorm_local_stats", &layernorm_local_stats);
   m.def("strided_copy_", &strided_copy_);
   m.def("add3", &add3);
@@ -821,5 +845,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
-        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("drop_bits") = py::none());
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("drop_bits") = py::none(),
+        py::arg("fused") = 0, py::arg("err_out") = py::none());
 }

@@ -83,7 +83,11 @@ int layernorm_fwd(int dt, const void* x, const void* residual, void* x_out, int 
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean,
                   const float* rstd, void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols,
                   int part_rows, const void* dres, hipStream_t s,
-                  const float* ext_sums = nullptr, float ext_n = 0.f);
+                  const float* ext_sums = nullptr, float ext_n = 0.f, void* dxd = nullptr,
+                  const DropoutArgs* drop = nullptr);
+// dxd (the dropout branch's gradient dx * keep / (1 - p), one pass with dx) is available for
+// these widths / alignment (the block-per-rows backward kernels)
+bool layernorm_bwd_dropout_fusable(int dt, int64_t cols, bool aligned);
 // dgamma/dbeta from the per-block partials; work = [kLnReduceSlices][2][cols] fp32 scratch.
 constexpr int kLnReduceSlices = 32;
 int layernorm_bwd_reduce(int wdt, const float* dw_part, const float* db_part, void* dw, void* db, int parts,
@@ -186,8 +190,16 @@ struct AttnBwdParams {
   int64_t dk_sb, dk_sh, dk_ss;
   int64_t dv_sb, dv_sh, dv_ss;
   float* delta;  // [b, h, sq] workspace
-  float* dq_acc;  // [b, h, sq, d] fp32 workspace
+  // fused backward (attention_d64_fused.hip): fp32 dQ partials [b h][ceil(sq / 64)][4096],
+  // per-(b h, query tile) hand-off flags and an error word, zeroed by the caller on the stream
+  float* dq_acc;
+  int* dq_flags;
+  int* dq_err;
+  int fused;  // 1: use the fused kernel (eligibility: attention_bwd_fused_ok)
 };
+// D = 64, causal self-attention without key bias / window: the fused single-kernel backward
+bool attention_bwd_fused_ok(const AttnBwdParams& p);
+int attention_bwd_fused_d64(int dt, const AttnBwdParams& p, hipStream_t s);
 int attention_fwd(int dt, const AttnParams& p, hipStream_t s);
 bool attention_head_dim_supported(int64_t d);
 int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);

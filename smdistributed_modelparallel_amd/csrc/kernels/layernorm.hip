@@ -518,9 +518,12 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
                                                   const float* __restrict__ rstd_in, T* __restrict__ dx,
                                                   float* __restrict__ dw_part, float* __restrict__ db_part,
                                                   int64_t rows, int cols, const T* __restrict__ dres,
-                                                  int64_t rows_per_block) {
+                                                  int64_t rows_per_block, T* __restrict__ dxd, DropoutArgs drop) {
   constexpr int N = Vec16<T>::N;
   __shared__ float red[2][2][4];  // [parity][s1|s2][wave]
+  // dxd != null: also the dropout branch's gradient dxd = dx * keep / (1 - p), decisions from the
+  // forward's element-index hash (the separate dropout_bwd pass re-read dx for this)
+  const uint32_t dkey = dxd != nullptr ? dropout_key(drop) : 0u;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int nvec = cols / N;
   float wv[VB][N], dwacc[VB][N], dbacc[VB][N];
@@ -587,9 +590,27 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
     for (int k = 0; k < VB; ++k) {
       if (!act[k]) continue;
       Vec16<T> o;
+      float dv[N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(rstd * (g[k][j] - s1 - xh[k][j] * s2) + rr[k][j]);
-      store16(dx + row * cols + static_cast<int64_t>(t + 256 * k) * N, o);
+      for (int j = 0; j < N; ++j) {
+        dv[j] = rstd * (g[k][j] - s1 - xh[k][j] * s2) + rr[k][j];
+        o.v[j] = from_f32<T>(dv[j]);
+      }
+      const int64_t off = row * cols + static_cast<int64_t>(t + 256 * k) * N;
+      store16(dx + off, o);
+      if (dxd != nullptr) {
+        // the dropout factor multiplies the ROUNDED dx, exactly as dropout_bwd(dx) did
+        float f[8];
+        if constexpr (N == 8) {
+          dropout_factors8(dkey, off, drop, f);
+        } else {
+#pragma unroll
+          for (int j = 0; j < N; ++j) f[j] = dropout_factor1(dkey, off + j, drop);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) o.v[j] = from_f32<T>(to_f32(o.v[j]) * f[j]);
+        store16(dxd + off, o);
+      }
     }
   }
   if (dw_part == nullptr) return;
@@ -782,7 +803,8 @@ static inline int ln_bwd_parts(int64_t rows, int64_t cols, bool reg_path) {
 
 int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w, const float* mean, const float* rstd,
                   void* dx, float* dw_part, float* db_part, int64_t rows, int64_t cols, int part_rows,
-                  const void* dres, hipStream_t s, const float* ext_sums, float ext_n) {
+                  const void* dres, hipStream_t s, const float* ext_sums, float ext_n, void* dxd,
+                  const DropoutArgs* drop) {
   if (rows <= 0) return 0;
   SMPK_DISPATCH(dt, T, {
     SMPK_DISPATCH(wdt, W, {
@@ -804,10 +826,16 @@ int layernorm_bwd(int dt, const void* dy, const void* x, int wdt, const void* w,
       const int64_t nvec = cols / N;
       const int64_t rpb = (rows + parts - 1) / parts;
       const bool blk_ok = ext_sums == nullptr;  // the block-per-rows form has no external-sum mode
-      if (blk_ok && reg && nvec <= 256 && nvec >= 128) {
-        ln_bwd_blk<T, W, 1><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
-      } else if (blk_ok && reg && nvec <= 512 && nvec > 256) {
-        ln_bwd_blk<T, W, 2><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb);
+      T* dxdd = static_cast<T*>(dxd);
+      const DropoutArgs dd = drop != nullptr ? *drop : DropoutArgs{};
+      const bool blk1 = blk_ok && reg && nvec <= 256 && nvec >= 128, blk2 = blk_ok && reg && nvec <= 512 && nvec > 256;
+      if (dxd != nullptr && !(blk1 || blk2)) return -4;  // fused dropout output: block kernels only
+      if (blk1) {
+        ln_bwd_blk<T, W, 1><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb, dxdd,
+                                                  dd);
+      } else if (blk2) {
+        ln_bwd_blk<T, W, 2><<<parts, 256, 0, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, rpb, dxdd,
+                                                  dd);
       } else if (reg && vpt <= 1) {
         ln_bwd_reg<T, W, 1><<<parts, 256, lds, s>>>(dyy, xx, ww, mean, rstd, dxx, dw_part, db_part, rows, c, dr, ext_sums, ext_n);
       } else if (reg && vpt <= 2) {
@@ -938,6 +966,13 @@ int layernorm_bwd_local_sums(int dt, const void* dy, const void* x, int wdt, con
 }
 
 // exported helper so bindings can size partial buffers
+bool layernorm_bwd_dropout_fusable(int dt, int64_t cols, bool aligned) {
+  const int N = dt == F32 ? 4 : 8;
+  if (!aligned || cols % N != 0) return false;
+  const int64_t nvec = cols / N, vpt = (cols + 64 * N - 1) / (64 * N);
+  return vpt <= 8 && nvec >= 128 && nvec <= 512;
+}
+
 int layernorm_bwd_num_parts(int dt, int64_t rows, int64_t cols, bool aligned) {
   const int N = dt == F32 ? 4 : 8;
   const int vpt = static_cast<int>((cols + 64 * N - 1) / (64 * N));

@@ -49,6 +49,7 @@ from .utils import (
     allgather_for_tp,
     bwd_allreduce_for_tp,
     dx_allreduce_async,
+    fwd_allreduce_async,
     fwd_allreduce_for_tp,
     get_local_channels,
     get_merge_shapes,
@@ -393,8 +394,9 @@ class DistributedAttentionLayer(DistributedModule):
                     use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
                     mask=mask, mask_value=getattr(self, "mask_value", -1e4),
                 )
-                out = linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias)
-                return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
+                # row-parallel: the TP all-reduce runs per token chunk beside the next chunk's GEMM
+                return linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias,
+                              fwd_ar=fwd_allreduce_async if self._tp > 1 and reduce else None)
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)
@@ -407,8 +409,8 @@ class DistributedAttentionLayer(DistributedModule):
             mask_value=getattr(self, "mask_value", -1e4),
         )
         ctx = ctx.reshape(B, s, lh * d)
-        out = linear(ctx, self.dense_weight, self.dense_bias)
-        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
+        return linear(ctx, self.dense_weight, self.dense_bias,
+                      fwd_ar=fwd_allreduce_async if self._tp > 1 and reduce else None)
 
     def _core_memory(self, a, mask):
         """optimize='memory': a is [B, s, h/tp] (hidden-sharded).  Partial QKV products
@@ -556,8 +558,8 @@ class DistributedTransformerOutputLayer(DistributedModule):
         x = linear(m, self.dense1_weight, dx_allreduce=dx_allreduce_async if self._tp > 1 else None,
                    dbias_of=self.dense1_bias if fuse_db else None)
         x = _activation(x, self.activation, self.dense1_bias, self._tanh_gelu, bias_grad=not fuse_db)
-        out = linear(x, self.dense2_weight, self.dense2_bias)
-        return (fwd_allreduce_for_tp(out, inplace=True) if self._tp > 1 and reduce else out)
+        return linear(x, self.dense2_weight, self.dense2_bias,
+                      fwd_ar=fwd_allreduce_async if self._tp > 1 and reduce else None)
 
     def forward(self, hidden):
         if self._tp > 1 and self.input_layer and not _prescaled():

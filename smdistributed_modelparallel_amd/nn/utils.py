@@ -265,6 +265,17 @@ def dx_allreduce_async(dx):
     return oneshot.all_reduce(dx, group=tp_group(), async_op=True)
 
 
+def fwd_allreduce_async(out):
+    """Forward all-reduce of a row-parallel output chunk (ops.linear's token-chunked path):
+    started without waiting -- the caller waits after issuing the next chunk's GEMM.  ``out``
+    is a fresh GEMM output chunk: reduced in place.  Returns the work handle (None when the
+    one-shot kernel ran: it is already ordered on the current stream)."""
+    if tp_size() == 1:
+        return None
+    with throttler().throttle(out):
+        return oneshot.all_reduce(out, group=tp_group(), async_op=True)
+
+
 class _Allgather(torch.autograd.Function):
     """fwd all-gather along dim; bwd narrow (each rank keeps its own slice)."""
 

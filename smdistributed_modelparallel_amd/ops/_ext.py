@@ -13,10 +13,47 @@ _C = None
 _err = None
 
 
+class _Counting:
+    """Proxy of the extension that counts calls into it (``track_calls``)."""
+
+    def __init__(self, mod, counts):
+        self._mod, self._counts = mod, counts
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+        counts = self._counts
+
+        def call(*a, **k):
+            counts[name] = counts.get(name, 0) + 1
+            return fn(*a, **k)
+
+        return call
+
+
+_tracking = []  # stack of count dicts of the active track_calls() contexts
+
+
+class track_calls:
+    """``with track_calls() as counts:`` -- every call into the HIP extension made through
+    ``ext()`` inside the block is counted by function name (tests use it to prove that a
+    reference pass ran no in-tree kernel, or that a fused path did)."""
+
+    def __enter__(self):
+        self.counts = {}
+        _tracking.append(self.counts)
+        return self.counts
+
+    def __exit__(self, *exc):
+        _tracking.remove(self.counts)
+        return False
+
+
 def ext():
     global _C, _err
     if _C is not None:
-        return _C
+        return _Counting(_C, _tracking[-1]) if _tracking else _C
     if _err is not None:
         raise HIPExtensionMissingError(_err)
     try:
@@ -29,7 +66,7 @@ def ext():
             f"(SMP_OFFLOAD_ARCH={os.environ.get('SMP_OFFLOAD_ARCH', 'gfx950')})"
         )
         raise HIPExtensionMissingError(_err)
-    return _C
+    return _Counting(_C, _tracking[-1]) if _tracking else _C
 
 
 def available():

@@ -12,6 +12,7 @@ GPU paths:
 CPU: PyTorch reference math.
 """
 import math
+import os
 
 import torch
 
@@ -128,6 +129,14 @@ def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu")
     return (u >= thr).view(b, h, sq, sk)
 
 
+# Fused single-kernel backward for D = 64 causal self-attention (csrc/kernels/attention_d64_fused.hip:
+# dK, dV and dQ in one pass with a deterministic ordered dQ hand-off).  SMP_ATTN_FUSED_BWD=1 turns
+# it on; FUSED_BWD_ERR[0], when set to an int32 [1] GPU tensor, receives the hand-off's error word
+# (a timed-out wait) after every fused backward -- tests assert it stays 0.
+FUSED_BWD = [os.environ.get("SMP_ATTN_FUSED_BWD", "0") == "1"]
+FUSED_BWD_ERR = [None]
+
+
 # forward launches of the flash kernels by variant, for run reports (bench.py "attention_calls":
 # a pipeline stage whose padding masks were decided all-ones launches no key-bias variant)
 FLASH_CALLS = {"plain": 0, "key_bias": 0}
@@ -157,7 +166,7 @@ class _FlashAttention(torch.autograd.Function):
         kb = ctx.kb
         bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
-                                 bias, p, seed, off, bits if p > 0.0 else None)
+                                 bias, p, seed, off, bits if p > 0.0 else None, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -186,7 +195,7 @@ class _FlashAttentionPacked(torch.autograd.Function):
         bias = kb.bias if kb is not None else None
         ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
                                  dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off,
-                                 bits if p > 0.0 else None)
+                                 bits if p > 0.0 else None, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
         return dqkv, None, None, None, None, None
 
 

@@ -12,15 +12,27 @@ from .dropout import dropout_seed_offset
 from .linear import _fusable
 
 
-def _ln_bwd(dy, x, w, b, mean, rstd, need_w, need_b, dres):
+def _ln_bwd(dy, x, w, b, mean, rstd, need_w, need_b, dres, drop=None):
     """LayerNorm backward; dgamma/dbeta of parameters bound to the flat grad buffer are
     accumulated in place by the reduce kernel (autograd then gets None for them, and the
-    params' post-accumulate hooks still fire)."""
+    params' post-accumulate hooks still fire).  ``drop = (p, seed, offset)``: also returns the
+    dropout backward of dx (4th value) -- from the same kernel pass where the block kernels
+    serve the width, else by a separate dropout pass."""
+    dkw = {}
+    if drop is not None and drop[0] > 0.0:
+        dkw = dict(dropout_p=drop[0], seed=drop[1], offset=drop[2])
     if need_w and need_b and _fusable(w) and _fusable(b):
-        dx, _, _ = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres, w.grad, b.grad)
-        return dx, None, None
-    dx, dw, db = ext().layernorm_bwd(dy, x, w, mean, rstd, need_w, need_b, dres)
-    return dx, (dw if need_w else None), (db if need_b else None)
+        out = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres, w.grad, b.grad, None, 0.0, **dkw)
+        dx, dw, db = out[0], None, None
+    else:
+        out = ext().layernorm_bwd(dy, x, w, mean, rstd, need_w, need_b, dres, None, None, None, 0.0, **dkw)
+        dx, dw, db = out[0], (out[1] if need_w else None), (out[2] if need_b else None)
+    if drop is None:
+        return dx, dw, db
+    if len(out) > 3:
+        return dx, dw, db, out[3]
+    p, seed, off = drop
+    return dx, dw, db, (ext().dropout_bwd(dx, p, seed, off) if p > 0.0 else dx)
 
 
 class _FusedLayerNorm(torch.autograd.Function):
@@ -94,9 +106,9 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         need_w = ctx.has_w and ctx.needs_input_grad[2]
         need_b = ctx.has_b and ctx.needs_input_grad[3]
         dres = ds.contiguous() if ds is not None else None
-        dx, dw, db = _ln_bwd(dy.contiguous(), s, w, ctx.bias, mean, rstd, need_w, need_b, dres)
-        p, seed, off = ctx.drop
-        dxin = ext().dropout_bwd(dx, p, seed, off) if p > 0.0 else dx
+        # the x branch's dropout backward comes out of the LN backward kernel itself (one pass
+        # writing dx and dx * keep / (1 - p)) instead of a separate read of dx
+        dx, dw, db, dxin = _ln_bwd(dy.contiguous(), s, w, ctx.bias, mean, rstd, need_w, need_b, dres, drop=ctx.drop)
         return dxin, dx, dw, db, None, None
 
 

@@ -289,6 +289,52 @@ TRACE_TP_OVERLAP = os.environ.get("SMP_TRACE_TP_OVERLAP", "0") == "1"
 TP_OVERLAP_TRACE = []
 
 
+# Token-chunked TP all-reduce overlap (reference row-parallel forward
+# all-reduce `torch/nn/transformer.py:1515-1522`, column-parallel backward `:1134-1141`): under
+# scaled-batch TP a row-parallel output is [B s, h] with a large B, so its GEMM is split into
+# token chunks and chunk i's all-reduce runs on RCCL's stream while chunk i + 1's GEMM runs; the
+# column-parallel input gradient likewise (each chunk's all-reduce starts right after its dX
+# GEMM, the weight gradient follows, then the waits).  SMP_TP_AR_CHUNKS: chunk count (default:
+# 4 from 16384 tokens, 2 from 4096, else 1 = one all-reduce).
+_TP_AR_CHUNKS = os.environ.get("SMP_TP_AR_CHUNKS", "auto")
+
+
+def tp_ar_chunks(tokens):
+    if _TP_AR_CHUNKS != "auto":
+        return max(1, int(_TP_AR_CHUNKS))
+    return 4 if tokens >= 16384 else (2 if tokens >= 4096 else 1)
+
+
+def _chunk_bounds(T, n):
+    step = -(-T // n)
+    step = -(-step // 16) * 16  # 16-row aligned chunks
+    return [(a, min(T, a + step)) for a in range(0, T, step)]
+
+
+def _chunked_fwd_allreduce(x, weight, bias, chunks, fwd_ar):
+    """out = all-reduce(x W^T + b) with the GEMM and the all-reduce overlapped per token chunk."""
+    x2 = x.reshape(-1, x.shape[-1])
+    T = x2.shape[0]
+    out = torch.empty(T, weight.shape[0], dtype=x.dtype, device=x.device)
+    works = []
+    wt = weight.t()
+    for a, b in _chunk_bounds(T, chunks):
+        if bias is not None:
+            torch.addmm(bias, x2[a:b], wt, out=out[a:b])
+        else:
+            torch.mm(x2[a:b], wt, out=out[a:b])
+        works.append(fwd_ar(out[a:b]))
+        if TRACE_TP_OVERLAP:
+            TP_OVERLAP_TRACE.append("fwd_chunk")
+    from ..parallel.comm_timer import timer as _comm_timer
+
+    with _comm_timer.region("tp", x.device):
+        for w in works:
+            if w is not None:
+                w.wait()
+    return out.view(*x.shape[:-1], weight.shape[0])
+
+
 class _LinearWGradAccum(torch.autograd.Function):
     """y = x W^T + b with (a) the weight gradient accumulated by a GEMM straight into the
     flat gradient buffer, (b) the bias gradient -- of ``b`` or of ``dbias_of``, a bias that a
@@ -299,13 +345,24 @@ class _LinearWGradAccum(torch.autograd.Function):
     the weight-gradient GEMM, so the two overlap."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, dx_allreduce=None, dbias_of=None):
+    def forward(ctx, x, weight, bias, dx_allreduce=None, dbias_of=None, fwd_ar=None):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias = bias
         ctx.dbias_of = dbias_of
         ctx.dx_allreduce = dx_allreduce
         ctx.wt = _transposed(weight) if _use_transposed(weight) else None
+        if fwd_ar is not None:
+            # row-parallel layer: the output leaves already all-reduced over TP (the all-reduce
+            # has an identity backward, so the backward below is unchanged)
+            n = tp_ar_chunks(x.numel() // x.shape[-1])
+            if n > 1:
+                return _chunked_fwd_allreduce(x, weight, bias, n, fwd_ar)
+            out = F.linear(x, weight, bias)
+            w = fwd_ar(out)
+            if w is not None:
+                w.wait()
+            return out
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -313,14 +370,31 @@ class _LinearWGradAccum(torch.autograd.Function):
         x, w = ctx.saved_tensors
         dx = dw = None
         grads = {2: None, 4: None}  # input index -> gradient returned to autograd
-        work = None
         dy2 = dy.reshape(-1, dy.shape[-1])
+        works = []
         if ctx.needs_input_grad[0]:
-            dx = F.linear(dy, ctx.wt) if ctx.wt is not None else torch.matmul(dy, w)
-            if ctx.dx_allreduce is not None:
-                work = ctx.dx_allreduce(dx)  # fresh tensor: reduced in place, async when large
-                if TRACE_TP_OVERLAP:
-                    TP_OVERLAP_TRACE.append("dx_allreduce_start")
+            n = tp_ar_chunks(dy2.shape[0]) if ctx.dx_allreduce is not None else 1
+            if n > 1:
+                # column-parallel dX in token chunks: each chunk's all-reduce starts right after
+                # its GEMM (a fresh tensor, reduced in place), overlapping the next chunk's GEMM
+                # and then the weight gradient
+                wm = ctx.wt.t() if ctx.wt is not None else w
+                dx2 = torch.empty(dy2.shape[0], wm.shape[1], dtype=dy.dtype, device=dy.device)
+                for a, b in _chunk_bounds(dy2.shape[0], n):
+                    if ctx.wt is not None:
+                        torch.mm(dy2[a:b], ctx.wt.t(), out=dx2[a:b])
+                    else:
+                        torch.mm(dy2[a:b], w, out=dx2[a:b])
+                    works.append(ctx.dx_allreduce(dx2[a:b]))
+                    if TRACE_TP_OVERLAP:
+                        TP_OVERLAP_TRACE.append("dx_allreduce_start")
+                dx = dx2.view(*dy.shape[:-1], wm.shape[1])
+            else:
+                dx = F.linear(dy, ctx.wt) if ctx.wt is not None else torch.matmul(dy, w)
+                if ctx.dx_allreduce is not None:
+                    works.append(ctx.dx_allreduce(dx))  # fresh tensor: reduced in place, async when large
+                    if TRACE_TP_OVERLAP:
+                        TP_OVERLAP_TRACE.append("dx_allreduce_start")
         # the bias whose gradient is colsum(dY): this layer's own, or the downstream one
         bidx = 2 if (ctx.has_bias and ctx.needs_input_grad[2]) else (
             4 if (ctx.dbias_of is not None and ctx.needs_input_grad[4]) else None)
@@ -350,27 +424,40 @@ class _LinearWGradAccum(torch.autograd.Function):
                     btarget = _col_sum(dy2)
             if btarget is not bparam.grad:
                 grads[bidx] = btarget.to(bparam.dtype)
-        if work is not None:
+        if any(wk is not None for wk in works):
             from ..parallel.comm_timer import timer as _comm_timer
 
             with _comm_timer.region("tp", dy.device):
-                work.wait()
-            if TRACE_TP_OVERLAP:
-                TP_OVERLAP_TRACE.append("dx_allreduce_wait")
-        return dx, dw, grads[2], None, grads[4]
+                for wk in works:
+                    if wk is not None:
+                        wk.wait()
+        if works and TRACE_TP_OVERLAP:
+            TP_OVERLAP_TRACE.append("dx_allreduce_wait")
+        return dx, dw, grads[2], None, grads[4], None
 
 
-def linear(x, weight, bias=None, dx_allreduce=None, dbias_of=None):
+def linear(x, weight, bias=None, dx_allreduce=None, dbias_of=None, fwd_ar=None):
     """F.linear with GEMM-fused weight-gradient accumulation into the flat grad buffer.
     ``dx_allreduce(dx) -> work | None``: the column-parallel layer's input-gradient
     all-reduce, overlapped with the weight-gradient GEMM (the caller then applies no
     separate backward all-reduce to x).  ``dbias_of``: a bias added to this layer's output
     by a fused activation that leaves its gradient to this layer (``bias_gelu(...,
     bias_grad=False)``): its gradient, the token sum of dY, is returned here -- from the
-    weight-gradient kernel's own pass over dY when that kernel runs."""
-    if torch.is_grad_enabled() and (dbias_of is not None or dx_allreduce is not None) and (
+    weight-gradient kernel's own pass over dY when that kernel runs.  ``fwd_ar(out) -> work |
+    None``: the row-parallel layer's forward all-reduce, applied here in token chunks
+    overlapped with the GEMM (the output is returned reduced)."""
+    if torch.is_grad_enabled() and (dbias_of is not None or dx_allreduce is not None or fwd_ar is not None) and (
             weight.requires_grad or x.requires_grad or (dbias_of is not None and dbias_of.requires_grad)):
-        return _LinearWGradAccum.apply(x, weight, bias, dx_allreduce, dbias_of)
+        return _LinearWGradAccum.apply(x, weight, bias, dx_allreduce, dbias_of, fwd_ar)
     if torch.is_grad_enabled() and weight.requires_grad and _fusable(weight):
-        return _LinearWGradAccum.apply(x, weight, bias, None, None)
+        return _LinearWGradAccum.apply(x, weight, bias, None, None, None)
+    if fwd_ar is not None:  # no gradient needed: the chunked, reduced output alone
+        n = tp_ar_chunks(x.numel() // x.shape[-1])
+        if n > 1:
+            return _chunked_fwd_allreduce(x, weight, bias, n, fwd_ar)
+        out = F.linear(x, weight, bias)
+        w = fwd_ar(out)
+        if w is not None:
+            w.wait()
+        return out
     return F.linear(x, weight, bias)

@@ -23,6 +23,8 @@ step long enough to amortise launch latency while leaving >10 buckets of overlap
 """
 import weakref
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -30,6 +32,19 @@ from ..backend.logger import get_logger
 from .comm_timer import timer as comm_timer
 
 logger = get_logger()
+
+
+
+def probe_premul_sum(group, dtype, device, group_size):
+    """Whether RCCL's pre-multiplied sum gives the right average for this dtype on this group:
+    one 8-element all-reduce, the same on every rank (so every rank reaches the same verdict),
+    once per reducer.  (On the ROCm 7 / RCCL 2.26 stack a single-rank bf16 premul-sum returned
+    zeros -- tests/test_runtime_gpu.py -- so the reducer must not trust the op blindly: when the
+    probe fails it keeps the separate scaling pass.)"""
+    probe = torch.ones(8, dtype=dtype, device=device)
+    dist.all_reduce(probe, op=dist._make_nccl_premul_sum(0.5), group=group)
+    want = torch.full((8,), 0.5 * group_size, dtype=torch.float32, device=device)
+    return bool(torch.allclose(probe.float(), want, rtol=1e-2, atol=0.0))
 
 
 class BucketReducer:
@@ -115,9 +130,17 @@ class BucketReducer:
         self.launched_before_sync += 0 if self._in_sync else 1
         buf = self.flat.grad[b.start : b.end]
         scale = 1.0 / (self.divisor * (self.active_size or self.group_size))
+        op = dist.ReduceOp.SUM
+        collective = self.group is not None and self.group_size > 1
         if scale != 1.0:
-            buf.mul_(scale)
-        if self.group is None or self.group_size == 1:
+            if collective and self.comm_hook is None and self._premul_ok():
+                # RCCL pre-multiplied sum: the average's scale is applied inside the reduction
+                # kernel, not by a separate pass over every gradient byte (reference
+                # `ddp_model.py:605-632` divides after)
+                op = dist._make_nccl_premul_sum(scale)
+            else:
+                buf.mul_(scale)
+        if not collective:
             b.work = None
             return
         if self.comm_hook is not None:
@@ -126,9 +149,19 @@ class BucketReducer:
         if self.shard:
             n = b.numel // self.group_size
             out = buf[self.group_rank * n : (self.group_rank + 1) * n]
-            b.work = dist.reduce_scatter_tensor(out, buf, group=self.group, async_op=True)
+            b.work = dist.reduce_scatter_tensor(out, buf, op=op, group=self.group, async_op=True)
         else:
-            b.work = dist.all_reduce(buf, group=self.group, async_op=True)
+            b.work = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+
+    def _premul_ok(self):
+        ok = getattr(self, "_premul", None)
+        if ok is None:
+            ok = (hasattr(dist, "_make_nccl_premul_sum") and self.flat.grad.is_cuda
+                  and dist.get_backend(self.group) == "nccl" and os.environ.get("SMP_DDP_PREMUL_SUM", "1") != "0"
+                  and probe_premul_sum(self.group, self.flat.grad.dtype, self.flat.grad.device, self.group_size))
+            self._premul = ok
+        return ok
+
 
     # ------------------------------------------------------------------ step
     def prepare_for_backward(self):

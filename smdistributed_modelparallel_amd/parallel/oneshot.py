@@ -46,6 +46,8 @@ _MAX_RANKS = 4  # one-shot reads every peer's slot: cost grows with the group
 _TIMEOUT_S = float(os.environ.get("SMP_ONESHOT_ALLREDUCE_TIMEOUT_S", "600"))
 _DTYPES = (torch.bfloat16, torch.float16, torch.float32)
 
+_TRACE = os.environ.get("SMP_ONESHOT_TRACE", "0") == "1"  # log every one-shot call (order triage)
+_ncalls = [0]
 _instances = {}  # group key -> IpcAllReduce or None (disabled)
 _failed = set()  # group keys whose instance reported a failure
 
@@ -165,6 +167,14 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None, async_op=False):
                 raise OneShotAllReduceError("one-shot all-reduce: this TP group failed earlier (a peer timed out "
                                             "or aborted); its results can no longer be trusted")
             code = 0 if op == dist.ReduceOp.SUM else 1
+            if _TRACE:
+                import sys
+                import traceback
+
+                _ncalls[0] += 1
+                fr = [f"{f.filename.rsplit('/', 1)[-1]}:{f.lineno}" for f in traceback.extract_stack(limit=6)[:-1]]
+                print(f"[oneshot r{dist.get_rank()}] #{_ncalls[0]} n={x.numel()} {x.dtype} op={code} "
+                      f"{' < '.join(reversed(fr))}", file=sys.stderr, flush=True)
             if x.data_ptr() % 16 == 0:
                 inst.all_reduce(x, x, code, _TIMEOUT_S)
             else:  # a view at an odd offset: reduce an aligned copy

@@ -364,13 +364,20 @@ class PipelineEngine:
 
     # ------------------------------------------------------- record / replay
     def replay_enabled(self):
-        """Record-and-replay runs for pipelines whose order must be deterministic (TP > 1)
-        or when static_mode asks for it; SMP_REPLAY=0 keeps the dynamic (recording-free)
-        scheduler."""
+        """Record-and-replay is the default for every pipeline with repeated steps (SURVEY
+        §7.1.6).  It is FORCED -- ``SMP_REPLAY=0`` does not turn it off -- where the reference
+        forces its DeterministicServerQueue (`torch/server.py:57-65`): TP > 1 (collective
+        order), ``static_mode``, ``fast_mode`` and ``offload_activations`` (the task-level
+        activation prefetch needs the frozen order).  ``SMP_REPLAY=0`` keeps the dynamic
+        scheduler for the other pipelines; SMP_NONDETERMINISTIC_TP_ORDER=1 (tests) disables
+        both."""
         core = self.core
-        if os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") == "1" or os.environ.get("SMP_REPLAY", "1") == "0":
+        if core.pp_size() <= 1 or os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") == "1":
             return False
-        return core.pp_size() > 1 and (core.tp_size() > 1 or bool(self.state.cfg.static_mode))
+        cfg = self.state.cfg
+        forced = (core.tp_size() > 1 or bool(cfg.static_mode) or bool(cfg.fast_mode)
+                  or bool(cfg.offload_activations))
+        return forced or os.environ.get("SMP_REPLAY", "1") != "0"
 
     def after_step(self, step_fn, seconds):
         """Called on every rank after every pipelined step (symmetric collectives)."""

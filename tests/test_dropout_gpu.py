@@ -87,3 +87,26 @@ def test_dropout_replays_under_activation_checkpointing():
     y2 = checkpoint(f, x, use_reentrant=False)
     (gx2,) = torch.autograd.grad(y2, x, g)
     assert torch.equal(y1, y2) and torch.equal(gx1, gx2)
+
+
+@pytest.mark.parametrize("h", [1024, 1600, 4096])
+def test_ln_bwd_fused_dropout_output_bitwise(h):
+    """The LN backward's fused dropout output (dx * keep / (1 - p), written beside dx by the
+    block kernels) is bitwise what the separate dropout_bwd pass over dx gives."""
+    from smdistributed_modelparallel_amd.ops._ext import ext
+
+    torch.manual_seed(2)
+    rows = 777
+    x = torch.randn(rows, h, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(h, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(h, device="cuda", dtype=torch.bfloat16)
+    _, mean, rstd = ext().layernorm_fwd(x, None, w, b, 1e-5)
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x)
+    out = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres, None, None, None, 0.0,
+                              dropout_p=0.1, seed=1234, offset=8)
+    assert len(out) == 4, "block kernels must serve this width"
+    ref = ext().dropout_bwd(out[0], 0.1, 1234, 8)
+    assert torch.equal(out[3], ref)
+    plain = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres)
+    assert torch.equal(out[0], plain[0]) and torch.equal(out[1], plain[1]) and torch.equal(out[2], plain[2])

@@ -14,6 +14,17 @@ def _tol(dt):
     return {torch.float32: 2e-5, torch.float16: 2e-3, torch.bfloat16: 2e-2}[dt]
 
 
+# relative-norm bound for reductions over rows (parameter gradients): ||out - ref|| / ||ref||.
+# An absolute element tolerance scaled for the largest sums let a reduction that drops a tile
+# pass; a dropped 1/37 of the rows moves the norm by ~3 %.
+_REL = {torch.float32: 1e-5, torch.float16: 2e-3, torch.bfloat16: 1e-2}
+
+
+def _rel(out, ref):
+    out, ref = out.double(), ref.double()
+    return ((out - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+
+
 @pytest.fixture(scope="module")
 def C():
     from smdistributed_modelparallel_amd.ops._ext import ext
@@ -39,8 +50,8 @@ def test_layernorm_fwd_bwd(C, dt, cols):
     y.backward(g.to(dt))
     yr.backward(g)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 4, rtol=tol * 4)
-    assert torch.allclose(w.grad.float(), wr.grad, atol=tol * 40, rtol=tol * 4)
-    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 40, rtol=tol * 4)
+    assert _rel(w.grad, wr.grad) < _REL[dt], _rel(w.grad, wr.grad)
+    assert _rel(b.grad, br.grad) < _REL[dt], _rel(b.grad, br.grad)
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
@@ -88,7 +99,7 @@ def test_bias_gelu(C, dt, rows, cols, exact):
     y.backward(g.to(dt))
     yr.backward(g)
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
-    assert torch.allclose(b.grad.float(), br.grad, atol=tol * 50 * max(1, rows // 200) ** 0.5, rtol=tol * 4)
+    assert _rel(b.grad, br.grad) < _REL[dt], _rel(b.grad, br.grad)
 
 
 @pytest.mark.parametrize("dt", DT)

@@ -57,6 +57,15 @@ def test_tp2_dx_allreduce_overlaps_weight_gradient():
     _run(2, 1, 2, 1, extra={"check_tp_overlap": True}, env={"SMP_TRACE_TP_OVERLAP": "1"})
 
 
+@pytest.mark.parametrize("world,tp", [(2, 2), (4, 4)])
+def test_tp_chunked_allreduce_overlap(world, tp):
+    """Token-chunked TP all-reduces: row-parallel outputs all-reduced per chunk
+    beside the next chunk's GEMM, column-parallel dX all-reduced per chunk ahead of the weight
+    gradient -- results still match the unpartitioned model at TP2 and TP4."""
+    _run(world, 1, tp, 1, extra={"check_tp_overlap": True, "expect_tp_chunks": 2},
+         env={"SMP_TRACE_TP_OVERLAP": "1", "SMP_TP_AR_CHUNKS": "3"})
+
+
 def test_tp2_uneven_heads():
     _run(2, 1, 2, 2, extra={"model": {"num_attention_heads": 3, "attention_head_size": 16, "hidden_size": 48,
                                       "intermediate_size": 96}})
@@ -213,6 +222,22 @@ def test_pp2_offload_task_level_prefetch_under_replay():
                                      "cfg": {"static_mode": True, "offload_activations": True,
                                              "task_level_activation_loading_horizon": 3}},
          env={"SMP_REPLAY_RECORD_STEPS": "2"})
+
+
+def test_pp2_offload_alone_forces_replay_and_task_prefetch():
+    """offload_activations alone (no static_mode, SMP_REPLAY=0 asked) engages the deterministic
+    record-and-replay order, as the reference's server does for offloading
+    (`torch/server.py:57-65`), and the task-level prefetch loads activations ahead."""
+    _run(2, 2, 1, 3, steps=4, extra={"ckpt_layers": True, "expect_replay": True, "expect_task_prefetch": True,
+                                     "cfg": {"offload_activations": True,
+                                             "task_level_activation_loading_horizon": 3}},
+         env={"SMP_REPLAY_RECORD_STEPS": "2", "SMP_REPLAY": "0"})
+
+
+def test_pp2_default_replays_repeated_steps():
+    """A plain pipeline (no TP, no static / fast mode, no offload) records and replays by
+    default; results still match the unpartitioned model."""
+    _run(2, 2, 1, 3, steps=4, extra={"expect_replay": True}, env={"SMP_REPLAY_RECORD_STEPS": "2"})
 
 
 def test_sharded_dp_fp16_overflow_skips_on_every_rank():

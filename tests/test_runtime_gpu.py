@@ -125,3 +125,29 @@ def test_all_ones_decision_mixed_devices():
     _decide_all_ones((mask, labels), {"position_ids": pos})
     assert mask._smp_all_ones[1] is True and labels._smp_all_ones[1] is True
     assert pos._smp_all_ones[1] is False
+
+
+def test_rccl_premul_sum_probe_single_rank(tmp_path):
+    """The DDP reducer averages inside RCCL (pre-multiplied sum) only for dtypes whose one-time
+    probe gives the right answer on the group; otherwise it keeps the scaling pass.  On a
+    single-rank nccl group: the probe's verdict must match an explicit check of the op."""
+    script = tmp_path / "premul.py"
+    script.write_text(
+        "import torch, torch.distributed as dist\n"
+        "from smdistributed_modelparallel_amd.parallel.ddp import probe_premul_sum\n"
+        "dist.init_process_group('nccl', rank=0, world_size=1)\n"
+        "for dt in (torch.float32, torch.bfloat16):\n"
+        "    x = torch.arange(64, dtype=dt, device='cuda')\n"
+        "    dist.all_reduce(x, op=dist._make_nccl_premul_sum(0.25))\n"
+        "    right = torch.equal(x, torch.arange(64, dtype=dt, device='cuda') * 0.25)\n"
+        "    verdict = probe_premul_sum(None, dt, torch.device('cuda'), 1)\n"
+        "    print(f'{dt} premul_right={right} probe={verdict}')\n"
+        "    assert verdict == right, (dt, verdict, right)\n"
+        "dist.destroy_process_group()\n"
+        "print('OK')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 2000),
+               PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120, cwd=root)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+    print(r.stdout)

@@ -31,10 +31,18 @@ def main():
     else:  # a BASELINE architecture at full width, few layers, small vocabulary
         kw = dict(num_layers=2, vocab_size=1024, num_positions=64)
     kw.update(extra.get("model", {}))
+    # reduced precision (tests/test_hybrid_gpu.py): the smp model in bf16 / fp16 with fp32 master
+    # weights against the SAME architecture run in that dtype without smp
+    low = extra.get("dtype")
+    ldt = {"bf16": torch.bfloat16, "fp16": torch.float16}.get(low)
+    if low:
+        cfg[low] = True
     ref = build_gpt(base, dropout=0.0, **kw)  # built before init: unsharded reference
     smp.init(cfg)
     dev = smp.state.device  # GPU runs (tests/test_hybrid_gpu.py): every rank on the box's one GPU
     ref.to(dev)
+    if ldt is not None:
+        ref.to(ldt)
     delayed = bool(extra.get("delayed"))
     with smp.delay_param_initialization(enabled=delayed):
         with smp.model_creation(tensor_parallelism=tp > 1):
@@ -82,8 +90,16 @@ def main():
         for layer in model.get_module().transformer.seq_layers:
             smp.set_activation_checkpointing(layer)
     lr = 0.05
-    opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=lr))
+    if low == "fp16":
+        # dynamic loss scaling (reference test_gpt_grad.py:121-154 fp16 variants)
+        opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=lr), dynamic_loss_scale=True,
+                                       dynamic_loss_args={"init_scale": 2.0 ** 12, "scale_window": 1000})
+    else:
+        opt = smp.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=lr))
     ropt = torch.optim.SGD(ref.parameters(), lr=lr)
+    from smdistributed_modelparallel_amd.ops.attention import FLASH_CALLS
+
+    flash0 = dict(FLASH_CALLS)
 
     @smp.step
     def train(model, ids, labels):
@@ -189,12 +205,28 @@ def main():
         from smdistributed_modelparallel_amd.ops import linear as lin
 
         tr = lin.TP_OVERLAP_TRACE
-        starts = [i for i, e in enumerate(tr) if e == "dx_allreduce_start"]
+        # last start of each run of consecutive starts (token-chunked dX: one start per chunk)
+        starts = [i for i, e in enumerate(tr) if e == "dx_allreduce_start" and (i + 1 == len(tr) or
+                                                                               tr[i + 1] != "dx_allreduce_start")]
         assert starts, tr[:20]
         for i in starts:
-            # the weight gradient runs while the dX all-reduce is in flight, then the wait
+            # the weight gradient runs while the dX all-reduce(s) are in flight, then the wait
             assert tr[i + 1:i + 3] == ["wgrad", "dx_allreduce_wait"], (i, tr[i:i + 3])
+        chunks = int(extra.get("expect_tp_chunks", 0))
+        if chunks:
+            runs = [i for i, e in enumerate(tr) if e == "dx_allreduce_start" and (i == 0 or tr[i - 1] != e)]
+            longest = 0
+            for i in runs:
+                j = i
+                while j < len(tr) and tr[j] == "dx_allreduce_start":
+                    j += 1
+                longest = max(longest, j - i)
+            assert longest >= chunks and tr.count("fwd_chunk") >= chunks, (longest, tr.count("fwd_chunk"))
         print(f"rank {smp.rank()} tp overlap: {len(starts)} dX all-reduces overlapped with wgrad", flush=True)
+    if extra.get("expect_flash"):
+        ran = FLASH_CALLS["plain"] + FLASH_CALLS["key_bias"] - flash0["plain"] - flash0["key_bias"]
+        assert ran > 0, ("the flash kernels did not run", FLASH_CALLS)
+        print(f"rank {smp.rank()} flash launches {ran}", flush=True)
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
 
