@@ -41,10 +41,9 @@ namespace smpk {
 namespace attn {
 namespace fused {
 
-#ifndef SMPK_FUSED_WAVES
-#define SMPK_FUSED_WAVES 8
-#endif
-constexpr int kWaves = SMPK_FUSED_WAVES;  // waves per workgroup (8: one workgroup per CU, 4: two)
+// waves per workgroup: 8 = one workgroup per CU.  (4 waves / two workgroups per CU doubles the
+// hand-off traffic and spilled with dropout: profiles/r5/attention_fused_bwd.md)
+constexpr int kWaves = 8;
 constexpr int kNT = 64 * kWaves;          // threads per workgroup
 constexpr int kKeys = 32 * kWaves;        // keys per workgroup (32 per wave, key on the lane)
 constexpr int kQI = 8 / kWaves;           // 16-query dQ row blocks per wave (x 2 d blocks)

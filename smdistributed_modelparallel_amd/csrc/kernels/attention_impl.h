@@ -69,25 +69,6 @@ struct MF<f16> {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
-// Compile-time A/B switches (tools/build_kvariant.sh builds a variant .so; defaults = shipped):
-//   SMPK_ATTN_PAIRS     element-wise softmax / dS code of dQ and dK/dV on f32x2 register pairs
-//                       (packed fp32 FMAs) instead of scalar code
-//   SMPK_ATTN_FWD_PAIRS the same for the forward's exponent arguments and row sums
-//   SMPK_ATTN_VPRE      forward D = 64: the tile's V fragments read before the softmax
-//   SMPK_ATTN_FWD_WAVES forward D <= 128: waves-per-SIMD floor given to the register allocator
-//                       (0 = none)
-#ifndef SMPK_ATTN_PAIRS
-#define SMPK_ATTN_PAIRS 1
-#endif
-#ifndef SMPK_ATTN_FWD_PAIRS
-#define SMPK_ATTN_FWD_PAIRS 0
-#endif
-#ifndef SMPK_ATTN_VPRE
-#define SMPK_ATTN_VPRE 0
-#endif
-#ifndef SMPK_ATTN_FWD_WAVES
-#define SMPK_ATTN_FWD_WAVES 0
-#endif
 constexpr int kThreads = 256;
 
 // LDS row stride (elements) for head dim D
@@ -519,9 +500,6 @@ struct QInLds {
 // selects executed on every tile -- profiles/r4/attention_isa.md.)
 template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
 __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
-#if SMPK_ATTN_FWD_WAVES
-    __attribute__((amdgpu_waves_per_eu(D >= 256 ? 1 : SMPK_ATTN_FWD_WAVES)))
-#endif
     attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr bool QLDS = QInLds<D>::v;
@@ -681,16 +659,6 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
       if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
         p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
     }
-    constexpr bool VPRE = SMPK_ATTN_VPRE && D == 64 && !BIAS;
-    typename MF<T>::e8 vfr[VPRE ? D / 32 : 1][4];
-    if constexpr (VPRE) {
-#pragma unroll
-      for (int i = 0; i < D / 32; ++i) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) vfr[i][s] = ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
     if (BIAS && tile_bias) {
       add_from_keys(s0, sB, hh);
       add_from_keys(s1, sB + 32, hh);
@@ -725,27 +693,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
       m_i = m_new;
       m_use = mu;
     }
-    // p = exp2(S sl2 - m): exponent arguments two at a time (v_pk_fma_f32), packed row sums
-#if SMPK_ATTN_FWD_PAIRS
-    const f32x2 sl2v = {sl2, sl2}, nm = {-m_use, -m_use};
-    f32x2 rs0 = {0.f, 0.f}, rs1 = {0.f, 0.f};
-#pragma unroll
-    for (int reg = 0; reg < 16; reg += 2) {
-      f32x2 a0 = {s0[reg], s0[reg + 1]}, a1 = {s1[reg], s1[reg + 1]};
-      a0 = __builtin_elementwise_fma(a0, sl2v, nm);
-      a1 = __builtin_elementwise_fma(a1, sl2v, nm);
-      a0 = f32x2{fast_exp2(a0.x), fast_exp2(a0.y)};
-      a1 = f32x2{fast_exp2(a1.x), fast_exp2(a1.y)};
-      s0[reg] = a0.x;
-      s0[reg + 1] = a0.y;
-      s1[reg] = a1.x;
-      s1[reg + 1] = a1.y;
-      rs0 += a0;
-      rs1 += a1;
-    }
-    rs0 += rs1;
-    l_i += rs0.x + rs0.y;
-#else
+    // p = exp2(S sl2 - m), scalar (the packed-pair form measured slower here: profiles/r4/attention_r4c.md)
     float rs0 = 0.f, rs1 = 0.f;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -757,7 +705,6 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
       rs1 += e1;
     }
     l_i += rs0 + rs1;
-#endif
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
       pf[0] = drop_packed(pf[0], f0[0], f0[1]);
@@ -769,10 +716,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
     for (int i = 0; i < D / 32; ++i) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        if constexpr (VPRE)
-          o[i] = MF<T>::mma(vfr[i][s], pf[s], o[i]);
-        else
-          o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
+        o[i] = MF<T>::mma(ld_tr<T>(sV, tro.lo[i] + 16 * s * DS, tro.hi[i] + 16 * s * DS), pf[s], o[i]);
       }
     }
   };
@@ -1004,7 +948,6 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
 #pragma unroll
       for (int g = 0; g < 4; ++g) kw[g] = *reinterpret_cast<const uint4*>(&sBits[bits_row + 32 * sub + 8 * g + 4 * hh]);
     }
-#if SMPK_ATTN_PAIRS
     // element-wise on register pairs (2j, 2j + 1): packed fp32 multiplies / FMAs
     f32x2 po[8], dso[8];
     const f32x2 sl2v = {sl2, sl2};
@@ -1038,29 +981,6 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dkdv_kerne
     // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
     typename MF<T>::e8 pf0 = pack8p<T>(po, 0), pf1 = pack8p<T>(po, 1);
     typename MF<T>::e8 sf0 = pack8p<T>(dso, 0), sf1 = pack8p<T>(dso, 1);
-#else
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      float pv = fast_exp2(s[reg] * sl2);
-      if constexpr (MASK) {
-        const int qq = qs + acc_row(reg, hh);
-        if (qq >= sq || krow >= sk || (CAUSAL && krow > qq + diag) || (win > 0 && krow <= qq + diag - win)) pv = 0.f;
-      }
-      if (DROP) {
-        const uint4 w4 = kw[reg >> 2];
-        const uint32_t w = (reg & 3) == 0 ? w4.x : (reg & 3) == 1 ? w4.y : (reg & 3) == 2 ? w4.z : w4.w;
-        const float z = __builtin_bit_cast(float, bit_mask(w, kbit) & rsd_bits);  // keep / (1 - p) or 0
-        s[reg] = pv * z;                             // (P o Z) for dV
-        dp[reg] = pv * fmaf(dp[reg], z, ndl[reg]);  // P o (Z o dP - delta)
-      } else {
-        s[reg] = pv;
-        dp[reg] *= pv;
-      }
-    }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (B operands = accumulators, A via transposed reads)
-    typename MF<T>::e8 pf0 = pack8<T>(s, 0), pf1 = pack8<T>(s, 1);
-    typename MF<T>::e8 sf0 = pack8<T>(dp, 0), sf1 = pack8<T>(dp, 1);
-#endif
 #pragma unroll
     for (int i = 0; i < DO / 32; ++i) {
       const int a0 = 32 * sub * DS, a1 = (32 * sub + 16) * DS;
@@ -1293,7 +1213,7 @@ __global__ void __launch_bounds__(kThreads, D == 64 ? 2 : 1) attn_bwd_dq_kernel(
       // lane per tile) -- with dropout element-wise on register pairs (packed fp32 FMAs /
       // multiplies: dQ -7 %); without it the scalar form measured 2 % faster
       // (profiles/r4/attention_r4c.md)
-      if constexpr (SMPK_ATTN_PAIRS && DROP) {
+      if constexpr (DROP) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int reg = 2 * j;

@@ -47,25 +47,14 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TM = 256;     // output tile rows (N)
 constexpr int TN = 256;     // output tile cols (K)
 constexpr int TK = 64;      // tokens per staged tile
-// stage geometry / wave priority: compile-time (tools/build_kvariant.sh builds A/B copies)
-#ifndef SMPK_WGRAD_TK
-#define SMPK_WGRAD_TK 64
-#endif
-#ifndef SMPK_WGRAD_NS
-#define SMPK_WGRAD_NS 2
-#endif
-#ifndef SMPK_WGRAD_PRIO
-#define SMPK_WGRAD_PRIO 0
-#endif
-// waves per workgroup: 8 (2 per SIMD, 128 x 64 wave blocks) or 4 (1 per SIMD, 128 x 128 wave
-// blocks -- a third less LDS read traffic per MFMA, accumulators past the 256 arch VGPRs)
-#ifndef SMPK_WGRAD_W
-#define SMPK_WGRAD_W 8
-#endif
-constexpr int kW = SMPK_WGRAD_W;
+// fallback kernel geometry: 8 waves (2 per SIMD, 128 x 64 wave blocks), 64-token LDS stages,
+// 2 stages.  (Round 4 A/B: 4 waves with 128 x 128 blocks was 10-14 % slower, 32-token / 3-stage
+// and a raised MFMA-wave priority lost too -- profiles/r4/attention_r4c.md,
+// profiles/r4/parallel_residual_fusion.md.)
+constexpr int kW = 8;
 constexpr int kWCOLS = 256 / (kW / 2);  // output columns per wave (2 wave rows of 128)
-constexpr int kTK = SMPK_WGRAD_TK;  // tokens per LDS stage of the kernel
-constexpr int kNS = SMPK_WGRAD_NS;  // LDS stages (2 x 64-token operand tiles + 16 KB column sums)
+constexpr int kTK = 64;  // tokens per LDS stage of the kernel
+constexpr int kNS = 2;   // LDS stages (2 x 64-token operand tiles + 16 KB column sums)
 constexpr int RW = 256;     // LDS row width (elements) of both staged tiles
 constexpr int CH = RW / 8;  // 16-B chunks per row
 
@@ -222,7 +211,6 @@ __device__ __forceinline__ void glds16_segment(const uint16_t* __restrict__ A, c
   const int n0 = tn * TM, k0 = tk * TN;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / (W / 2), wn = wave % (W / 2);
-  if (SMPK_WGRAD_PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half
   // transposed-read offsets for k-step 0: row 8 (l / 16) + q (+4), column block base + 4 p
   int aLo[NI], aHi[NI], bLo[NJ], bHi[NJ];
   {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B copy of the kernel extension: the given kernel TUs recompiled with extra hipcc
-# flags (e.g. -DSMPK_WGRAD_TK=32, -DSMPK_ATTN_PAIRS=0), linked with the in-tree objects of every
+# flags (e.g. -D macros an experiment adds), linked with the in-tree objects of every
 # other TU, written to abtest/_C_<tag>.so (abtest/ travels with gpurun; time it with
 # tools/kvariant_time.py or tools/attn_time.py <so>).  A TU's own in-tree flags
 # (_build._TU_FLAGS, e.g. the dQ TU's -fno-slp-vectorize) are kept.
