@@ -32,9 +32,8 @@
 // Fixed summation order everywhere: bitwise reproducible.
 //
 // Status (profiles/r5/attention_fused_bwd.md): correct and deterministic, but at the GPT-2 XL
-// shape still 4 % (no dropout) / 15 % (dropout) slower than the split kernels -- the write-
-// through partials come back from the memory-side cache, not L2 -- so it is opt-in
-// (SMP_ATTN_FUSED_BWD=1).
+// shape still 4 % (no dropout) / 15 % (dropout) slower than the split kernels -- the dQ partial
+// loads cost ~270 us per layer inside the tile schedule -- so it is opt-in (SMP_ATTN_FUSED_BWD=1).
 #include "attention_impl.h"
 
 namespace smpk {
@@ -290,8 +289,7 @@ __global__ void __launch_bounds__(kNT, 2) attn_bwd_fused_kernel(AttnBwdParams P)
     __syncthreads();
     // the predecessor (block kb + 1) adds into this tile before this block; the diagonal block
     // stores first.  When the flag read half a tile ago already shows the predecessor's partial,
-    // its loads go out now and have the whole tile to land (the partial was stored write-through
-    // and comes from memory-side cache, not L2); otherwise the flag is looked at again now and
+    // its loads go out now and have the whole tile to land; otherwise the flag is looked at again now and
     // awaited between the two sub-steps.
     const int kb_first = imin(nkb - 1, (q0 + kBQ - 1) / kKeys);
     const bool has_pred = kb < kb_first;
