@@ -443,21 +443,25 @@ def test_offloaded_checkpoint_gpu():
 
 
 @pytest.mark.parametrize("neox", [False, True])
-@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_rope_kernel(neox, dt):
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("d,rd", [(64, 32), (96, 24), (64, 10), (256, 64)])
+def test_rope_kernel(neox, dt, d, rd):
+    """HIP RoPE vs the torch formula, fwd (strided packed-QKV view, position offset) and bwd.
+    (d, rd) covers the 16-bit vector kernel with 16-byte chunks (64/32, GPT-J's 256/64), with
+    8-byte chunks (NeoX-20B's 96/24) and the scalar fallback (rd 10)."""
     from smdistributed_modelparallel_amd.ops.rope import apply_rotary, apply_rotary_torch
 
     torch.manual_seed(4)
-    qkv = torch.randn(2, 37, 3, 5, 64, device="cuda", dtype=dt)
+    qkv = torch.randn(2, 37, 3, 5, d, device="cuda", dtype=dt)
     q = qkv[:, :, 0]  # strided view into the packed QKV projection
     x = q.detach().clone().requires_grad_()
-    y = apply_rotary(q, 32, 10000, neox)
-    yr = apply_rotary_torch(q.float(), 32, 10000, neox)
+    y = apply_rotary(q, rd, 10000, neox)
+    yr = apply_rotary_torch(q.float(), rd, 10000, neox)
     tol = 1e-5 if dt == torch.float32 else 2e-2
     assert torch.allclose(y.float(), yr, atol=tol, rtol=tol)
-    y2 = apply_rotary(x, 32, 10000, neox, offset=3)
+    y2 = apply_rotary(x, rd, 10000, neox, offset=3)
     xr = x.detach().float().requires_grad_()
-    yr2 = apply_rotary_torch(xr, 32, 10000, neox, offset=3)
+    yr2 = apply_rotary_torch(xr, rd, 10000, neox, offset=3)
     assert torch.allclose(y2.float(), yr2, atol=tol, rtol=tol)
     g = torch.randn_like(yr2)
     y2.backward(g.to(dt))
