@@ -710,7 +710,7 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
 std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale, bool causal,
                                       int64_t window, c10::optional<at::Tensor> kbias,
                                       double dropout_p, int64_t seed,
-                                      int64_t offset) {
+                                      int64_t offset, bool store_bits) {
   auto p = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   auto o = at::empty({p.b, p.sq, p.h, p.d}, q.options());
   auto lse = at::empty({p.b, p.h, p.sq}, q.options().dtype(at::kFloat));
@@ -719,7 +719,7 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
   p.lse = lse.data_ptr<float>();
   // dropout: the keep bits for the backward (1 bit per score: b h sq sk / 8 bytes)
   at::Tensor bits;
-  if (p.drop_on) {
+  if (p.drop_on && store_bits) {
     bits = at::empty({p.b * p.h, (p.sk + 63) / 64, p.sq, 2}, q.options().dtype(at::kInt));
     p.drop_bits = reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>());
   } else {
@@ -727,6 +727,18 @@ std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, 
   }
   check(smpk::attention_fwd(dt_code(q), p, stream()), "attention_fwd");
   return {o, lse, bits};
+}
+
+// The keep bits a dropout forward with these arguments stores, regenerated from the hash (for a
+// forward called with store_bits = false).
+at::Tensor attention_keep_bits(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, int64_t window,
+                               double dropout_p, int64_t seed, int64_t offset) {
+  TORCH_CHECK(dropout_p > 0.0, "attention_keep_bits: dropout_p must be > 0");
+  auto p = attn_params(q, k, v, 1.0, causal, window, c10::nullopt, dropout_p, seed, offset);
+  auto bits = at::empty({p.b * p.h, (p.sk + 63) / 64, p.sq, 2}, q.options().dtype(at::kInt));
+  check(smpk::attention_keep_bits(p, reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>()), stream()),
+        "attention_keep_bits");
+  return bits;
 }
 
 // Writes into the provided dq/dk/dv (may be views of one packed gradient buffer).
@@ -841,7 +853,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("vocab_start"), py::arg("ignore_index"), py::arg("vocab") = -1);
   m.def("attention_fwd", &attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
-        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0);
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("store_bits") = true);
+  m.def("attention_keep_bits", &attention_keep_bits, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
+        py::arg("window"), py::arg("dropout_p"), py::arg("seed"), py::arg("offset"));
   m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),

@@ -201,6 +201,9 @@ struct AttnBwdParams {
 bool attention_bwd_fused_ok(const AttnBwdParams& p);
 int attention_bwd_fused_d64(int dt, const AttnBwdParams& p, hipStream_t s);
 int attention_fwd(int dt, const AttnParams& p, hipStream_t s);
+// the keep bits the dropout forward stores, regenerated from the hash into `bits`
+// ([b h, ceil(sk / 64), sq, 2] uint32) for a forward that stored none
+int attention_keep_bits(const AttnParams& p, uint32_t* bits, hipStream_t s);
 bool attention_head_dim_supported(int64_t d);
 int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);
 

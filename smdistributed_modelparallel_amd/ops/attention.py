@@ -142,6 +142,30 @@ FUSED_BWD_ERR = [None]
 FLASH_CALLS = {"plain": 0, "key_bias": 0}
 
 
+# Per-layer budget of stored dropout keep bits (b h ceil(sk / 64) sq 8 bytes).  Above it the
+# forward stores none and the backward regenerates them from the hash right before it runs
+# (ext().attention_keep_bits): transient memory for one layer instead of saved activations that
+# grow with sq * sk (GPT-2 XL b 32 s 2048 stores 419 MB per layer).
+KEEPBITS_MAX_BYTES = [int(float(os.environ.get("SMP_ATTN_KEEPBITS_MAX_MB", "1024")) * (1 << 20))]
+
+
+def _store_bits(q, k, dropout_p):
+    if dropout_p <= 0.0:
+        return True
+    b, sq, h = q.shape[0], q.shape[1], q.shape[2]
+    sk = k.shape[1]
+    return b * h * ((sk + 63) // 64) * sq * 8 <= KEEPBITS_MAX_BYTES[0]
+
+
+def _keep_bits(bits, q, k, v, causal, window, p, seed, off):
+    """The forward's keep bits, or (forward stored none) the same words regenerated now."""
+    if p <= 0.0:
+        return None
+    if bits.numel() == 0:
+        return ext().attention_keep_bits(q, k, v, causal, window, p, seed, off)
+    return bits
+
+
 def _count_flash(kb):
     FLASH_CALLS["key_bias" if kb is not None else "plain"] += 1
 
@@ -151,7 +175,8 @@ class _FlashAttention(torch.autograd.Function):
     def forward(ctx, q, k, v, scale, causal, window, kb, dropout_p):
         seed, off = dropout_seed_offset(q.device) if dropout_p > 0.0 else (0, 0)
         bias = kb.bias if kb is not None else None
-        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off,
+                                           _store_bits(q, k, dropout_p))
         ctx.save_for_backward(q, k, v, o, lse, bits)
         ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
@@ -165,8 +190,9 @@ class _FlashAttention(torch.autograd.Function):
         p, seed, off = ctx.drop
         kb = ctx.kb
         bias = kb.bias if kb is not None else None
+        bits = _keep_bits(bits, q, k, v, ctx.causal, ctx.window, p, seed, off)
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
-                                 bias, p, seed, off, bits if p > 0.0 else None, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
+                                 bias, p, seed, off, bits, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -179,7 +205,8 @@ class _FlashAttentionPacked(torch.autograd.Function):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
         bias = kb.bias if kb is not None else None
-        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off)
+        o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off,
+                                           _store_bits(q, k, dropout_p))
         ctx.save_for_backward(qkv, o, lse, bits)
         ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
@@ -193,9 +220,11 @@ class _FlashAttentionPacked(torch.autograd.Function):
         p, seed, off = ctx.drop
         kb = ctx.kb
         bias = kb.bias if kb is not None else None
-        ext().attention_bwd_into(do.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], o, lse, dqkv[:, :, 0],
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        bits = _keep_bits(bits, q, k, v, ctx.causal, ctx.window, p, seed, off)
+        ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dqkv[:, :, 0],
                                  dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off,
-                                 bits if p > 0.0 else None, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
+                                 bits, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
         return dqkv, None, None, None, None, None
 
 

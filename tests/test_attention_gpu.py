@@ -97,6 +97,50 @@ def test_flash_dropout_matches_host_mask(d, causal, p):
     assert not torch.equal(o.detach(), o2)
 
 
+@pytest.mark.parametrize("causal,sq,sk", [(True, 200, 200), (False, 128, 320), (True, 2048, 2048)])
+def test_keep_bits_regenerated_equal_stored(causal, sq, sk):
+    """Over the per-layer keep-bit budget the forward stores no bits and the backward
+    regenerates them from the hash: the regenerated words equal the stored ones wherever the
+    forward wrote them (tiles a query can see), and the whole backward is bitwise the same."""
+    from smdistributed_modelparallel_amd.ops import attention as A
+    from smdistributed_modelparallel_amd.ops._ext import ext
+
+    torch.manual_seed(5)
+    b, h, d, p = 2, 3, 64, 0.1
+    q = torch.randn(b, sq, h, d, device="cuda", dtype=torch.bfloat16)
+    k, v = (torch.randn(b, sk, h, d, device="cuda", dtype=torch.bfloat16) for _ in range(2))
+    seed, off = 1234, 56
+    _, _, bits = ext().attention_fwd(q, k, v, 0.125, causal, 0, None, p, seed, off)
+    regen = ext().attention_keep_bits(q, k, v, causal, 0, p, seed, off)
+    assert regen.shape == bits.shape
+    nt = (sk + 63) // 64
+    qi = torch.arange(sq, device="cuda").view(1, 1, sq, 1)
+    kt = torch.arange(nt, device="cuda").view(1, nt, 1, 1)
+    seen = (64 * kt <= qi + (sk - sq)) if causal else torch.ones(1, nt, sq, 1, dtype=torch.bool, device="cuda")
+    seen = seen.expand(b * h, nt, sq, 2)
+    assert torch.equal(bits[seen], regen[seen])
+    _, _, none = ext().attention_fwd(q, k, v, 0.125, causal, 0, None, p, seed, off, False)
+    assert none.numel() == 0
+
+    def grads(limit):
+        A.KEEPBITS_MAX_BYTES[0] = limit
+        torch.manual_seed(7)
+        qq, kk, vv = (t.detach().clone().requires_grad_() for t in (q, k, v))
+        gen = torch.cuda.default_generators[torch.cuda.current_device()]
+        gen.manual_seed(99)
+        o = A._FlashAttention.apply(qq, kk, vv, 0.125, causal, 0, None, p)
+        o.backward(torch.ones_like(o))
+        return o.detach(), qq.grad, kk.grad, vv.grad
+
+    saved = A.KEEPBITS_MAX_BYTES[0]
+    try:
+        stored, regenerated = grads(1 << 40), grads(0)
+    finally:
+        A.KEEPBITS_MAX_BYTES[0] = saved
+    for a, r in zip(stored, regenerated):
+        assert torch.equal(a, r)
+
+
 def test_flash_bench_shape_dropout_fp32():
     """The bench's attention exactly (GPT-2 XL: 25 heads x 64, s 2048, causal, dropout 0.1),
     forward and backward against fp32 with the host-rebuilt keep mask (the
