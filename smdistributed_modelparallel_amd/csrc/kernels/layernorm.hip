@@ -509,8 +509,8 @@ __global__ void __launch_bounds__(256) ln_bwd_reg(const T* __restrict__ dy, cons
 // (thread t owns vectors t and t+256), so a thread's dgamma/dbeta accumulators cover only
 // its own columns for all the block's rows -- 8*VB floats each instead of a wave's whole
 // row -- and need no LDS combine: the block writes its fp32 partial row directly.  Row
-// sums go through one LDS exchange per row (double-buffered: one barrier per row); the
-// next row's x / dy / dres vectors are loaded before the current row's reduction.
+// sums go through one LDS exchange per row (double-buffered: one barrier per row); x / dy /
+// dres are loaded two rows ahead (a ring of two register sets).
 // Low register use (high occupancy) is what the one-wave-per-row kernel lacked at 1600.
 template <typename T, typename W, int VB>
 __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, const T* __restrict__ x,
@@ -543,21 +543,24 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  Vec16<T> xa[VB], da[VB], ra[VB];
-  auto load_row = [&](int64_t row) {
+  // two rows of x / dy / dres in flight (register ring of 2): the loads of row + 2 go out as
+  // soon as row's values are in float registers, i.e. ahead of row's reduction and barrier
+  Vec16<T> xa[2][VB], da[2][VB], ra[2][VB];
+  auto load_row = [&](int64_t row, auto buf_c) {
+    constexpr int B = decltype(buf_c)::value;
 #pragma unroll
     for (int k = 0; k < VB; ++k) {
       if (act[k]) {
         const int64_t off = row * cols + static_cast<int64_t>(t + 256 * k) * N;
-        xa[k] = load16(x + off);
-        da[k] = load16(dy + off);
-        if (dres != nullptr) ra[k] = load16(dres + off);
+        xa[B][k] = load16(x + off);
+        da[B][k] = load16(dy + off);
+        if (dres != nullptr) ra[B][k] = load16(dres + off);
       }
     }
   };
-  if (r0 < r1) load_row(r0);
   int parity = 0;
-  for (int64_t row = r0; row < r1; ++row) {
+  auto body = [&](int64_t row, auto buf_c) {
+    constexpr int B = decltype(buf_c)::value;
     const float mean = mean_in[row], rstd = rstd_in[row];
     float xh[VB][N], g[VB][N], rr[VB][N];
     float s1 = 0.f, s2 = 0.f;
@@ -565,9 +568,9 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
     for (int k = 0; k < VB; ++k) {
 #pragma unroll
       for (int j = 0; j < N; ++j) {
-        const float dyv = act[k] ? to_f32(da[k].v[j]) : 0.f;
-        xh[k][j] = act[k] ? (to_f32(xa[k].v[j]) - mean) * rstd : 0.f;
-        rr[k][j] = (act[k] && dres != nullptr) ? to_f32(ra[k].v[j]) : 0.f;
+        const float dyv = act[k] ? to_f32(da[B][k].v[j]) : 0.f;
+        xh[k][j] = act[k] ? (to_f32(xa[B][k].v[j]) - mean) * rstd : 0.f;
+        rr[k][j] = (act[k] && dres != nullptr) ? to_f32(ra[B][k].v[j]) : 0.f;
         g[k][j] = dyv * wv[k][j];
         s1 += g[k][j];
         s2 += g[k][j] * xh[k][j];
@@ -575,7 +578,7 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
         dbacc[k][j] += dyv;
       }
     }
-    if (row + 1 < r1) load_row(row + 1);  // prefetch under the reduction
+    if (row + 2 < r1) load_row(row + 2, buf_c);  // this buffer's next row, two ahead
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
     if (lane == 0) {
@@ -612,6 +615,12 @@ __global__ void __launch_bounds__(256) ln_bwd_blk(const T* __restrict__ dy, cons
         store16(dxd + off, o);
       }
     }
+  };
+  if (r0 < r1) load_row(r0, std::integral_constant<int, 0>{});
+  if (r0 + 1 < r1) load_row(r0 + 1, std::integral_constant<int, 1>{});
+  for (int64_t row = r0; row < r1; row += 2) {
+    body(row, std::integral_constant<int, 0>{});
+    if (row + 1 < r1) body(row + 1, std::integral_constant<int, 1>{});
   }
   if (dw_part == nullptr) return;
 #pragma unroll
