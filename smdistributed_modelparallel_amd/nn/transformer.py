@@ -573,6 +573,31 @@ class DistributedTransformerOutputLayer(DistributedModule):
         return out
 
 
+class _Deferred:
+    """Marks a layer output whose MLP residual add (+ dropout) is deferred into the NEXT layer's
+    first LayerNorm kernel (``forward_add``: dropout + add + LN in one pass, and in the backward
+    the LN kernel writes the dropout branch's gradient too): the layer returns
+    (residual, *inputs[1:], mlp_branch, _Deferred(p)) -- the branch stays a plain tuple element,
+    visible to every hook that walks module outputs (sharded data parallel, offloading).  Saves a
+    read and a write of the hidden state per layer each way, and two kernels; results are bitwise
+    those of the separate dropout-add + LayerNorm (same hash, seed draw order and rounding).  Only
+    ever passed between two consecutive layers of one pipeline stage, never across a checkpoint
+    boundary."""
+
+    __slots__ = ("p",)
+
+    def __init__(self, p):
+        self.p = p
+
+
+_FUSE_CROSS_LAYER = [os.environ.get("SMP_FUSE_CROSS_LAYER_RESIDUAL", "1") != "0"]
+
+
+def _checkpointing_anywhere():
+    mm = state.module_manager
+    return mm is not None and len(getattr(mm, "_ckpt_config", ())) > 0
+
+
 # ========================================================== transformer layer
 class DistributedTransformerLayer(DistributedModule):
     _smp_sdp_atomic = True  # forward calls attention.core() etc. directly: never split for ZeRO
@@ -600,8 +625,22 @@ class DistributedTransformerLayer(DistributedModule):
         self.output = DistributedTransformerOutputLayer(**out_cfg)
         self.input_layer = True
         self.output_layer = True
+        self._defer_ok = False  # the next layer is on this stage and can take a deferred residual
+
+    def _structure_can_defer(self):
+        """This layer can hand its MLP residual add to the next layer (and take one)."""
+        at, out = self.attention, self.output
+        return (not self.parallel_attn_output and not self.add_cross_attention and not out.post_layernorm
+                and not at.post_layernorm and at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_add")
+                and not self._mem)
+
+    def _defers(self):
+        return self._defer_ok and _FUSE_CROSS_LAYER[0] and not self.output_layer and not _checkpointing_anywhere()
 
     def forward(self, inputs):
+        deferred = None
+        if isinstance(inputs[-1], _Deferred):
+            deferred, inputs = (inputs[-2], inputs[-1].p), inputs[:-2]
         hidden, mask = inputs[0], inputs[1]
         if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = _enter_tp(hidden, self._mem, self.hidden_size)
@@ -628,7 +667,10 @@ class DistributedTransformerLayer(DistributedModule):
             else:
                 hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:
-            if at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
+            if deferred is not None:
+                # the previous layer's MLP dropout + residual add, fused into this LN1
+                a, hidden = at.pre_layernorm_module.forward_add(deferred[0], hidden, deferred[1])
+            elif at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
                 # hidden feeds LN1 and the residual add: its two gradients meet in the LN kernel
                 a, hidden = at.pre_layernorm_module.forward_passthrough(hidden)
             else:
@@ -650,7 +692,10 @@ class DistributedTransformerLayer(DistributedModule):
                 if ca.post_layernorm:
                     hidden = ca.layernorm(hidden)
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
-            hidden = out.dropout.add(out.core(m), hidden)
+            mlp = out.core(m)
+            if self._defers():
+                return (hidden,) + tuple(inputs[1:]) + (mlp, _Deferred(out.dropout.active_p()))
+            hidden = out.dropout.add(mlp, hidden)
             if out.post_layernorm:
                 hidden = out.layernorm(hidden)
         if self._tp > 1 and self.output_layer and not _prescaled():
@@ -699,6 +744,12 @@ class DistributedTransformer(DistributedModule):
             for sub in (layer.attention, layer.output):
                 sub.input_layer = False
                 sub.output_layer = False
+        # cross-layer residual fusion: a layer may hand its MLP residual add to the next layer of
+        # its stage (checked again at run time: checkpointing, kill switch)
+        for i, layer in enumerate(layers):
+            nxt = layers[i + 1] if i + 1 < len(layers) else None
+            layer._defer_ok = (nxt is not None and not layer.output_layer and not nxt.input_layer
+                               and layer._structure_can_defer() and nxt._structure_can_defer())
 
     def forward(self, inputs):
         return self.seq_layers(inputs)

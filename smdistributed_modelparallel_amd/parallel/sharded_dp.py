@@ -479,7 +479,7 @@ class ShardedDataParallel:
                 for q, o, n, shp in zip(u.params, u.offsets, u.numels, u.shapes):
                     if q.requires_grad and q.data.numel() > 0:
                         q.grad = u.full_grad[o:o + n].view(shp)
-                i = u.params.index(p)
+                i = next(k for k, q in enumerate(u.params) if q is p)  # identity (not tensor ==)
                 o, n = u.offsets[i], u.numels[i]
                 u.full_grad[o:o + n].copy_(g.reshape(-1))
                 if p.data.numel() == n:

@@ -110,3 +110,12 @@ def test_ln_bwd_fused_dropout_output_bitwise(h):
     assert torch.equal(out[3], ref)
     plain = ext().layernorm_bwd(dy, x, w, mean, rstd, True, True, dres)
     assert torch.equal(out[0], plain[0]) and torch.equal(out[1], plain[1]) and torch.equal(out[2], plain[2])
+
+
+def test_cross_layer_residual_fusion_is_bitwise_neutral():
+    """A layer's MLP dropout + residual add deferred into the next layer's LayerNorm kernel gives
+    bitwise the same loss and gradients as the separate kernels (tests/workers/cross_layer.py)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("cross_layer", 1, [], timeout=300, env_extra={"SMP_FORCE_CPU": "0"})
+    assert "OK bitwise" in outs[0], outs[0][-2000:]
