@@ -42,6 +42,33 @@ def _lm_parity(hf_model, mod, vocab, seq=16, atol=2e-4):
     assert len([k for k in hf_sd if k not in back]) == 0, [k for k in hf_sd if k not in back][:5]
 
 
+def test_cross_layer_residual_deferral_follows_stages_and_is_exact():
+    """A pre-LN layer hands its MLP residual add to the next layer of its stage only (never
+    across a pipeline-stage boundary, never from the last layer), and the deferred forward equals
+    the plain one (fp32, CPU path)."""
+    from smdistributed_modelparallel_amd.nn import transformer as tr
+
+    torch.manual_seed(0)
+    t = DistributedTransformer(num_layers=6, num_attention_heads=2, attention_head_size=8, hidden_size=16,
+                               intermediate_size=32, pre_layernorm=True, post_layernorm=False,
+                               attention_dropout_prob=0.0, hidden_dropout_prob=0.0)
+    layers = list(t.seq_layers)
+    assert [m._defer_ok for m in layers] == [True] * 5 + [False]
+    t.update_layer_boundaries(lambda m: 0 if any(m is x for x in layers[:3]) else 1)
+    assert [m._defer_ok for m in layers] == [True, True, False, True, True, False]
+    t.update_layer_boundaries()
+    x = torch.randn(2, 8, 16)
+    outs = []
+    for fuse in (True, False):
+        tr._FUSE_CROSS_LAYER[0] = fuse
+        try:
+            outs.append(t((x, None))[0])
+        finally:
+            tr._FUSE_CROSS_LAYER[0] = True
+    assert len(t((x, None))) == 2  # no deferred items leak out of the stack
+    assert torch.allclose(outs[0], outs[1], atol=1e-6, rtol=1e-5)
+
+
 def test_gpt2_parity():
     from transformers import GPT2Config, GPT2LMHeadModel
 
