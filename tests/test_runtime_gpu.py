@@ -151,3 +151,11 @@ def test_rccl_premul_sum_probe_single_rank(tmp_path):
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=120, cwd=root)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
     print(r.stdout)
+
+
+def test_full_gpu_path_trains():
+    """40 AdamW steps of the fused bf16 path memorise one batch (tests/workers/converge.py)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("converge", 1, [], timeout=300, env_extra={"SMP_FORCE_CPU": "0"})
+    assert "OK converged" in outs[0], outs[0][-3000:]
