@@ -198,8 +198,15 @@ class BucketReducer:
 
     def shadow(self):
         """Joined rank (model.join): issue this reducer's bucket collectives in bucket order
-        with zero contributions, matching the ranks that are still training."""
+        with zero contributions, matching the ranks that are still training -- with the same
+        reduction op they use (a pre-multiplied sum when they average inside RCCL: every rank of
+        a collective must pass the same op)."""
         works = []
+        op = dist.ReduceOp.SUM
+        if self.group is not None and self.group_size > 1 and self.comm_hook is None:
+            scale = 1.0 / (self.divisor * (self.active_size or self.group_size))
+            if scale != 1.0 and self._premul_ok():
+                op = dist._make_nccl_premul_sum(scale)
         for b in self.flat.buckets:
             if self.group is None or self.group_size == 1:
                 continue
@@ -208,9 +215,10 @@ class BucketReducer:
                 works.append(self.comm_hook(b, zeros, self.group))
             elif self.shard:
                 n = b.numel // self.group_size
-                works.append(dist.reduce_scatter_tensor(zeros[:n].clone(), zeros, group=self.group, async_op=True))
+                works.append(dist.reduce_scatter_tensor(zeros[:n].clone(), zeros, op=op, group=self.group,
+                                                        async_op=True))
             else:
-                works.append(dist.all_reduce(zeros, group=self.group, async_op=True))
+                works.append(dist.all_reduce(zeros, op=op, group=self.group, async_op=True))
         for w in works:
             if w is not None and hasattr(w, "wait"):
                 w.wait()
