@@ -364,7 +364,14 @@ __global__ void __launch_bounds__(256) parts_reduce_stage2(const float* __restri
   const int64_t c = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (c >= cols) return;
   float a = accumulate ? to_f32(out[c]) : 0.f;
-  for (int p = 0; p < slices; ++p) a += part[static_cast<int64_t>(p) * cols + c];
+  // eight slice loads in flight at a time, added in slice order (deterministic)
+  for (int p = 0; p < slices; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p + j < slices ? part[static_cast<int64_t>(p + j) * cols + c] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += v[j];
+  }
   out[c] = from_f32<T>(a);
 }
 

@@ -706,9 +706,18 @@ __global__ void __launch_bounds__(256) ln_bwd_reduce_stage2(const float* __restr
   if (c >= cols) return;
   float a = (accumulate && dw) ? to_f32(dw[c]) : 0.f;
   float b = (accumulate && db) ? to_f32(db[c]) : 0.f;
-  for (int s = 0; s < slices; ++s) {
-    a += part2[static_cast<int64_t>(s) * 2 * cols + c];
-    b += part2[static_cast<int64_t>(s) * 2 * cols + cols + c];
+  // the slice loads in flight together (the adds keep their fixed order): a rolled loop waited
+  // for each load in turn, 12 us per call for 32 slices
+  float va[kLnReduceSlices], vb[kLnReduceSlices];
+#pragma unroll
+  for (int s = 0; s < kLnReduceSlices; ++s) {
+    va[s] = s < slices ? part2[static_cast<int64_t>(s) * 2 * cols + c] : 0.f;
+    vb[s] = s < slices ? part2[static_cast<int64_t>(s) * 2 * cols + cols + c] : 0.f;
+  }
+#pragma unroll
+  for (int s = 0; s < kLnReduceSlices; ++s) {
+    a += va[s];
+    b += vb[s];
   }
   if (dw) dw[c] = from_f32<W>(a);
   if (db) db[c] = from_f32<W>(b);

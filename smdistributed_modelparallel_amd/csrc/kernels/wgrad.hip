@@ -711,7 +711,14 @@ __global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restr
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float a = accumulate ? to_f32(bias[i]) : 0.f;
-  for (int p = 0; p < splits; ++p) a += cs[static_cast<int64_t>(p) * n + i];
+  // eight partial rows in flight at a time, added in order (deterministic)
+  for (int p = 0; p < splits; p += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p + j < splits ? cs[static_cast<int64_t>(p + j) * n + i] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += v[j];
+  }
   bias[i] = from_f32<TO>(a);
 }
 
