@@ -19,11 +19,11 @@ W^T copies of ``ops/linear.py``), so
 
 The user still receives [.., V] logits (a view) and can backpropagate through them.
 
-Measured on MI355X for GPT-2 XL (TunableOp-selected GEMMs, mbs 16): forward 3.50 ms padded
-vs 3.03 ms unpadded, input gradient 3.90 vs 4.74 ms, weight gradient 5.30 vs 4.91 ms -- a
-wash (same-box A/B within noise), because hipBLASLt's best kernels for the odd shape are
-already good.  The path is therefore OFF by default (``SMP_PADDED_LM_HEAD=1`` enables it)
-and kept for vocabularies where the unaligned GEMMs are slower.
+Measured on MI355X for GPT-2 XL (TunableOp-selected GEMMs, mbs 16, round 2): forward 3.50 ms
+padded vs 3.03 ms unpadded, input gradient 3.90 vs 4.74 ms, weight gradient 5.30 vs 4.91 ms --
+a wash then.  With the round-5 ping-pong weight-gradient kernel at the bench's mbs 32 the
+padded path wins: 748.38 / 748.56 vs 750.73 / 752.94 ms per step, same box alternating, same
+loss (tools/gpu_r5w.sh) -- so it is ON by default (``SMP_PADDED_LM_HEAD=0`` disables it).
 Reference behaviour being reproduced: the LM head + CE of ``DistributedTransformerLMHead``
 (`smp/torch/nn/transformer.py:455-548`).
 """
@@ -39,7 +39,7 @@ from .linear import _WT_EPOCH, _fusable
 _WGRAD_KERNEL = True
 
 _ALIGN = 64
-_ENABLED = os.environ.get("SMP_PADDED_LM_HEAD", "0") == "1"
+_ENABLED = os.environ.get("SMP_PADDED_LM_HEAD", "1") == "1"
 
 
 def _padded(w, vp):
