@@ -175,6 +175,12 @@ def p2p_record(smp, args):
     return rec
 
 
+def _lm_head_padded():
+    from smdistributed_modelparallel_amd.ops import lm_head
+
+    return bool(lm_head._ENABLED)
+
+
 def main():
     args = parse()
     import smdistributed_modelparallel_amd.torch as smp
@@ -344,6 +350,8 @@ def main():
                 "flash_attention": (not args.no_flash) and mc["attention_head_size"] in FLASH_HEAD_DIMS,
                 "dropout": args.dropout,
                 "gemm_selection": "tunableop" if tmode != "off" else "heuristic",
+                # LM head + CE over the 64-padded vocabulary (ops/lm_head.py; same loss)
+                "lm_head": "padded64" if _lm_head_padded() else "plain",
             },
             "dist_backend": dist.get_backend() if dist.is_initialized() else None,
             # world sizes of the process groups the backend actually formed (1: not created)
