@@ -498,8 +498,11 @@ struct QInLds {
 // its edge tiles: the interior tiles run a separately compiled mask-free body.  (With one loop
 // and a per-tile `if (!interior)`, hipcc if-converted the masks into ~100 VALU + ~100 SALU
 // selects executed on every tile -- profiles/r4/attention_isa.md.)
+// D = 64 DMA without dropout fits 128 VGPRs: 4 waves per SIMD instead of 3, -2 % (611 vs 624 us
+// at GPT-2 XL shape); with dropout the same bound spills 35 registers and runs 2-3 % slower
+// (profiles/r5/dropout_hash_ab.md)
 template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
-__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : 2)
+__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !DROP ? 4 : 2))
     attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr bool QLDS = QInLds<D>::v;
