@@ -1,14 +1,20 @@
 #!/bin/bash
-# Round 5: fused attention backward kernel profile (kernel trace + stats) at the bench shape,
-# and the GPT-J TP4 bf16 test on the RCCL/gloo TP path.
+# Round 5 final check: the whole GPU test suite, the default 1-GPU bench, and its step kernel table.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r5f
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5f/prof -o attn -- python tools/attn_fused_time.py \
-  > gpurun_out/r5f/prof.log 2>&1 || { tail -20 gpurun_out/r5f/prof.log; exit 1; }
-grep bwd_us gpurun_out/r5f/prof.log
-find gpurun_out/r5f/prof -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -12 {} | cut -c1-220'
-timeout -k 10 300 python -u -m pytest -v --timeout 250 --timeout-method thread \
-  "tests/test_hybrid_gpu.py::test_gptj6b_width_tp4_bf16_gpu" > gpurun_out/r5f/gptj.log 2>&1
-echo "gptj rc=$?"; tail -1 gpurun_out/r5f/gptj.log
+( while sleep 50; do echo "heartbeat $(date +%T)" >> gpurun_out/r5f/heartbeat.log; done ) &
+HB=$!
+trap "kill $HB" EXIT
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r5f/smoke.log 2>&1 || { tail -20 gpurun_out/r5f/smoke.log; exit 1; }
+tail -1 gpurun_out/r5f/smoke.log
+timeout -k 10 1000 python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread tests/ > gpurun_out/r5f/pytest.log 2>&1
+rc=$?; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/r5f/pytest.log | tail -12; [ $rc -le 1 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/r5f/bench.log 2>&1 || { tail -20 gpurun_out/r5f/bench.log; exit 1; }
+grep '"metric"' gpurun_out/r5f/bench.log
+timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/r5f/trace_bench -o t -- python3 bench.py --steps 3 --warmup 2 \
+  > gpurun_out/r5f/trace_bench.log 2>&1 || { tail -20 gpurun_out/r5f/trace_bench.log; exit 1; }
+f=$(find gpurun_out/r5f/trace_bench -name "*.db" | head -1)
+python3 tools/step_kernels.py "$f" > gpurun_out/r5f/kernels_bench.txt && head -32 gpurun_out/r5f/kernels_bench.txt
+rm -f "$f"
