@@ -139,6 +139,44 @@ class UnsupportedCommunicationVolumeUnitError(SMPUnsupportedError):
     pass
 
 
+# ------------------------------------------------------- HuggingFace translation
+class HFConfigError(SMPValidationError, NotImplementedError):
+    """An HF model config or forward argument the DistributedTransformer translation cannot
+    reproduce (reference `torch/exceptions.py:57-82`: one class per model family)."""
+
+
+class HFBertConfigError(HFConfigError):
+    pass
+
+
+class HFRobertaConfigError(HFConfigError):
+    pass
+
+
+class HFGPT2ConfigError(HFConfigError):
+    pass
+
+
+class HFGPTJConfigError(HFConfigError):
+    pass
+
+
+class HFGPTNeoConfigError(HFConfigError):
+    pass
+
+
+class HFGPTNeoxConfigError(HFConfigError):
+    pass
+
+
+class HFT5ConfigError(HFConfigError):
+    pass
+
+
+class HFViTConfigError(HFConfigError):
+    pass
+
+
 class TracingEnd(Exception):
     """Internal control-flow signal: stop the step function once the traced forward ends
     (reference `patches/tracing.py:41-86`)."""

@@ -41,8 +41,8 @@ GPT_CONFIGS = {
 def build_gpt(name, dropout=0.1, **overrides):
     cfg = dict(GPT_CONFIGS[name])
     cfg.update(attention_dropout_prob=dropout, hidden_dropout_prob=dropout, embedding_dropout_prob=dropout)
-    cfg["causal_mask_size"] = cfg["num_positions"]
     cfg.update(overrides)
+    cfg.setdefault("causal_mask_size", cfg["num_positions"])  # follows a num_positions override
     return DistributedTransformerLMHead(**cfg)
 
 

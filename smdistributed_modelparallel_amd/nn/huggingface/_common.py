@@ -57,38 +57,47 @@ def _fill_regex(pattern, groups):
     return s.replace("\\.", ".")
 
 
-def pack_qkv(sd, out, q_re, k_re, v_re, smp_fmt, bias=False):
-    """Concatenate separate q/k/v projections into the fused [3*h, h] (or [3*h]) layout."""
-    qs = {}
+def pack_parts(sd, out, patterns, smp_fmt):
+    """Concatenate separate projections (e.g. q / k / v, or a cross-attention's k / v) along
+    dim 0 into one fused smp tensor, in the order of `patterns`."""
+    groups = {}
     rest = {}
     for k, v in sd.items():
-        for role, pat in (("q", q_re), ("k", k_re), ("v", v_re)):
+        for i, pat in enumerate(patterns):
             m = re.match(r"^(.*?)" + pat + r"$", k)
             if m:
-                qs.setdefault((m.group(1), m.groups()[1:]), {})[role] = v
+                groups.setdefault((m.group(1), m.groups()[1:]), {})[i] = v
                 break
         else:
             rest[k] = v
-    for (pre, groups), parts in qs.items():
-        if len(parts) != 3:
-            raise KeyError(f"incomplete q/k/v set for {pre}{groups}")
-        out[pre + smp_fmt.format(*groups)] = torch.cat([parts["q"], parts["k"], parts["v"]], dim=0)
+    for (pre, idx), parts in groups.items():
+        if len(parts) != len(patterns):
+            raise KeyError(f"incomplete projection set for {pre}{idx}: have {sorted(parts)} of {len(patterns)}")
+        out[pre + smp_fmt.format(*idx)] = torch.cat([parts[i] for i in range(len(patterns))], dim=0)
     return rest
 
 
-def unpack_qkv(sd, out, smp_re, q_fmt, k_fmt, v_fmt):
+def unpack_parts(sd, out, smp_re, fmts):
+    """Inverse of `pack_parts`: split a fused tensor into len(fmts) equal dim-0 chunks."""
     rest = {}
     for k, v in sd.items():
         m = re.match(r"^(.*?)" + smp_re + r"$", k)
         if m:
             pre, groups = m.group(1), m.groups()[1:]
-            q, kk, vv = v.chunk(3, dim=0)
-            out[pre + q_fmt.format(*groups)] = q
-            out[pre + k_fmt.format(*groups)] = kk
-            out[pre + v_fmt.format(*groups)] = vv
+            for fmt, part in zip(fmts, v.chunk(len(fmts), dim=0)):
+                out[pre + fmt.format(*groups)] = part
         else:
             rest[k] = v
     return rest
+
+
+def pack_qkv(sd, out, q_re, k_re, v_re, smp_fmt, bias=False):
+    """Concatenate separate q/k/v projections into the fused [3*h, h] (or [3*h]) layout."""
+    return pack_parts(sd, out, (q_re, k_re, v_re), smp_fmt)
+
+
+def unpack_qkv(sd, out, smp_re, q_fmt, k_fmt, v_fmt):
+    return unpack_parts(sd, out, smp_re, (q_fmt, k_fmt, v_fmt))
 
 
 def masked_from_hf(mask):
@@ -144,10 +153,12 @@ def lm_forward_hook(input_ids=None, *args, attention_mask=None, token_type_ids=N
     if args:
         # positional past_key_values (the HF signature's 2nd argument)
         past_key_values = args[0] if past_key_values is None else past_key_values
+    from ...backend.exceptions import HFConfigError
+
     if past_key_values is not None:
-        raise NotImplementedError("past_key_values (incremental decoding) is not supported by the distributed LM head")
+        raise HFConfigError("past_key_values (incremental decoding) is not supported by the distributed LM head")
     if kwargs.get("inputs_embeds") is not None:
-        raise NotImplementedError("inputs_embeds is not supported by the distributed LM head")
+        raise HFConfigError("inputs_embeds is not supported by the distributed LM head")
     return ((input_ids, attention_mask, token_type_ids, position_ids, labels),), {}
 
 
@@ -156,8 +167,33 @@ def lm_return_hook(out):
     return causal_lm_output(out, isinstance(out, tuple))
 
 
-def encoder_forward_hook(hidden_states, attention_mask=None, *args, **kwargs):
-    return ((hidden_states, masked_from_hf(attention_mask)),), {}
+def encoder_forward_hook(hidden_states, attention_mask=None, encoder_hidden_states=None, encoder_attention_mask=None,
+                         past_key_values=None, use_cache=None, head_mask=None, output_attentions=False,
+                         output_hidden_states=False, return_dict=None, error=None, family="encoder", **kwargs):
+    """HF ``BertEncoder`` / ``RobertaEncoder`` call -> the DistributedTransformer input tuple:
+    (hidden, mask) or, with encoder states for the cross-attention layers, (hidden, mask,
+    encoder_hidden_states, encoder_mask).  Arguments the distributed stack cannot honour are
+    refused instead of silently ignored, as the reference's hooks do
+    (`nn/huggingface/bert.py:111-160`, `roberta.py:111-160`).  Pass-through kwargs of
+    transformers 5.x (``position_ids``, ``cache_position``) are ignored: absolute positions
+    live in the embeddings, outside the encoder."""
+    from ...backend.exceptions import HFConfigError
+
+    err = error or HFConfigError
+    if head_mask is not None and (not isinstance(head_mask, (list, tuple)) or any(m is not None for m in head_mask)):
+        raise err(f"head_mask argument of the HuggingFace {family} encoder is not supported")
+    if past_key_values is not None and (not hasattr(past_key_values, "get_seq_length")
+                                        or past_key_values.get_seq_length() > 0):
+        raise err(f"past_key_values argument of the HuggingFace {family} encoder is not supported")
+    if output_attentions or output_hidden_states or kwargs.get("output_attentions") or kwargs.get("output_hidden_states"):
+        raise err(f"output_attentions and output_hidden_states arguments of the HuggingFace {family} encoder are "
+                  "not supported")
+    if return_dict is not None and not return_dict:
+        raise err(f"return_dict=False for the HuggingFace {family} encoder is not supported")
+    mask = masked_from_hf(attention_mask)
+    if encoder_hidden_states is not None:
+        return ((hidden_states, mask, encoder_hidden_states, masked_from_hf(encoder_attention_mask)),), {}
+    return ((hidden_states, mask),), {}
 
 
 def encoder_return_hook(out):

@@ -1,11 +1,18 @@
-"""BERT / RoBERTa encoders (HF ``BertEncoder`` / ``RobertaEncoder``) <-> ``DistributedTransformer``.
+"""BERT encoder (HF ``BertEncoder``) <-> ``DistributedTransformer``.
 
-Reference: `smp/torch/nn/huggingface/bert.py`, `roberta.py`.  Post-LayerNorm layers,
-bidirectional attention with the HF padding mask, exact-erf GeLU (``hidden_act="gelu"``).
-Only the encoder stack is distributed; embeddings and pooler stay HF modules, so keys
-keep their ``...encoder.`` prefix: ``encoder.layer.{i}.*`` <-> ``encoder.seq_layers.{i}.*``.
+Reference: `smp/torch/nn/huggingface/bert.py`.  Post-LayerNorm layers, bidirectional
+attention with the HF padding mask (causal for ``is_decoder`` configs), exact-erf GeLU
+(``hidden_act="gelu"``), and -- for ``add_cross_attention`` configs -- a cross-attention
+block per layer fed by ``encoder_hidden_states``.  Only the encoder stack is distributed;
+embeddings and pooler stay HF modules, so keys keep their ``...encoder.`` prefix:
+``encoder.layer.{i}.*`` <-> ``encoder.seq_layers.{i}.*``.  RoBERTa shares the layout
+(`roberta.py`).
 """
-from ._common import KeyMap, encoder_forward_hook, encoder_return_hook, pack_qkv, unpack_qkv
+from functools import partial
+
+from ...backend.exceptions import HFBertConfigError
+from ._common import (KeyMap, encoder_forward_hook, encoder_return_hook, pack_parts, pack_qkv, unpack_parts,
+                      unpack_qkv)
 
 _L = r"encoder\.layer\.(\d+)\."
 _S = "encoder.seq_layers.{}."
@@ -20,12 +27,30 @@ RULES = KeyMap([
     (_L + r"output\.dense\.bias", _S + "output.dense2_bias", "copy"),
     (_L + r"output\.LayerNorm\.weight", _S + "output.layernorm.weight", "copy"),
     (_L + r"output\.LayerNorm\.bias", _S + "output.layernorm.bias", "copy"),
+    (_L + r"crossattention\.output\.dense\.weight", _S + "cross_attention.dense_weight", "copy"),
+    (_L + r"crossattention\.output\.dense\.bias", _S + "cross_attention.dense_bias", "copy"),
+    (_L + r"crossattention\.output\.LayerNorm\.weight", _S + "cross_attention.layernorm.weight", "copy"),
+    (_L + r"crossattention\.output\.LayerNorm\.bias", _S + "cross_attention.layernorm.bias", "copy"),
+    (_L + r"crossattention\.self\.query\.weight", _S + "cross_attention.qkv_weight", "copy"),
+    (_L + r"crossattention\.self\.query\.bias", _S + "cross_attention.qkv_bias", "copy"),
 ])
 
 _ACT = {"gelu": "gelu_exact", "gelu_new": "gelu", "gelu_pytorch_tanh": "gelu", "relu": "relu"}
 
 
-def config_to_kwargs(config):
+def validate_config(config, error=HFBertConfigError, family="BERT"):
+    """Configs the translation cannot reproduce (reference `bert.py:170-185`)."""
+    if config.hidden_size % config.num_attention_heads != 0:
+        raise error(f"hidden size ({config.hidden_size}) must be divisible by the number of attention heads "
+                    f"({config.num_attention_heads}) for the HuggingFace {family} model")
+    pe = getattr(config, "position_embedding_type", "absolute")
+    if pe != "absolute":
+        raise error(f"only position_embedding_type='absolute' is supported for the HuggingFace {family} model, "
+                    f"got {pe!r}")
+
+
+def config_to_kwargs(config, error=HFBertConfigError, family="BERT"):
+    validate_config(config, error, family)
     h = config.hidden_size
     return {
         "num_layers": config.num_hidden_layers,
@@ -39,7 +64,10 @@ def config_to_kwargs(config):
         "layernorm_epsilon": config.layer_norm_eps,
         "initializer_range": config.initializer_range,
         "use_normal_initialization": True,
-        "causal_mask_size": None,
+        # a decoder BERT (is_decoder) attends causally; HF then also hands the encoder a 4-D
+        # causal mask, which the layer applies on top (same result)
+        "causal_mask_size": config.max_position_embeddings if getattr(config, "is_decoder", False) else None,
+        "add_cross_attention": bool(getattr(config, "add_cross_attention", False)),
         "pre_layernorm": False,
         "post_layernorm": True,
     }
@@ -49,7 +77,7 @@ def init_hook(config, *args, **kwargs):
     return (), config_to_kwargs(config)
 
 
-forward_hook = encoder_forward_hook
+forward_hook = partial(encoder_forward_hook, error=HFBertConfigError, family="BERT")
 return_hook = encoder_return_hook
 
 
@@ -59,6 +87,10 @@ def hf_to_smp(sd):
                     _L + r"attention\.self\.value\.weight", _S + "attention.qkv_weight")
     rest = pack_qkv(rest, out, _L + r"attention\.self\.query\.bias", _L + r"attention\.self\.key\.bias",
                     _L + r"attention\.self\.value\.bias", _S + "attention.qkv_bias")
+    rest = pack_parts(rest, out, (_L + r"crossattention\.self\.key\.weight", _L + r"crossattention\.self\.value\.weight"),
+                      _S + "cross_attention.kv_weight")
+    rest = pack_parts(rest, out, (_L + r"crossattention\.self\.key\.bias", _L + r"crossattention\.self\.value\.bias"),
+                      _S + "cross_attention.kv_bias")
     rest = RULES.hf_to_smp(rest, out)
     out.update(rest)
     return out
@@ -72,6 +104,10 @@ def smp_to_hf(sd):
     rest = unpack_qkv(rest, out, r"encoder\.seq_layers\.(\d+)\.attention\.qkv_bias",
                       "encoder.layer.{}.attention.self.query.bias", "encoder.layer.{}.attention.self.key.bias",
                       "encoder.layer.{}.attention.self.value.bias")
+    for kind in ("weight", "bias"):
+        rest = unpack_parts(rest, out, r"encoder\.seq_layers\.(\d+)\.cross_attention\.kv_" + kind,
+                            ("encoder.layer.{}.crossattention.self.key." + kind,
+                             "encoder.layer.{}.crossattention.self.value." + kind))
     rest = RULES.smp_to_hf(rest, out)
     out.update(rest)
     return out

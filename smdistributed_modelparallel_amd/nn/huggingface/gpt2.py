@@ -79,9 +79,9 @@ def _activation(name):
         return "gelu"
     if name == "relu":
         return "relu"
-    from ...backend.exceptions import SMPUnsupportedError
+    from ...backend.exceptions import HFGPT2ConfigError
 
-    raise SMPUnsupportedError(f"GPT-2 activation_function {name!r} is not supported by DistributedTransformer")
+    raise HFGPT2ConfigError(f"GPT-2 activation_function {name!r} is not supported by DistributedTransformer")
 
 
 def init_hook(config, *args, **kwargs):
@@ -171,10 +171,12 @@ def layer_forward_hook(hidden_states, past_key_values=None, attention_mask=None,
     other pass-through kwargs are ignored (GPT-2 positions live in the embedding); an
     incremental-decoding cache is refused (the layer keeps no KV cache), as the reference
     refuses ``use_cache``."""
+    from ...backend.exceptions import HFGPT2ConfigError
+
     if kwargs.get("output_attentions"):
-        raise NotImplementedError("output_attentions is not supported by the distributed GPT-2 layer")
+        raise HFGPT2ConfigError("output_attentions is not supported by the distributed GPT-2 layer")
     if past_key_values is not None and past_key_values.get_seq_length() > 0:
-        raise NotImplementedError("past_key_values (incremental decoding) is not supported by the distributed GPT-2 layer")
+        raise HFGPT2ConfigError("past_key_values (incremental decoding) is not supported by the distributed GPT-2 layer")
     mask = block_mask_from_hf(attention_mask)
     if encoder_hidden_states is not None:
         return ((hidden_states, mask, encoder_hidden_states, masked_from_hf(encoder_attention_mask)),), {}

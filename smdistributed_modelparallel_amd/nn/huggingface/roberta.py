@@ -1,2 +1,28 @@
-"""RoBERTa encoder: same layer structure and key names as BERT (`bert.py`)."""
-from .bert import config_to_kwargs, forward_hook, hf_to_smp, init_hook, return_hook, smp_to_hf  # noqa: F401
+"""RoBERTa encoder (HF ``RobertaEncoder``) <-> ``DistributedTransformer``.
+
+Reference: `smp/torch/nn/huggingface/roberta.py`.  The encoder layers are BERT's (post-LN,
+exact-erf GeLU, ``encoder.layer.{i}.*`` keys, optional cross-attention), so the key rules and
+the layer translation are `bert.py`'s; what is RoBERTa's own is the validation, raised as
+``HFRobertaConfigError`` as the reference does.  RoBERTa's padding-offset position ids are
+computed by the HF embeddings module, which stays outside the distributed stack.
+"""
+from functools import partial
+
+from ...backend.exceptions import HFRobertaConfigError
+from . import bert
+from ._common import encoder_forward_hook, encoder_return_hook
+
+hf_to_smp = bert.hf_to_smp
+smp_to_hf = bert.smp_to_hf
+
+
+def config_to_kwargs(config):
+    return bert.config_to_kwargs(config, error=HFRobertaConfigError, family="RoBERTa")
+
+
+def init_hook(config, *args, **kwargs):
+    return (), config_to_kwargs(config)
+
+
+forward_hook = partial(encoder_forward_hook, error=HFRobertaConfigError, family="RoBERTa")
+return_hook = encoder_return_hook

@@ -36,7 +36,9 @@ _ACT = {"gelu": "gelu_exact", "gelu_new": "gelu", "gelu_pytorch_tanh": "gelu", "
 def config_to_kwargs(config):
     h = config.hidden_size
     if config.hidden_act not in _ACT:
-        raise ValueError(f"unsupported ViT activation {config.hidden_act!r}")
+        from ...backend.exceptions import HFViTConfigError
+
+        raise HFViTConfigError(f"unsupported ViT activation {config.hidden_act!r}")
     return {
         "num_attention_heads": config.num_attention_heads,
         "attention_head_size": h // config.num_attention_heads,
@@ -61,8 +63,10 @@ def init_hook(config, *args, **kwargs):
 
 
 def forward_hook(hidden_states, attention_mask=None, *args, **kwargs):
-    if kwargs.get("output_attentions"):
-        raise NotImplementedError("output_attentions is not supported by the distributed ViT layer")
+    if kwargs.get("output_attentions") or kwargs.get("output_hidden_states"):
+        from ...backend.exceptions import HFViTConfigError
+
+        raise HFViTConfigError("output_attentions / output_hidden_states are not supported by the distributed ViT layer")
     return ((hidden_states, masked_from_hf(attention_mask)),), {}
 
 

@@ -161,6 +161,85 @@ def test_encoder_parity(family):
     assert torch.allclose(out[valid], ref[valid], atol=2e-4, rtol=1e-3), (out[valid] - ref[valid]).abs().max()
 
 
+@pytest.mark.parametrize("family", ["bert", "roberta"])
+def test_encoder_decoder_cross_attention_parity(family):
+    """A decoder BERT / RoBERTa (is_decoder + add_cross_attention, as inside an HF
+    EncoderDecoderModel): causal self-attention with padding, cross-attention over encoder
+    states with their own padding; keys round-trip HF -> smp -> HF exactly (reference
+    `nn/huggingface/bert.py:111-160` feeds the same four-tensor input tuple)."""
+    if family == "bert":
+        from transformers import BertConfig as C
+        from transformers import BertModel as M
+
+        from smdistributed_modelparallel_amd.nn.huggingface import bert as mod
+    else:
+        from transformers import RobertaConfig as C
+        from transformers import RobertaModel as M
+
+        from smdistributed_modelparallel_amd.nn.huggingface import roberta as mod
+    from smdistributed_modelparallel_amd.nn.huggingface._common import masked_from_hf
+
+    torch.manual_seed(0)
+    hf = M(C(num_hidden_layers=2, hidden_size=64, num_attention_heads=4, intermediate_size=128, vocab_size=97,
+             max_position_embeddings=40, pad_token_id=1, is_decoder=True, add_cross_attention=True),
+           add_pooling_layer=False)
+    hf.eval()
+    kw = mod.config_to_kwargs(hf.config)
+    assert kw["add_cross_attention"] and kw["causal_mask_size"] == 40
+    enc = DistributedTransformer(**kw)
+    enc.eval()
+    hf_enc = {k: v for k, v in hf.state_dict().items() if k.startswith("encoder.")}
+    smp_sd = mod.hf_to_smp(hf_enc)
+    sd = {k[len("encoder."):]: v for k, v in smp_sd.items()}
+    missing, unexpected = enc.load_state_dict(sd, strict=False)
+    assert not missing and not unexpected, (missing, unexpected)
+    back = mod.smp_to_hf(smp_sd)
+    assert sorted(back) == sorted(hf_enc)
+    assert all(torch.equal(back[k], hf_enc[k]) for k in hf_enc)
+    ids = torch.randint(2, 97, (2, 12))
+    am = torch.ones(2, 12, dtype=torch.long)
+    am[1, 9:] = 0
+    states = torch.randn(2, 7, 64)
+    sm = torch.ones(2, 7, dtype=torch.long)
+    sm[0, 5:] = 0
+    with torch.no_grad():
+        ref = hf(input_ids=ids, attention_mask=am, encoder_hidden_states=states, encoder_attention_mask=sm,
+                 use_cache=False).last_hidden_state
+        emb = hf.embeddings(input_ids=ids)
+        # the hook takes HF-format masks (here the 2-D keep masks) and converts them itself
+        (inputs,), _ = mod.forward_hook(emb, am, encoder_hidden_states=states, encoder_attention_mask=sm)
+        assert torch.equal(inputs[1], masked_from_hf(am)) and torch.equal(inputs[3], masked_from_hf(sm))
+        assert len(inputs) == 4
+        out = enc(inputs)[0]
+    valid = am.bool()
+    assert torch.allclose(out[valid], ref[valid], atol=2e-4, rtol=1e-3), (out[valid] - ref[valid]).abs().max()
+
+
+def test_encoder_hooks_refuse_what_they_cannot_honour():
+    """Arguments / configs the distributed stack would silently get wrong raise the family's
+    config error (reference `torch/exceptions.py:57-82`, `nn/huggingface/bert.py:111-185`)."""
+    from transformers import BertConfig, RobertaConfig
+
+    from smdistributed_modelparallel_amd.backend.exceptions import HFBertConfigError, HFRobertaConfigError
+    from smdistributed_modelparallel_amd.nn.huggingface import bert, roberta
+
+    h = torch.zeros(1, 4, 8)
+    for mod, err in ((bert, HFBertConfigError), (roberta, HFRobertaConfigError)):
+        for bad in (dict(output_attentions=True), dict(output_hidden_states=True), dict(return_dict=False),
+                    dict(head_mask=[torch.ones(2)]), dict(past_key_values=object())):
+            with pytest.raises(err):
+                mod.forward_hook(h, None, **bad)
+        (inputs,), _ = mod.forward_hook(h, None, head_mask=[None, None], use_cache=False, position_ids=None)
+        assert len(inputs) == 2
+    with pytest.raises(HFBertConfigError):
+        bert.config_to_kwargs(BertConfig(hidden_size=66, num_attention_heads=4))
+    cfg = RobertaConfig(hidden_size=64, num_attention_heads=4)
+    cfg.position_embedding_type = "relative_key"
+    with pytest.raises(HFRobertaConfigError):
+        roberta.config_to_kwargs(cfg)
+    assert issubclass(HFBertConfigError, NotImplementedError)
+
+
 def test_hf_gpt2_auto_tp2_matches_hf():
     outs = run_workers("hf_gpt2_tp", 2, [], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
     assert all("OK" in o for o in outs)
