@@ -2,7 +2,9 @@
 // ops, `smp/torch/nn/transformer.py:114-182,1565-1615`).
 //
 // y = rope(x) for x [b, s, h, d] with arbitrary (b, s, h) strides (e.g. q/k views into the
-// packed QKV projection) and contiguous d; y is written contiguous [b, s, h, d].  Only the
+// packed QKV projection) and contiguous d; y has its own (b, s, h) strides (contiguous, or a
+// slice of a packed [b, s, 3, h, d] buffer; y may alias x: every element pair is read and
+// written by one thread, so the rotation can run in place).  Only the
 // first rotary_dim channels rotate; the rest are copied.  style 0 = GPT-J (interleaved
 // pairs 2i, 2i+1), 1 = GPT-NeoX (pairs i, i + rotary_dim/2).  `inverse` rotates by -theta
 // (the backward).  cos/sin come from fp32 tables [positions, rotary_dim/2].
@@ -17,17 +19,17 @@ namespace smpk {
 namespace {
 
 template <typename T>
-__global__ void __launch_bounds__(256) rope_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                   const float* __restrict__ cos_t, const float* __restrict__ sin_t,
-                                                   int64_t rows, int64_t s_len, int64_t h, int d, int rd,
-                                                   int64_t sb, int64_t ss, int64_t sh, int style, int inverse,
+__global__ void __launch_bounds__(256) rope_kernel(const T* x, T* y, const float* __restrict__ cos_t,
+                                                   const float* __restrict__ sin_t, int64_t rows, int64_t s_len,
+                                                   int64_t h, int d, int rd, int64_t sb, int64_t ss, int64_t sh,
+                                                   int64_t yb, int64_t ys, int64_t yh, int style, int inverse,
                                                    int64_t pos_offset) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int64_t hh = row % h, bs = row / h, pos = bs % s_len, bb = bs / s_len;
   const T* xr = x + bb * sb + pos * ss + hh * sh;
-  T* yr = y + row * d;
+  T* yr = y + bb * yb + pos * ys + hh * yh;
   const float* cr = cos_t + (pos + pos_offset) * (rd / 2);
   const float* sr = sin_t + (pos + pos_offset) * (rd / 2);
   const float sgn = inverse ? -1.f : 1.f;
@@ -61,11 +63,11 @@ struct VecT<4> {
 };
 
 template <typename T, int VEC, int STYLE>
-__global__ void __launch_bounds__(256) rope_vec_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                       const float* __restrict__ cos_t,
+__global__ void __launch_bounds__(256) rope_vec_kernel(const T* x, T* y, const float* __restrict__ cos_t,
                                                        const float* __restrict__ sin_t, int64_t chunks, int cpr,
                                                        int64_t s_len, int64_t h, int rd, int64_t sb, int64_t ss,
-                                                       int64_t sh, int inverse, int64_t pos_offset) {
+                                                       int64_t sh, int64_t yb, int64_t ys, int64_t yh, int inverse,
+                                                       int64_t pos_offset) {
   typedef typename VecT<VEC>::U U;
   union Pack {
     U u;
@@ -77,7 +79,7 @@ __global__ void __launch_bounds__(256) rope_vec_kernel(const T* __restrict__ x, 
   const int e0 = static_cast<int>(g - row * cpr) * VEC;
   const int64_t hh = row % h, bs = row / h, pos = bs % s_len, bb = bs / s_len;
   const T* xr = x + bb * sb + pos * ss + hh * sh;
-  T* yr = y + row * static_cast<int64_t>(cpr) * VEC;
+  T* yr = y + bb * yb + pos * ys + hh * yh;
   if (e0 >= rd) {  // pass-through channels
     *reinterpret_cast<U*>(yr + e0) = *reinterpret_cast<const U*>(xr + e0);
     return;
@@ -118,53 +120,57 @@ __global__ void __launch_bounds__(256) rope_vec_kernel(const T* __restrict__ x, 
 
 template <typename T, int VEC>
 void launch_vec(const void* x, void* y, const float* cos_t, const float* sin_t, int64_t rows, int64_t s_len,
-                int64_t h, int64_t d, int64_t rd, int64_t sb, int64_t ss, int64_t sh, int style, int inverse,
-                int64_t pos_offset, hipStream_t s) {
+                int64_t h, int64_t d, int64_t rd, int64_t sb, int64_t ss, int64_t sh, int64_t yb, int64_t ys,
+                int64_t yh, int style, int inverse, int64_t pos_offset, hipStream_t s) {
   const int cpr = static_cast<int>(d / VEC);
   const int64_t chunks = rows * cpr;
   const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
   if (style == 0)
     rope_vec_kernel<T, VEC, 0><<<grid, 256, 0, s>>>(static_cast<const T*>(x), static_cast<T*>(y), cos_t, sin_t, chunks,
-                                                    cpr, s_len, h, static_cast<int>(rd), sb, ss, sh, inverse, pos_offset);
+                                                    cpr, s_len, h, static_cast<int>(rd), sb, ss, sh, yb, ys, yh, inverse,
+                                                    pos_offset);
   else
     rope_vec_kernel<T, VEC, 1><<<grid, 256, 0, s>>>(static_cast<const T*>(x), static_cast<T*>(y), cos_t, sin_t, chunks,
-                                                    cpr, s_len, h, static_cast<int>(rd), sb, ss, sh, inverse, pos_offset);
+                                                    cpr, s_len, h, static_cast<int>(rd), sb, ss, sh, yb, ys, yh, inverse,
+                                                    pos_offset);
 }
 
 // the vector path's conditions for VEC elements per access (element size 2)
-bool rope_vec_ok(int vec, const void* x, int64_t d, int64_t rd, int64_t sb, int64_t ss, int64_t sh) {
-  return d % vec == 0 && rd % (2 * vec) == 0 && sb % vec == 0 && ss % vec == 0 && sh % vec == 0 &&
-         reinterpret_cast<uintptr_t>(x) % (2 * vec) == 0;
+bool rope_vec_ok(int vec, const void* x, const void* y, int64_t d, int64_t rd, int64_t sb, int64_t ss, int64_t sh,
+                 int64_t yb, int64_t ys, int64_t yh) {
+  return d % vec == 0 && rd % (2 * vec) == 0 && sb % vec == 0 && ss % vec == 0 && sh % vec == 0 && yb % vec == 0 &&
+         ys % vec == 0 && yh % vec == 0 && reinterpret_cast<uintptr_t>(x) % (2 * vec) == 0 &&
+         reinterpret_cast<uintptr_t>(y) % (2 * vec) == 0;
 }
 
 }  // namespace
 
 int rope_apply(int dt, const void* x, void* y, const float* cos_t, const float* sin_t, int64_t b, int64_t s_len,
                int64_t h, int64_t d, int64_t rotary_dim, int64_t stride_b, int64_t stride_s, int64_t stride_h,
-               int style, int inverse, int64_t pos_offset, hipStream_t s) {
+               int64_t y_b, int64_t y_s, int64_t y_h, int style, int inverse, int64_t pos_offset, hipStream_t s) {
   const int64_t rows = b * s_len * h;
   if (rows <= 0) return 0;
   if (rotary_dim % 2 != 0 || rotary_dim > d) return -2;
   if (dt == BF16 || dt == F16) {
     for (int vec : {8, 4}) {
-      if (!rope_vec_ok(vec, x, d, rotary_dim, stride_b, stride_s, stride_h)) continue;
+      if (!rope_vec_ok(vec, x, y, d, rotary_dim, stride_b, stride_s, stride_h, y_b, y_s, y_h)) continue;
       if (dt == BF16)
         vec == 8 ? launch_vec<bf16, 8>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                       style, inverse, pos_offset, s)
+                                       y_b, y_s, y_h, style, inverse, pos_offset, s)
                  : launch_vec<bf16, 4>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                       style, inverse, pos_offset, s);
+                                       y_b, y_s, y_h, style, inverse, pos_offset, s);
       else
         vec == 8 ? launch_vec<f16, 8>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                      style, inverse, pos_offset, s)
+                                      y_b, y_s, y_h, style, inverse, pos_offset, s)
                  : launch_vec<f16, 4>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                      style, inverse, pos_offset, s);
+                                      y_b, y_s, y_h, style, inverse, pos_offset, s);
       return static_cast<int>(hipGetLastError());
     }
   }
   SMPK_DISPATCH(dt, T, {
     rope_kernel<T><<<static_cast<unsigned>((rows + 3) / 4), 256, 0, s>>>(
         static_cast<const T*>(x), static_cast<T*>(y), cos_t, sin_t, rows, s_len, h, static_cast<int>(d),
-        static_cast<int>(rotary_dim), stride_b, stride_s, stride_h, style, inverse, pos_offset);
+        static_cast<int>(rotary_dim), stride_b, stride_s, stride_h, y_b, y_s, y_h, style, inverse, pos_offset);
   });
   return static_cast<int>(hipGetLastError());
 }

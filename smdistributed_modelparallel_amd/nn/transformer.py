@@ -42,7 +42,7 @@ from ..ops import linear as _lin
 from ..ops.gelu import bias_gelu
 from ..ops import lm_head as lm_head_op
 from ..ops.linear import linear
-from ..ops.rope import apply_rotary
+from ..ops.rope import apply_rotary, apply_rotary_qkv
 from ..torch.state_mod import state
 from .layer_norm import DistributedLayerNorm, FusedLayerNorm
 from .utils import (
@@ -387,7 +387,12 @@ class DistributedAttentionLayer(DistributedModule):
             qkv = linear(a, self.qkv_weight, self.qkv_bias, dx_allreduce=ar).view(B, s, 3, lh, d)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
-            if not self.rotary_dim and not self.attention_in_fp32:
+            if not self.attention_in_fp32 and (_ROPE_PACKED or not self.rotary_dim):
+                if self.rotary_dim:
+                    # rotary on the packed buffer: one dqkv buffer in the backward, no per-view
+                    # zero-filled gradients to add up
+                    qkv = apply_rotary_qkv(qkv, self.rotary_dim, self.rotary_emb_base or 10000,
+                                           self.gpt_neox_type_rotary)
                 ctx = attention_packed(
                     qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
                     window=self.window_size, training=self.training,
@@ -591,6 +596,8 @@ class _Deferred:
 
 
 _FUSE_CROSS_LAYER = [os.environ.get("SMP_FUSE_CROSS_LAYER_RESIDUAL", "1") != "0"]
+# rotary on the packed QKV buffer (SMP_ROPE_PACKED=0: per-view rotation, the A/B baseline)
+_ROPE_PACKED = os.environ.get("SMP_ROPE_PACKED", "1") != "0"
 
 
 def _checkpointing_anywhere():

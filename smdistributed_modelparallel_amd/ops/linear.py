@@ -232,12 +232,15 @@ def _wgrad_kernel_wins(g, dy2, x2):
 # Two kernel modes (csrc/kernels/wgrad.hip): when the input width K leaves a wave column of the
 # last 256-wide output tile idle (K % 256 in [1, 192] -- every GPT-2 XL layer but fc2, K = 1600)
 # that wave sums dY on the matrix core (B fragment = ones): no cost on the busy SIMDs, so it is
-# always fused.  Otherwise the sums go through LDS inside the MFMA loop, which in-step costs
-# about what a separate column-sum pass does (GPT-2 XL b32 kernel traces: fc1 wgrad +150 us
-# vs. bias-GeLU backward -148 us), so that mode is only used for wide dY (>= 4096 columns).
-# SMP_WGRAD_DBIAS=0 turns the fused bias sums off (separate column-sum pass).
+# always fused.  Otherwise the sums would go through LDS inside the round-4 kernel's MFMA loop
+# (the ping-pong kernel has no such mode), and forcing that kernel for the fused sums loses to
+# the table's pick plus a separate column-sum pass on the wide config 3 / 4 shapes (round 5,
+# tools/gpu_r5wb.sh: GPT-NeoX PP2xTP4 shard 263.0 / 265.7 vs 274.2 / 274.1 ms per step, GPT-J
+# TP4 shard 160.9 / 160.3 vs 162.2 / 163.1), so only the idle-wave mode is fused.
+# SMP_WGRAD_DBIAS=0 turns the fused bias sums off (separate column-sum pass); =wide restores the
+# round-4 LDS mode for dY of >= 4096 columns.
 _WGRAD_DBIAS = os.environ.get("SMP_WGRAD_DBIAS", "1") != "0"
-_WGRAD_DBIAS_MIN_N = 4096
+_WGRAD_DBIAS_MIN_N = 4096 if os.environ.get("SMP_WGRAD_DBIAS", "1") == "wide" else 1 << 62
 
 
 def _wgrad_dbias_free(k):

@@ -68,6 +68,56 @@ def apply_rotary(x, rotary_dim, base=10000, neox_style=False, offset=0):
     return apply_rotary_torch(x, rotary_dim, base, neox_style, offset)
 
 
+class _RopeQKVHIP(torch.autograd.Function):
+    """Rotary on the q / k parts of a packed [b, s, 3, h, d] QKV projection, returning a packed
+    tensor (v copied), so the attention runs on its packed path and the backward hands back ONE
+    dqkv buffer.  Rotating q and k as separate views made autograd materialise a zero-filled
+    [b, s, 3, h, d] gradient per view and add the three (GPT-J TP4 / NeoX PP2xTP4 shard traces:
+    ~250 us per layer of fills, copies and adds, profiles/r5/shards_r5.md)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, rotary_dim, neox, offset):
+        from ._ext import ext
+
+        ctx.save_for_backward(cos, sin)
+        ctx.args = (rotary_dim, neox, offset)
+        out = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        C = ext()
+        C.rope_apply_into(qkv[:, :, 0], out[:, :, 0], cos, sin, rotary_dim, neox, False, offset)
+        C.rope_apply_into(qkv[:, :, 1], out[:, :, 1], cos, sin, rotary_dim, neox, False, offset)
+        out[:, :, 2].copy_(qkv[:, :, 2])
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._ext import ext
+
+        cos, sin = ctx.saved_tensors
+        rd, neox, offset = ctx.args
+        if g.stride(-1) != 1:
+            g = g.contiguous()
+        dqkv = torch.empty(g.shape, dtype=g.dtype, device=g.device)
+        C = ext()
+        C.rope_apply_into(g[:, :, 0], dqkv[:, :, 0], cos, sin, rd, neox, True, offset)
+        C.rope_apply_into(g[:, :, 1], dqkv[:, :, 1], cos, sin, rd, neox, True, offset)
+        dqkv[:, :, 2].copy_(g[:, :, 2])
+        return dqkv, None, None, None, None, None
+
+
+def apply_rotary_qkv(qkv, rotary_dim, base=10000, neox_style=False, offset=0):
+    """Packed [b, s, 3, h, d] QKV -> packed tensor with rotary applied to q and k."""
+    if rotary_dim is None or rotary_dim == 0:
+        return qkv
+    if qkv.is_cuda and qkv.dtype in (torch.float16, torch.bfloat16, torch.float32) and qkv.stride(-1) == 1 \
+            and rotary_dim % 2 == 0:
+        s = qkv.shape[1]
+        cos, sin = rope_tables(s + offset, rotary_dim, base, qkv.device, 0)
+        return _RopeQKVHIP.apply(qkv, cos.contiguous(), sin.contiguous(), rotary_dim, neox_style, offset)
+    q = apply_rotary_torch(qkv[:, :, 0], rotary_dim, base, neox_style, offset)
+    k = apply_rotary_torch(qkv[:, :, 1], rotary_dim, base, neox_style, offset)
+    return torch.stack((q, k, qkv[:, :, 2]), dim=2)
+
+
 def apply_rotary_torch(x, rotary_dim, base=10000, neox_style=False, offset=0):
     """Plain torch implementation (CPU path and the numerics reference)."""
     if rotary_dim is None or rotary_dim == 0:

@@ -469,6 +469,40 @@ def test_rope_kernel(neox, dt, d, rd):
     assert torch.allclose(x.grad.float(), xr.grad, atol=tol * 2, rtol=tol * 2)
 
 
+@pytest.mark.parametrize("neox", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("d,rd", [(64, 32), (96, 24), (64, 10), (256, 64)])
+def test_rope_packed_qkv(neox, dt, d, rd):
+    """Rotary on a packed [b, s, 3, h, d] QKV buffer (ops.rope.apply_rotary_qkv: q / k rotated
+    straight into a packed output, v copied; the backward returns one dqkv buffer) against the
+    fp32 torch formula on each part, plus the in-place form of rope_apply_into."""
+    from smdistributed_modelparallel_amd.ops._ext import ext
+    from smdistributed_modelparallel_amd.ops.rope import apply_rotary_qkv, apply_rotary_torch, rope_tables
+
+    torch.manual_seed(5)
+    base = torch.randn(2, 37, 3 * 5 * d, device="cuda", dtype=dt)
+    qkv = base.view(2, 37, 3, 5, d).detach().requires_grad_()
+    out = apply_rotary_qkv(qkv, rd, 10000, neox)
+    ref_in = qkv.detach().float().requires_grad_()
+    ref = torch.stack((apply_rotary_torch(ref_in[:, :, 0], rd, 10000, neox),
+                       apply_rotary_torch(ref_in[:, :, 1], rd, 10000, neox), ref_in[:, :, 2]), dim=2)
+    tol = 1e-5 if dt == torch.float32 else 2e-2
+    assert out.shape == qkv.shape and out.is_contiguous()
+    assert torch.allclose(out.float(), ref, atol=tol, rtol=tol)
+    assert torch.equal(out[:, :, 2], qkv[:, :, 2])
+    g = torch.randn_like(ref)
+    out.backward(g.to(dt))
+    ref.backward(g)
+    assert torch.allclose(qkv.grad.float(), ref_in.grad, atol=tol * 2, rtol=tol * 2)
+    # in place: y aliases x (each element pair is read and written by one thread)
+    cos, sin = rope_tables(37, rd, 10000, qkv.device, 0)
+    x = qkv.detach().clone()
+    want = ext().rope_apply(x[:, :, 1], cos.contiguous(), sin.contiguous(), rd, neox, False, 0)
+    ext().rope_apply_into(x[:, :, 1], x[:, :, 1], cos.contiguous(), sin.contiguous(), rd, neox, False, 0)
+    assert torch.equal(x[:, :, 1], want)
+    assert torch.equal(x[:, :, 0], qkv[:, :, 0].detach()) and torch.equal(x[:, :, 2], qkv[:, :, 2].detach())
+
+
 def test_lamb_segmented_kernel_matches_cpu():
     """Whole-domain LAMB stage 2 (lamb_norms_chunked + lamb_stage2_chunked): per-segment trust
     ratios equal the per-parameter CPU computation; the bf16 param copy is written too."""
