@@ -537,7 +537,7 @@ at::Tensor transpose_into(at::Tensor src, at::Tensor dst) {
 
 // ------------------------------------------------------------------------ rope
 static void rope_launch(at::Tensor x, at::Tensor y, at::Tensor cos_t, at::Tensor sin_t, int64_t rotary_dim, bool neox,
-                        bool inverse, int64_t pos_offset) {
+                        bool inverse, int64_t pos_offset, bool copy_rest) {
   TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");  // strided (b, s, h) views are fine
   TORCH_CHECK(x.dim() == 4 && x.stride(3) == 1, "x must be [b, s, h, d] with contiguous d");
   TORCH_CHECK(y.is_cuda() && y.dim() == 4 && y.stride(3) == 1 && y.sizes() == x.sizes() &&
@@ -547,22 +547,25 @@ static void rope_launch(at::Tensor x, at::Tensor y, at::Tensor cos_t, at::Tensor
   TORCH_CHECK(cos_t.size(0) >= x.size(1) + pos_offset && cos_t.size(1) == rotary_dim / 2, "cos/sin table shape");
   check(smpk::rope_apply(dt_code(x), x.data_ptr(), y.data_ptr(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(),
                          x.size(0), x.size(1), x.size(2), x.size(3), rotary_dim, x.stride(0), x.stride(1), x.stride(2),
-                         y.stride(0), y.stride(1), y.stride(2), neox ? 1 : 0, inverse ? 1 : 0, pos_offset, stream()),
+                         y.stride(0), y.stride(1), y.stride(2), neox ? 1 : 0, inverse ? 1 : 0, pos_offset,
+                         copy_rest ? 1 : 0, stream()),
         "rope_apply");
 }
 
 at::Tensor rope_apply(at::Tensor x, at::Tensor cos_t, at::Tensor sin_t, int64_t rotary_dim, bool neox, bool inverse,
                       int64_t pos_offset) {
   auto y = at::empty({x.size(0), x.size(1), x.size(2), x.size(3)}, x.options());
-  rope_launch(x, y, cos_t, sin_t, rotary_dim, neox, inverse, pos_offset);
+  rope_launch(x, y, cos_t, sin_t, rotary_dim, neox, inverse, pos_offset, true);
   return y;
 }
 
 // y = rope(x) into a caller-given [b, s, h, d] view (e.g. the q / k slices of a packed QKV
-// buffer); y may be x itself (in-place rotation)
+// buffer); y may be x itself (in-place rotation, with copy_rest = false touching only the
+// rotary channels)
 void rope_apply_into(at::Tensor x, at::Tensor y, at::Tensor cos_t, at::Tensor sin_t, int64_t rotary_dim, bool neox,
-                     bool inverse, int64_t pos_offset) {
-  rope_launch(x, y, cos_t, sin_t, rotary_dim, neox, inverse, pos_offset);
+                     bool inverse, int64_t pos_offset, bool copy_rest) {
+  TORCH_CHECK(copy_rest || x.data_ptr() == y.data_ptr(), "copy_rest = false needs y to be x (in place)");
+  rope_launch(x, y, cos_t, sin_t, rotary_dim, neox, inverse, pos_offset, copy_rest);
 }
 
 // --------------------------------------------------------------------- softmax
@@ -856,7 +859,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("impl") = -1);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("rope_apply", &rope_apply);
-  m.def("rope_apply_into", &rope_apply_into);
+  m.def("rope_apply_into", &rope_apply_into, py::arg("x"), py::arg("y"), py::arg("cos"), py::arg("sin"),
+        py::arg("rotary_dim"), py::arg("neox"), py::arg("inverse"), py::arg("pos_offset"), py::arg("copy_rest") = true);
   m.def("bias_gelu_bwd_dbias", &bias_gelu_bwd_dbias, py::arg("dy"), py::arg("x"), py::arg("bias"),
         py::arg("dbias_out") = py::none(), py::arg("exact") = false);
   m.def("scaled_masked_softmax_fwd", &scaled_masked_softmax_fwd);

@@ -141,11 +141,12 @@ int scaled_softmax_bwd(int dt, const void* dy, const void* y, void* dx, int64_t 
 
 // ------------------------------------------------------------------------ rope (rope.hip)
 // y = rope(x): x and y [b, s, h, d] with their own (b, s, h) strides and contiguous d (y may
-// alias x); rotary_dim channels rotate, style 0 = GPT-J (interleaved pairs), 1 = NeoX (half
+// alias x); rotary_dim channels rotate (the rest are copied unless copy_rest = 0), style 0 = GPT-J (interleaved pairs), 1 = NeoX (half
 // rotation), inverse = rotate by -theta (backward).  cos/sin tables [positions, rotary_dim/2] fp32.
 int rope_apply(int dt, const void* x, void* y, const float* cos_t, const float* sin_t, int64_t b, int64_t s_len,
                int64_t h, int64_t d, int64_t rotary_dim, int64_t stride_b, int64_t stride_s, int64_t stride_h,
-               int64_t y_b, int64_t y_s, int64_t y_h, int style, int inverse, int64_t pos_offset, hipStream_t s);
+               int64_t y_b, int64_t y_s, int64_t y_h, int style, int inverse, int64_t pos_offset, int copy_rest,
+               hipStream_t s);
 
 // -------------------------------------------------------------- attention (attention.hip)
 // Flash-style attention, bf16/fp16 in, fp32 softmax stats. q,k,v,o: [b, h, s, d] with

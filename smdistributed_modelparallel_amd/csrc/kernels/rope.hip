@@ -5,7 +5,8 @@
 // packed QKV projection) and contiguous d; y has its own (b, s, h) strides (contiguous, or a
 // slice of a packed [b, s, 3, h, d] buffer; y may alias x: every element pair is read and
 // written by one thread, so the rotation can run in place).  Only the
-// first rotary_dim channels rotate; the rest are copied.  style 0 = GPT-J (interleaved
+// first rotary_dim channels rotate; the rest are copied (copy_rest = 0 leaves them alone: the
+// in-place form then reads and writes the rotary channels only).  style 0 = GPT-J (interleaved
 // pairs 2i, 2i+1), 1 = GPT-NeoX (pairs i, i + rotary_dim/2).  `inverse` rotates by -theta
 // (the backward).  cos/sin come from fp32 tables [positions, rotary_dim/2].
 //
@@ -23,7 +24,7 @@ __global__ void __launch_bounds__(256) rope_kernel(const T* x, T* y, const float
                                                    const float* __restrict__ sin_t, int64_t rows, int64_t s_len,
                                                    int64_t h, int d, int rd, int64_t sb, int64_t ss, int64_t sh,
                                                    int64_t yb, int64_t ys, int64_t yh, int style, int inverse,
-                                                   int64_t pos_offset) {
+                                                   int64_t pos_offset, int copy_rest) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -42,7 +43,8 @@ __global__ void __launch_bounds__(256) rope_kernel(const T* x, T* y, const float
     yr[i0] = from_f32<T>(a * c - b * sn);
     yr[i1] = from_f32<T>(b * c + a * sn);
   }
-  for (int i = rd + lane; i < d; i += 64) yr[i] = xr[i];
+  if (copy_rest)
+    for (int i = rd + lane; i < d; i += 64) yr[i] = xr[i];
 }
 
 // Vector path: one thread per VEC-element chunk of a row (VEC = 8: 16-byte accesses, VEC = 4:
@@ -121,8 +123,9 @@ __global__ void __launch_bounds__(256) rope_vec_kernel(const T* x, T* y, const f
 template <typename T, int VEC>
 void launch_vec(const void* x, void* y, const float* cos_t, const float* sin_t, int64_t rows, int64_t s_len,
                 int64_t h, int64_t d, int64_t rd, int64_t sb, int64_t ss, int64_t sh, int64_t yb, int64_t ys,
-                int64_t yh, int style, int inverse, int64_t pos_offset, hipStream_t s) {
-  const int cpr = static_cast<int>(d / VEC);
+                int64_t yh, int style, int inverse, int64_t pos_offset, int copy_rest, hipStream_t s) {
+  // without the pass-through copy (in-place rotation) only the rotary chunks get a thread
+  const int cpr = static_cast<int>((copy_rest ? d : rd) / VEC);
   const int64_t chunks = rows * cpr;
   const unsigned grid = static_cast<unsigned>((chunks + 255) / 256);
   if (style == 0)
@@ -147,7 +150,8 @@ bool rope_vec_ok(int vec, const void* x, const void* y, int64_t d, int64_t rd, i
 
 int rope_apply(int dt, const void* x, void* y, const float* cos_t, const float* sin_t, int64_t b, int64_t s_len,
                int64_t h, int64_t d, int64_t rotary_dim, int64_t stride_b, int64_t stride_s, int64_t stride_h,
-               int64_t y_b, int64_t y_s, int64_t y_h, int style, int inverse, int64_t pos_offset, hipStream_t s) {
+               int64_t y_b, int64_t y_s, int64_t y_h, int style, int inverse, int64_t pos_offset, int copy_rest,
+               hipStream_t s) {
   const int64_t rows = b * s_len * h;
   if (rows <= 0) return 0;
   if (rotary_dim % 2 != 0 || rotary_dim > d) return -2;
@@ -156,21 +160,21 @@ int rope_apply(int dt, const void* x, void* y, const float* cos_t, const float* 
       if (!rope_vec_ok(vec, x, y, d, rotary_dim, stride_b, stride_s, stride_h, y_b, y_s, y_h)) continue;
       if (dt == BF16)
         vec == 8 ? launch_vec<bf16, 8>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                       y_b, y_s, y_h, style, inverse, pos_offset, s)
+                                       y_b, y_s, y_h, style, inverse, pos_offset, copy_rest, s)
                  : launch_vec<bf16, 4>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                       y_b, y_s, y_h, style, inverse, pos_offset, s);
+                                       y_b, y_s, y_h, style, inverse, pos_offset, copy_rest, s);
       else
         vec == 8 ? launch_vec<f16, 8>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                      y_b, y_s, y_h, style, inverse, pos_offset, s)
+                                      y_b, y_s, y_h, style, inverse, pos_offset, copy_rest, s)
                  : launch_vec<f16, 4>(x, y, cos_t, sin_t, rows, s_len, h, d, rotary_dim, stride_b, stride_s, stride_h,
-                                      y_b, y_s, y_h, style, inverse, pos_offset, s);
+                                      y_b, y_s, y_h, style, inverse, pos_offset, copy_rest, s);
       return static_cast<int>(hipGetLastError());
     }
   }
   SMPK_DISPATCH(dt, T, {
     rope_kernel<T><<<static_cast<unsigned>((rows + 3) / 4), 256, 0, s>>>(
         static_cast<const T*>(x), static_cast<T*>(y), cos_t, sin_t, rows, s_len, h, static_cast<int>(d),
-        static_cast<int>(rotary_dim), stride_b, stride_s, stride_h, y_b, y_s, y_h, style, inverse, pos_offset);
+        static_cast<int>(rotary_dim), stride_b, stride_s, stride_h, y_b, y_s, y_h, style, inverse, pos_offset, copy_rest);
   });
   return static_cast<int>(hipGetLastError());
 }

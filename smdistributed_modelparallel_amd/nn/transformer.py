@@ -384,15 +384,18 @@ class DistributedAttentionLayer(DistributedModule):
             k, v = kv[:, :, 0], kv[:, :, 1]
             causal, mask = False, cross_mask
         else:
-            qkv = linear(a, self.qkv_weight, self.qkv_bias, dx_allreduce=ar).view(B, s, 3, lh, d)
-            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
             causal = self.causal_mask_size is not None
-            if not self.attention_in_fp32 and (_ROPE_PACKED or not self.rotary_dim):
-                if self.rotary_dim:
-                    # rotary on the packed buffer: one dqkv buffer in the backward, no per-view
-                    # zero-filled gradients to add up
-                    qkv = apply_rotary_qkv(qkv, self.rotary_dim, self.rotary_emb_base or 10000,
-                                           self.gpt_neox_type_rotary)
+            packed = not self.attention_in_fp32 and (_ROPE_PACKED or not self.rotary_dim)
+            if packed and self.rotary_dim:
+                # rotary on the packed buffer, in place on the projection's 2-D (non-view) output:
+                # one dqkv buffer in the backward, no per-view zero-filled gradients to add up
+                y = linear(a.reshape(B * s, a.shape[-1]), self.qkv_weight, self.qkv_bias, dx_allreduce=ar)
+                y = apply_rotary_qkv(y, B, s, lh, d, self.rotary_dim, self.rotary_emb_base or 10000,
+                                     self.gpt_neox_type_rotary)
+            else:
+                y = linear(a, self.qkv_weight, self.qkv_bias, dx_allreduce=ar)
+            if packed:
+                qkv = y.view(B, s, 3, lh, d)
                 ctx = attention_packed(
                     qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
                     window=self.window_size, training=self.training,
@@ -402,6 +405,8 @@ class DistributedAttentionLayer(DistributedModule):
                 # row-parallel: the TP all-reduce runs per token chunk beside the next chunk's GEMM
                 return linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias,
                               fwd_ar=fwd_allreduce_async if self._tp > 1 and reduce else None)
+            qkv = y.view(B, s, 3, lh, d)
+            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         if self.rotary_dim:
             base = self.rotary_emb_base or 10000
             q = apply_rotary(q, self.rotary_dim, base, self.gpt_neox_type_rotary)

@@ -225,6 +225,8 @@ class _FlashAttentionPacked(torch.autograd.Function):
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dqkv[:, :, 0],
                                  dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off,
                                  bits, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
+        # a fresh buffer no one else holds: the packed rotary's backward may rotate it in place
+        dqkv._smp_fresh_grad = True
         return dqkv, None, None, None, None, None
 
 

@@ -8,6 +8,7 @@ than on-device trig, per the elementwise guidance for CDNA).
 import torch
 
 _cache = {}
+PACKED_CALLS = [0]  # GPU in-place packed-QKV rotations (tests check the fast path engaged)
 
 
 def rope_tables(seq_len, rotary_dim, base, device, offset=0):
@@ -69,53 +70,67 @@ def apply_rotary(x, rotary_dim, base=10000, neox_style=False, offset=0):
 
 
 class _RopeQKVHIP(torch.autograd.Function):
-    """Rotary on the q / k parts of a packed [b, s, 3, h, d] QKV projection, returning a packed
-    tensor (v copied), so the attention runs on its packed path and the backward hands back ONE
-    dqkv buffer.  Rotating q and k as separate views made autograd materialise a zero-filled
+    """Rotary on the q / k parts of the packed QKV projection output ``y`` [b, s, 3 h d], IN
+    PLACE and on the rotary channels only (v and the pass-through channels are not touched), so
+    the attention takes its packed path and its backward hands back one dqkv buffer, which is
+    rotated back in place.  Rotating q and k as separate views made autograd build a zero-filled
     [b, s, 3, h, d] gradient per view and add the three (GPT-J TP4 / NeoX PP2xTP4 shard traces:
-    ~250 us per layer of fills, copies and adds, profiles/r5/shards_r5.md)."""
+    ~250 us per layer of fills, copies and adds, profiles/r5/shards_r5.md).  ``y`` must be a
+    non-view tensor that no other autograd node saved (a linear layer's output: its backward
+    keeps the input and the weight); its gradient is rotated back in place only when its
+    producer marked it a fresh buffer (``_smp_fresh_grad``, set by the packed attention)."""
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, rotary_dim, neox, offset):
+    def forward(ctx, y, cos, sin, rotary_dim, neox, offset, batch, seq, heads, d):
         from ._ext import ext
 
         ctx.save_for_backward(cos, sin)
-        ctx.args = (rotary_dim, neox, offset)
-        out = torch.empty(qkv.shape, dtype=qkv.dtype, device=qkv.device)
+        ctx.args = (rotary_dim, neox, offset, batch, seq, heads, d)
+        y5 = y.view(batch, seq, 3, heads, d)
         C = ext()
-        C.rope_apply_into(qkv[:, :, 0], out[:, :, 0], cos, sin, rotary_dim, neox, False, offset)
-        C.rope_apply_into(qkv[:, :, 1], out[:, :, 1], cos, sin, rotary_dim, neox, False, offset)
-        out[:, :, 2].copy_(qkv[:, :, 2])
-        return out
+        for part in (0, 1):
+            C.rope_apply_into(y5[:, :, part], y5[:, :, part], cos, sin, rotary_dim, neox, False, offset, False)
+        ctx.mark_dirty(y)
+        return y
 
     @staticmethod
     def backward(ctx, g):
         from ._ext import ext
 
         cos, sin = ctx.saved_tensors
-        rd, neox, offset = ctx.args
-        if g.stride(-1) != 1:
-            g = g.contiguous()
-        dqkv = torch.empty(g.shape, dtype=g.dtype, device=g.device)
+        rd, neox, offset, batch, seq, heads, d = ctx.args
+        # rotated back in place when the producer declared the buffer its own fresh allocation
+        # (the packed attention's dqkv, seen here through the view); any other gradient -- e.g.
+        # one a caller passed to backward() -- is copied first
+        owner = g._base if g._base is not None else g
+        if not (g.is_contiguous() and getattr(owner, "_smp_fresh_grad", False)):
+            g = g.clone(memory_format=torch.contiguous_format)
+        g5 = g.view(batch, seq, 3, heads, d)
         C = ext()
-        C.rope_apply_into(g[:, :, 0], dqkv[:, :, 0], cos, sin, rd, neox, True, offset)
-        C.rope_apply_into(g[:, :, 1], dqkv[:, :, 1], cos, sin, rd, neox, True, offset)
-        dqkv[:, :, 2].copy_(g[:, :, 2])
-        return dqkv, None, None, None, None, None
+        for part in (0, 1):
+            C.rope_apply_into(g5[:, :, part], g5[:, :, part], cos, sin, rd, neox, True, offset, False)
+        return g, None, None, None, None, None, None, None, None, None
 
 
-def apply_rotary_qkv(qkv, rotary_dim, base=10000, neox_style=False, offset=0):
-    """Packed [b, s, 3, h, d] QKV -> packed tensor with rotary applied to q and k."""
+def apply_rotary_qkv(y, batch, seq, heads, head_dim, rotary_dim, base=10000, neox_style=False, offset=0):
+    """Packed QKV projection output ``y`` (batch * seq * 3 * heads * head_dim elements, e.g. the
+    2-D [batch * seq, 3 * heads * head_dim] output of a linear layer) -> [batch, seq, 3, heads,
+    head_dim] with rotary applied to q and k.  GPU: in place on ``y``, which must then be a
+    contiguous non-view tensor (a 2-D linear output is; a 3-D one is a view of the GEMM's 2-D
+    result) -- otherwise the out-of-place torch path runs."""
     if rotary_dim is None or rotary_dim == 0:
-        return qkv
-    if qkv.is_cuda and qkv.dtype in (torch.float16, torch.bfloat16, torch.float32) and qkv.stride(-1) == 1 \
-            and rotary_dim % 2 == 0:
-        s = qkv.shape[1]
-        cos, sin = rope_tables(s + offset, rotary_dim, base, qkv.device, 0)
-        return _RopeQKVHIP.apply(qkv, cos.contiguous(), sin.contiguous(), rotary_dim, neox_style, offset)
-    q = apply_rotary_torch(qkv[:, :, 0], rotary_dim, base, neox_style, offset)
-    k = apply_rotary_torch(qkv[:, :, 1], rotary_dim, base, neox_style, offset)
-    return torch.stack((q, k, qkv[:, :, 2]), dim=2)
+        return y.view(batch, seq, 3, heads, head_dim)
+    if y.is_cuda and y.dtype in (torch.float16, torch.bfloat16, torch.float32) and y.is_contiguous() \
+            and rotary_dim % 2 == 0 and y._base is None:
+        cos, sin = rope_tables(seq + offset, rotary_dim, base, y.device, 0)
+        PACKED_CALLS[0] += 1
+        out = _RopeQKVHIP.apply(y, cos.contiguous(), sin.contiguous(), rotary_dim, neox_style, offset, batch, seq,
+                                heads, head_dim)
+        return out.view(batch, seq, 3, heads, head_dim)
+    y5 = y.view(batch, seq, 3, heads, head_dim)
+    q = apply_rotary_torch(y5[:, :, 0], rotary_dim, base, neox_style, offset)
+    k = apply_rotary_torch(y5[:, :, 1], rotary_dim, base, neox_style, offset)
+    return torch.stack((q, k, y5[:, :, 2]), dim=2)
 
 
 def apply_rotary_torch(x, rotary_dim, base=10000, neox_style=False, offset=0):

@@ -473,34 +473,68 @@ def test_rope_kernel(neox, dt, d, rd):
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("d,rd", [(64, 32), (96, 24), (64, 10), (256, 64)])
 def test_rope_packed_qkv(neox, dt, d, rd):
-    """Rotary on a packed [b, s, 3, h, d] QKV buffer (ops.rope.apply_rotary_qkv: q / k rotated
-    straight into a packed output, v copied; the backward returns one dqkv buffer) against the
-    fp32 torch formula on each part, plus the in-place form of rope_apply_into."""
-    from smdistributed_modelparallel_amd.ops._ext import ext
-    from smdistributed_modelparallel_amd.ops.rope import apply_rotary_qkv, apply_rotary_torch, rope_tables
+    """Rotary on a packed QKV projection output (ops.rope.apply_rotary_qkv: q / k rotated in
+    place on their rotary channels only, v and the pass-through channels untouched; the
+    backward rotates the one dqkv buffer back in place) against the fp32 torch formula."""
+    from smdistributed_modelparallel_amd.ops import rope
 
     torch.manual_seed(5)
-    base = torch.randn(2, 37, 3 * 5 * d, device="cuda", dtype=dt)
-    qkv = base.view(2, 37, 3, 5, d).detach().requires_grad_()
-    out = apply_rotary_qkv(qkv, rd, 10000, neox)
-    ref_in = qkv.detach().float().requires_grad_()
-    ref = torch.stack((apply_rotary_torch(ref_in[:, :, 0], rd, 10000, neox),
-                       apply_rotary_torch(ref_in[:, :, 1], rd, 10000, neox), ref_in[:, :, 2]), dim=2)
+    leaf = torch.randn(2, 37, 3 * 5 * d, device="cuda", dtype=dt, requires_grad=True)
+    y = leaf * 1  # a non-leaf, non-view tensor, like a linear layer's output
+    before = y.detach().clone().view(2, 37, 3, 5, d)
+    n0 = rope.PACKED_CALLS[0]
+    out = rope.apply_rotary_qkv(y, 2, 37, 5, d, rd, 10000, neox)
+    assert rope.PACKED_CALLS[0] == n0 + 1
+    assert out.shape == (2, 37, 3, 5, d) and out.data_ptr() == y.data_ptr()  # in place
+    ref_in = before.float().requires_grad_()
+    ref = torch.stack((rope.apply_rotary_torch(ref_in[:, :, 0], rd, 10000, neox),
+                       rope.apply_rotary_torch(ref_in[:, :, 1], rd, 10000, neox), ref_in[:, :, 2]), dim=2)
     tol = 1e-5 if dt == torch.float32 else 2e-2
-    assert out.shape == qkv.shape and out.is_contiguous()
     assert torch.allclose(out.float(), ref, atol=tol, rtol=tol)
-    assert torch.equal(out[:, :, 2], qkv[:, :, 2])
+    assert torch.equal(out[:, :, 2], before[:, :, 2])
+    assert torch.equal(out[..., rd:], before[..., rd:])  # pass-through channels untouched
     g = torch.randn_like(ref)
-    out.backward(g.to(dt))
+    gd = g.to(dt).clone()
+    keep = gd.clone()
+    out.backward(gd)
     ref.backward(g)
-    assert torch.allclose(qkv.grad.float(), ref_in.grad, atol=tol * 2, rtol=tol * 2)
-    # in place: y aliases x (each element pair is read and written by one thread)
-    cos, sin = rope_tables(37, rd, 10000, qkv.device, 0)
-    x = qkv.detach().clone()
-    want = ext().rope_apply(x[:, :, 1], cos.contiguous(), sin.contiguous(), rd, neox, False, 0)
-    ext().rope_apply_into(x[:, :, 1], x[:, :, 1], cos.contiguous(), sin.contiguous(), rd, neox, False, 0)
-    assert torch.equal(x[:, :, 1], want)
-    assert torch.equal(x[:, :, 0], qkv[:, :, 0].detach()) and torch.equal(x[:, :, 2], qkv[:, :, 2].detach())
+    assert torch.allclose(leaf.grad.float().view_as(ref_in.grad), ref_in.grad, atol=tol * 2, rtol=tol * 2)
+    assert torch.equal(gd, keep)  # a caller's gradient is not modified (only marked fresh buffers are)
+
+
+@pytest.mark.parametrize("neox", [False, True])
+def test_rotary_layer_packed_matches_per_view(neox):
+    """A rotary DistributedTransformer (GPT-J / NeoX style) on GPU: the packed in-place rotary
+    path gives the same outputs and gradients as the per-view path (SMP_ROPE_PACKED=0)."""
+    import smdistributed_modelparallel_amd.nn.transformer as T
+    from smdistributed_modelparallel_amd.nn import DistributedTransformer
+    from smdistributed_modelparallel_amd.ops import rope
+
+    torch.manual_seed(0)
+    kw = dict(num_layers=2, num_attention_heads=4, attention_head_size=64, hidden_size=256, intermediate_size=512,
+              rotary_dim=16 if neox else 32, gpt_neox_type_rotary=neox, causal_mask_size=128,
+              attention_dropout_prob=0.0, hidden_dropout_prob=0.0, pre_layernorm=True, post_layernorm=False,
+              parallel_attn_output=True)
+    ref = DistributedTransformer(**kw).cuda().to(torch.bfloat16)
+    x = torch.randn(2, 128, 256, device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for packed in (True, False):
+        T._ROPE_PACKED = packed
+        try:
+            m = DistributedTransformer(**kw).cuda().to(torch.bfloat16)
+            m.load_state_dict(ref.state_dict())
+            xi = x.clone().requires_grad_()
+            n0 = rope.PACKED_CALLS[0]
+            out = m((xi, None))[0]
+            out.float().pow(2).sum().backward()
+            assert (rope.PACKED_CALLS[0] > n0) == packed
+            res[packed] = (out.float(), xi.grad.float(), [p.grad.float() for p in m.parameters()])
+        finally:
+            T._ROPE_PACKED = True
+    a, b = res[True], res[False]
+    assert torch.allclose(a[0], b[0], atol=2e-2, rtol=2e-2)
+    for u, v in [(a[1], b[1])] + list(zip(a[2], b[2])):
+        assert ((u - v).norm() / v.norm().clamp_min(1e-6)).item() < 2e-2
 
 
 def test_lamb_segmented_kernel_matches_cpu():
