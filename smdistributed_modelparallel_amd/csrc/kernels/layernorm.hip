@@ -311,17 +311,40 @@ __global__ void __launch_bounds__(256) ln_bwd_wide(const T* __restrict__ dy, con
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < rows ? r0 + rows_per_block : rows;
-  for (int64_t row = r0; row < r1; ++row) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    Vec16<T> xa[VB], da[VB];
-    float s1 = 0.f, s2 = 0.f;
+  // a ring of two register rows (VB <= 4: the second set fits beside the dgamma / dbeta
+  // accumulators): the next row's x / dy / dres loads are in flight while this row reduces,
+  // crosses its barrier and writes dx -- one row at a time left each block waiting on HBM
+#ifndef SMPK_LN_WIDE_RING
+#define SMPK_LN_WIDE_RING 1
+#endif
+  constexpr bool RING = SMPK_LN_WIDE_RING && VB <= 4;
+  constexpr int VR = RING ? VB : 1;
+  Vec16<T> xa[VB], da[VB], ra[VB], xn[VR], dn[VR], rn[VR];
+  auto load_row = [&](int64_t row, Vec16<T>* xx, Vec16<T>* dd, Vec16<T>* rr) {
 #pragma unroll
     for (int k = 0; k < VB; ++k) {
       const int vi = t + 256 * k;
       if (vi < nvec) {
         const int64_t off = row * cols + static_cast<int64_t>(vi) * N;
-        xa[k] = load16(x + off);
-        da[k] = load16(dy + off);
+        xx[k] = load16(x + off);
+        dd[k] = load16(dy + off);
+        if (dres != nullptr) rr[k] = load16(dres + off);
+      }
+    }
+  };
+  if (RING && r0 < r1) load_row(r0, xa, da, ra);
+  for (int64_t row = r0; row < r1; ++row) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    if constexpr (RING) {
+      if (row + 1 < r1) load_row(row + 1, xn, dn, rn);
+    } else {
+      load_row(row, xa, da, ra);
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < VB; ++k) {
+      const int vi = t + 256 * k;
+      if (vi < nvec) {
         float g[N];
         if (w) {
           load_wn<W, N>(w + vi * N, g);
@@ -369,17 +392,23 @@ __global__ void __launch_bounds__(256) ln_bwd_wide(const T* __restrict__ dy, con
 #pragma unroll
           for (int j = 0; j < N; ++j) g[j] = 1.f;
         }
-        Vec16<T> ra;
-        if (dres != nullptr) ra = load16(dres + off);
         Vec16<T> o;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
           const float xh = (to_f32(xa[k].v[j]) - mean) * rstd;
           float vv = rstd * (to_f32(da[k].v[j]) * g[j] - s1 - xh * s2);
-          if (dres != nullptr) vv += to_f32(ra.v[j]);
+          if (dres != nullptr) vv += to_f32(ra[k].v[j]);
           o.v[j] = from_f32<T>(vv);
         }
         store16(dx + off, o);
+      }
+    }
+    if constexpr (RING) {
+#pragma unroll
+      for (int k = 0; k < VB; ++k) {
+        xa[k] = xn[k];
+        da[k] = dn[k];
+        ra[k] = rn[k];
       }
     }
   }
