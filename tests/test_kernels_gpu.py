@@ -54,6 +54,30 @@ def test_layernorm_fwd_bwd(C, dt, cols):
     assert _rel(b.grad, br.grad) < _REL[dt], _rel(b.grad, br.grad)
 
 
+@pytest.mark.parametrize("cols", [6144, 8192])
+@pytest.mark.parametrize("with_dres", [False, True])
+def test_layernorm_wide_bwd_many_rows(C, cols, with_dres):
+    """Wide-row LayerNorm backward over many rows per block (the two-row register ring carries
+    the next row's x / dy / residual gradient across iterations): dx, dgamma, dbeta against
+    fp32 at 4099 rows (odd, so the last block is short)."""
+    torch.manual_seed(2)
+    rows = 4099
+    x = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(cols, device="cuda")).to(torch.bfloat16)
+    b = (0.1 * torch.randn(cols, device="cuda")).to(torch.bfloat16)
+    y, mean, rstd = C.layernorm_fwd(x, None, w, b, 1e-5)
+    dy = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16)
+    dr = torch.randn(rows, cols, device="cuda", dtype=torch.bfloat16) if with_dres else None
+    dx, dw, db = C.layernorm_bwd(dy, x, w, mean, rstd, True, True, dr, None, None, None, 0.0)[:3]
+    xr = x.float().requires_grad_()
+    wr, br = w.float().requires_grad_(), b.float().requires_grad_()
+    torch.nn.functional.layer_norm(xr, (cols,), wr, br, 1e-5).backward(dy.float())
+    want = xr.grad + (dr.float() if with_dres else 0.0)
+    assert _rel(dx, want) < 1e-2, _rel(dx, want)
+    assert _rel(dw, wr.grad) < 1e-2, _rel(dw, wr.grad)
+    assert _rel(db, br.grad) < 1e-2, _rel(db, br.grad)
+
+
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("cols", [1600, 6144])
 def test_add_layernorm(C, dt, cols):
