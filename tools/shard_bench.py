@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--layers", type=int, default=None, help="override the layer count (smoke tests)")
+    ap.add_argument("--tunableop", choices=["auto", "off", "use", "tune"], default="auto",
+                    help="per-shape GEMM solutions (configs/tunableop/<shard>_mbs<m>_s<s>.csv): 'tune' measures "
+                         "them during warmup and writes the file, auto = use when the file exists")
     args = ap.parse_args()
 
     import torch
@@ -77,7 +80,12 @@ def main():
     import smdistributed_modelparallel_amd.torch as smp
     from smdistributed_modelparallel_amd.models import GPT_CONFIGS, build_gpt, gpt_inputs
 
-    os.environ.setdefault("SMP_STEP_TIMEOUT_S", "600")
+    os.environ.setdefault("SMP_STEP_TIMEOUT_S", "3600" if args.tunableop == "tune" else "600")
+    import bench  # the repo-root benchmark's TunableOp helpers
+
+    tfile = os.path.join(ROOT, "configs", "tunableop", f"{args.shard}_mbs{args.mbs}_s{args.seq}.csv")
+    os.environ["SMP_TUNABLEOP_FILE"] = tfile
+    tmode = bench.setup_tunableop(argparse.Namespace(tunableop=args.tunableop))
     smp.init({"bf16": True, "ddp": False})
     base, ov = shard_overrides(args.shard, args.seq)
     if args.layers:
@@ -109,11 +117,26 @@ def main():
         opt.step()
         return out
 
+    if tmode == "tune":  # tuning steps can run for minutes: keep printing
+        import threading
+
+        t_start = time.time()
+        done = threading.Event()
+
+        def beat():
+            while not done.wait(30):
+                print(f"tunableop: tuning in progress, {time.time() - t_start:.0f} s", flush=True)
+
+        threading.Thread(target=beat, daemon=True).start()
     for i in range(args.warmup):
         out = one()
         print(f"warmup {i}: loss {float(out.reduce_mean()):.4f}", flush=True)
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     sync()
+    if tmode == "tune":
+        done.set()
+        torch.cuda.tunable.tuning_enable(False)
+        bench.write_tunableop_results(tfile)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = one()
@@ -130,7 +153,7 @@ def main():
            "samples_per_s": round(args.mbs / ms * 1e3, 3),
            "model_tflops_shard": round(flops_tok * tokens / ms / 1e9, 1),
            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 1e9, 2) if torch.cuda.is_available() else None,
-           "final_loss": round(float(out.reduce_mean()), 4),
+           "final_loss": round(float(out.reduce_mean()), 4), "gemm_selection": tmode,
            "comm_estimate": comm_estimate(h, tokens, c["num_layers"], SHARDS[args.shard]["tp"])}
     print("SHARD " + json.dumps(rec), flush=True)
 
