@@ -314,10 +314,8 @@ __global__ void __launch_bounds__(256) ln_bwd_wide(const T* __restrict__ dy, con
   // a ring of two register rows (VB <= 4: the second set fits beside the dgamma / dbeta
   // accumulators): the next row's x / dy / dres loads are in flight while this row reduces,
   // crosses its barrier and writes dx -- one row at a time left each block waiting on HBM
-#ifndef SMPK_LN_WIDE_RING
-#define SMPK_LN_WIDE_RING 1
-#endif
-  constexpr bool RING = SMPK_LN_WIDE_RING && VB <= 4;
+  // (A/B against one row at a time: profiles/r5/shards_r5.md)
+  constexpr bool RING = VB <= 4;
   constexpr int VR = RING ? VB : 1;
   Vec16<T> xa[VB], da[VB], ra[VB], xn[VR], dn[VR], rn[VR];
   auto load_row = [&](int64_t row, Vec16<T>* xx, Vec16<T>* dd, Vec16<T>* rr) {
