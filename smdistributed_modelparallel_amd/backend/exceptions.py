@@ -28,6 +28,11 @@ class SMPConfigError(SMPValidationError):
     pass
 
 
+class DistTransformerConfigError(SMPInvalidArgumentError):
+    """An smp.nn transformer module was given an unsupported combination of options
+    (reference `torch/exceptions.py:53`)."""
+
+
 class InvalidEnvironmentError(SMPValidationError):
     pass
 

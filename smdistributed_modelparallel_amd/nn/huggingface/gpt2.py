@@ -62,11 +62,19 @@ def _attention_flags(config):
     """Score scaling / precision fields of the HF GPT-2 config (reference
     `torch/nn/huggingface/gpt2.py:75-78`): ``scale_attn_weights`` -> divide scores by
     sqrt(d); ``reorder_and_upcast_attn`` -> layer-idx query/key scaling with the scores and
-    softmax in fp32."""
+    softmax in fp32.
+
+    One deliberate difference: with ``scale_attn_by_inverse_layer_idx`` as well, HF divides the
+    upcast scores by layer_idx + 1, while the reference's query_key_layer_scaling multiplies that
+    factor back inside the softmax (no net layer scaling, `torch/nn/transformer.py:1324-1329`) --
+    the reference translation silently changes such a model.  There the upcast maps to
+    ``attention_in_fp32`` alone, which keeps HF's numerics (the flash kernel's scores are fp32
+    anyway)."""
     upcast = bool(getattr(config, "reorder_and_upcast_attn", False))
+    by_layer = bool(getattr(config, "scale_attn_by_inverse_layer_idx", False))
     return {
         "scale_attention_scores": bool(getattr(config, "scale_attn_weights", True)),
-        "query_key_layer_scaling": upcast,
+        "query_key_layer_scaling": upcast and not by_layer,
         "attention_in_fp32": upcast,
     }
 

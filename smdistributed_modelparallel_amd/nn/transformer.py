@@ -31,7 +31,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..backend.exceptions import SMPInvalidArgumentError
+from ..backend.exceptions import DistTransformerConfigError, SMPInvalidArgumentError
 from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
 from ..ops.attention import attention_packed
@@ -44,7 +44,7 @@ from ..ops import lm_head as lm_head_op
 from ..ops.linear import linear
 from ..ops.rope import apply_rotary, apply_rotary_qkv
 from ..torch.state_mod import state
-from .layer_norm import DistributedLayerNorm, FusedLayerNorm
+from .layer_norm import DistributedLayerNorm, FusedLayerNorm, MixedFusedLayerNorm
 from .utils import (
     allgather_for_tp,
     bwd_allreduce_for_tp,
@@ -188,8 +188,30 @@ class _Dropout(nn.Module):
         return _dropout_add(x, None, self.p, True)
 
     def add(self, x, residual):
-        """residual + dropout(x) in one pass."""
+        """residual + dropout(x) in one pass; an fp32 residual stream (fp32_residual_addition)
+        takes the low-precision branch by type promotion."""
+        if residual.dtype != x.dtype:
+            return residual + self(x)
         return _dropout_add(x, residual, self.p, self.training)
+
+
+def _layer_norm_cls(mem, fp32_residual):
+    """LayerNorm of a sub-layer: hidden-sharded under optimize="memory"; with
+    ``fp32_residual_addition`` the mixed-dtype kernel (fp32 residual stream in, parameter dtype
+    out, K10 -- reference `torch/nn/transformer.py:755,1029,1315` MixedLayerNorm)."""
+    if mem:
+        return DistributedLayerNorm
+    return MixedFusedLayerNorm if fp32_residual else FusedLayerNorm
+
+
+def _check_fp32_residual(module, has_pre_ln):
+    """Reference `torch/nn/transformer.py:356-364,1059-1073,1375-1389`."""
+    if not module.fp32_residual_addition:
+        return
+    if module._mem or (state.initialized and state.cfg.optimize == "memory"):
+        raise DistTransformerConfigError("fp32 residual addition only supports optimize == speed.")
+    if not has_pre_ln:
+        raise DistTransformerConfigError("fp32 residual addition requires pre-layernorm to be true.")
 
 
 def _all_ones(attention_mask):
@@ -306,7 +328,8 @@ class DistributedAttentionLayer(DistributedModule):
         self.register_parameter(
             "dense_bias",
             nn.Parameter(torch.zeros(h, dtype=dtype)) if (self.use_attn_dense_bias and tp_rank() == 0) else None)
-        LN = DistributedLayerNorm if self._mem else FusedLayerNorm
+        _check_fp32_residual(self, self.pre_layernorm)
+        LN = _layer_norm_cls(self._mem, self.fp32_residual_addition)
         if self.pre_layernorm:
             self.pre_layernorm_module = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:
@@ -348,8 +371,14 @@ class DistributedAttentionLayer(DistributedModule):
 
     # ------------------------------------------------------------------ core
     def _scale(self):
+        """Softmax scale.  ``scale_attn_by_layer_idx`` divides the scores by layer_idx + 1; with
+        ``query_key_layer_scaling`` as well, the reference divides Q K^T by (layer_idx + 1) only to
+        keep the low-precision GEMM from overflowing and multiplies the factor back inside its
+        fp32 softmax (`torch/nn/transformer.py:1324-1329,1754-1766,1800-1806`), so the net scale
+        has no layer factor.  The flash kernel keeps scores in fp32, so it applies the net scale
+        directly."""
         s = 1.0 / math.sqrt(self.attention_head_size) if self.scale_attention_scores else 1.0
-        if self.scale_attn_by_layer_idx:
+        if self.scale_attn_by_layer_idx and not self.query_key_layer_scaling:
             s = s / float(self.layer_idx + 1)
         return s
 
@@ -503,9 +532,11 @@ class DistributedTransformerOutputLayer(DistributedModule):
                                        "fused_bias_gelu", "_precision_test")]
     )
 
-    def __init__(self, *args, **kwargs):
+    def __init__(self, *args, _single_pre=False, **kwargs):
         super().__init__()
         parse_args(self, args, kwargs, self._KEYS)
+        # _single_pre: the enclosing layer's single_pre_layernorm feeds this MLP
+        _check_fp32_residual(self, self.pre_layernorm or _single_pre)
         self._tanh_gelu = bool(self.fused_bias_gelu) or os.environ.get("SMP_USE_HF_GELU") == "1"
         self.local_inter = get_local_channels(self.intermediate_size)
         h, li = self.hidden_size, self.local_inter
@@ -520,7 +551,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
             self.dense1_bias = nn.Parameter(torch.zeros(li, dtype=dtype))
         self.dense2_weight = nn.Parameter(torch.empty(h, li, dtype=dtype))
         self.register_parameter("dense2_bias", nn.Parameter(torch.zeros(h, dtype=dtype)) if tp_rank() == 0 else None)
-        LN = DistributedLayerNorm if self._mem else FusedLayerNorm
+        LN = _layer_norm_cls(self._mem, self.fp32_residual_addition)
         if self.pre_layernorm:
             self.pre_layernorm_module = LN(h, eps=self.layernorm_epsilon, dtype=dtype)
         if self.post_layernorm:
@@ -634,7 +665,7 @@ class DistributedTransformerLayer(DistributedModule):
         if self.add_cross_attention:
             cross_cfg = dict(attn_cfg, cross_attention=True, causal_mask_size=None, rotary_dim=None)
             self.cross_attention = DistributedAttentionLayer(layer_idx=layer_idx, **cross_cfg)
-        self.output = DistributedTransformerOutputLayer(**out_cfg)
+        self.output = DistributedTransformerOutputLayer(_single_pre=bool(self.single_pre_layernorm), **out_cfg)
         self.input_layer = True
         self.output_layer = True
         self._defer_ok = False  # the next layer is on this stage and can take a deferred residual
@@ -643,8 +674,8 @@ class DistributedTransformerLayer(DistributedModule):
         """This layer can hand its MLP residual add to the next layer (and take one)."""
         at, out = self.attention, self.output
         return (not self.parallel_attn_output and not self.add_cross_attention and not out.post_layernorm
-                and not at.post_layernorm and at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_add")
-                and not self._mem)
+                and not self.fp32_residual_addition and not at.post_layernorm and at.pre_layernorm
+                and hasattr(at.pre_layernorm_module, "forward_add") and not self._mem)
 
     def _defers(self):
         return self._defer_ok and _FUSE_CROSS_LAYER[0] and not self.output_layer and not _checkpointing_anywhere()
@@ -657,6 +688,12 @@ class DistributedTransformerLayer(DistributedModule):
         if self._tp > 1 and self.input_layer and not _prescaled():
             hidden = _enter_tp(hidden, self._mem, self.hidden_size)
             mask = _gather_mask(mask)
+        if self.fp32_residual_addition:
+            # fp32 residual stream from the first transformer layer on (reference
+            # `torch/nn/transformer.py:890-894`; a no-op on the later layers and stages, which
+            # receive it in fp32): the mixed LayerNorms hand the branches the parameter dtype,
+            # the residual adds promote back to fp32
+            hidden = hidden.float()
         at, out = self.attention, self.output
         if self.parallel_attn_output:
             fuse = os.environ.get("SMP_FUSE_PARALLEL_RESIDUAL", "1") != "0"
@@ -691,7 +728,8 @@ class DistributedTransformerLayer(DistributedModule):
             if at.post_layernorm:
                 hidden = at.layernorm(at.dropout.add(attn, hidden))
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
-            elif out.pre_layernorm and hasattr(out.pre_layernorm_module, "forward_add"):
+            elif (out.pre_layernorm and hasattr(out.pre_layernorm_module, "forward_add")
+                  and attn.dtype == hidden.dtype):
                 # fused: attention-branch dropout + residual add + LayerNorm in one HIP kernel
                 m, hidden = out.pre_layernorm_module.forward_add(attn, hidden, at.dropout.active_p())
             else:
@@ -798,6 +836,14 @@ class DistributedTransformerLMHead(DistributedModule):
         if self.distribute_embedding and self.parallel_attn_output:
             warnings.warn("distribute_embedding is not supported with parallel_attn_output; disabling it")
             self.distribute_embedding = False
+        if self.distribute_embedding:
+            # reference `torch/nn/transformer.py:344-354`: suggested together, enabled unless given
+            for key in ("fp32_residual_addition", "scale_attn_by_layer_idx"):
+                if key not in kwargs:
+                    logger.warning(f"{key} is suggested when distribute_embedding is enabled. Enabling {key}.")
+                    setattr(self, key, True)
+                    cfg[key] = True
+        _check_fp32_residual(self, self.pre_layernorm or self.single_pre_layernorm)
         dtype = _param_dtype()
         h = self.hidden_size
         if self.distribute_embedding:
@@ -829,7 +875,9 @@ class DistributedTransformerLMHead(DistributedModule):
         tcfg["_output_full_batch"] = self.distribute_embedding
         self.transformer = DistributedTransformer(**tcfg)
         if self.final_layernorm:
-            self.layernorm = FusedLayerNorm(h, eps=self.layernorm_epsilon, dtype=dtype)
+            # fp32 residual stream: the final LN hands the head the parameter dtype
+            self.layernorm = _layer_norm_cls(False, self.fp32_residual_addition)(h, eps=self.layernorm_epsilon,
+                                                                                 dtype=dtype)
             if self.distribute_embedding and self._tp > 1:
                 # applied to the full TP-group batch, with the TP-scaled CE gradient: averaged
                 # over the TP group like the tensor-parallel weights (scaled-batch divisor)
@@ -886,6 +934,8 @@ class DistributedTransformerLMHead(DistributedModule):
             (hidden,) = shard_sequence(hidden, shift=-1)
         if self.final_layernorm:
             hidden = self.layernorm(hidden)
+        elif self.fp32_residual_addition:
+            hidden = hidden.to(self.word_embedding.weight.dtype)
 
         if self.distribute_embedding:
             hidden = (bwd_allreduce_for_tp(hidden) if self._tp > 1 else hidden)

@@ -136,9 +136,11 @@ def mixed_layer_norm(x, weight, bias, eps=1e-5):
     """LayerNorm whose output takes the affine parameters' dtype (input any dtype)."""
     if x.is_cuda and weight is not None and bias is not None:
         return _MixedLayerNorm.apply(x, weight, bias, eps)
-    y = torch.nn.functional.layer_norm(x.to(weight.dtype) if weight is not None else x, (x.shape[-1],), weight, bias,
-                                       eps)
-    return y.to(weight.dtype) if weight is not None else y
+    # statistics and affine in fp32 from the unrounded input, one rounding into the parameters' dtype
+    w = weight.float() if weight is not None else None
+    b = bias.float() if bias is not None else None
+    y = torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w, b, eps)
+    return y.to(weight.dtype) if weight is not None else y.to(x.dtype)
 
 
 def layer_norm(x, weight, bias, eps=1e-5):

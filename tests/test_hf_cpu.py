@@ -92,7 +92,10 @@ def test_gpt2_attention_config_flags_parity(scale_attn_weights, reorder_and_upca
                      scale_attn_by_inverse_layer_idx=by_layer)
     kw = gpt2.config_to_kwargs(cfg)
     assert kw["scale_attention_scores"] == scale_attn_weights
-    assert kw["attention_in_fp32"] == kw["query_key_layer_scaling"] == reorder_and_upcast_attn
+    assert kw["attention_in_fp32"] == reorder_and_upcast_attn
+    # query-key layer scaling cancels the layer-index division (reference semantics): only
+    # translated where HF does not divide by the layer index
+    assert kw["query_key_layer_scaling"] == (reorder_and_upcast_attn and not by_layer)
     _lm_parity(GPT2LMHeadModel(cfg), gpt2, 97)
 
 
