@@ -181,6 +181,29 @@ def _lm_head_padded():
     return bool(lm_head._ENABLED)
 
 
+def device_record(smp, dev):
+    """Every rank's (hostname, device index, GPU UUID): the record proves one rank per physical
+    GPU.  Unless SMP_DEVICE_INDEX pins ranks on purpose (one-GPU rehearsals), two ranks of one
+    host on the same GPU abort the bench."""
+    import socket
+
+    me = [socket.gethostname(), None, None]
+    if dev.type == "cuda":
+        me[1] = dev.index if dev.index is not None else torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(me[1])
+        me[2] = str(getattr(props, "uuid", "")) or getattr(props, "pci_bus_id", None)
+    allr = smp.allgather(me, smp.WORLD) if smp.size() > 1 else [me]
+    if dev.type == "cuda" and not os.environ.get("SMP_DEVICE_INDEX"):
+        seen = {}
+        for r, (host, idx, uuid) in enumerate(allr):
+            key = (host, uuid or idx)
+            if key in seen:
+                raise RuntimeError(f"ranks {seen[key]} and {r} share GPU {idx} ({uuid}) on {host}: the bench needs one "
+                                   "rank per GPU")
+            seen[key] = r
+    return [{"rank": r, "device": idx, "uuid": uuid} for r, (host, idx, uuid) in enumerate(allr)]
+
+
 def main():
     args = parse()
     import smdistributed_modelparallel_amd.torch as smp
@@ -209,6 +232,9 @@ def main():
     split = None
     if args.pp > 1:
         cfg["pipeline"] = "interleaved"
+        # the step's module graph is identical every step: freeze and replay its schedule
+        # (engine record-and-replay; the dynamic scheduler is the default otherwise)
+        cfg["static_mode"] = True
         if os.environ.get("SMP_BENCH_AUTO_PARTITION", "0") == "1":
             cfg["auto_partition"] = True
         else:
@@ -247,6 +273,7 @@ def main():
         return loss
 
     dev = smp.state.device  # the device smp.init bound this rank to
+    devices = device_record(smp, dev)
     batch = args.mbs * args.microbatches
     g = torch.Generator(device=dev)
     g.manual_seed(42 + smp.rank())
@@ -359,6 +386,7 @@ def main():
                        for name, g in (("world", smp.state.pgs.world), ("dp", smp.state.pgs.dp),
                                        ("pp", smp.state.pgs.pp), ("tp", smp.state.pgs.tp))},
             "p2p": p2p_record(smp, args),
+            "devices": devices,
             # per-step compute-stream stall on communication (max over ranks): the DP bucket
             # all-reduces left after backward, pipeline activation / gradient pulls, and the
             # tensor-parallel collectives (the asynchronous dX all-reduce: its final wait only)

@@ -39,7 +39,9 @@ How it is built here (our design, not the reference's):
   TP peers, and from then on all ranks of the model-parallel group replay it: no decision
   messages, no dynamic choices (reference `server_queue.py:224-626`, record window 5 steps
   `:245`, best step `:575-626`).  All stages replay the SAME recorded step, so the replayed
-  orders are one feasible global execution.  ``static_mode`` turns this on without TP.
+  orders are one feasible global execution.  It runs for TP > 1, ``static_mode``,
+  ``fast_mode`` and activation offloading (``SMP_REPLAY=1`` opts other pipelines in); a
+  replayed step whose events differ from the frozen ones raises instead of waiting.
   With the IPC transport a tensor is pulled the moment its control message is dispatched,
   so the reference's pre-registered receptions (`:488`) have nothing left to pre-post.
 * **Fast mode** (``fast_mode``; reference `torch/serialization.py:365-473`, `step.py:150-230`,
@@ -57,7 +59,7 @@ How it is built here (our design, not the reference's):
 """
 import os
 import time
-from collections import deque
+from collections import Counter, deque
 import itertools
 
 import torch
@@ -364,20 +366,21 @@ class PipelineEngine:
 
     # ------------------------------------------------------- record / replay
     def replay_enabled(self):
-        """Record-and-replay is the default for every pipeline with repeated steps (SURVEY
-        §7.1.6).  It is FORCED -- ``SMP_REPLAY=0`` does not turn it off -- where the reference
-        forces its DeterministicServerQueue (`torch/server.py:57-65`): TP > 1 (collective
-        order), ``static_mode``, ``fast_mode`` and ``offload_activations`` (the task-level
-        activation prefetch needs the frozen order).  ``SMP_REPLAY=0`` keeps the dynamic
-        scheduler for the other pipelines; SMP_NONDETERMINISTIC_TP_ORDER=1 (tests) disables
-        both."""
+        """Record-and-replay runs where the reference forces its DeterministicServerQueue
+        (`torch/server.py:57-65`): TP > 1 (collective order), ``static_mode``, ``fast_mode`` and
+        ``offload_activations`` (the task-level activation prefetch needs the frozen order).
+        Every other pipeline keeps the dynamic scheduler -- its module graph may change from
+        step to step (static_mode=False is the default) -- unless ``SMP_REPLAY=1`` opts in.
+        SMP_NONDETERMINISTIC_TP_ORDER=1 (tests) disables both.  A replayed step whose events
+        differ from the frozen schedule raises (``_serve_follower``) instead of waiting
+        forever."""
         core = self.core
         if core.pp_size() <= 1 or os.environ.get("SMP_NONDETERMINISTIC_TP_ORDER", "0") == "1":
             return False
         cfg = self.state.cfg
         forced = (core.tp_size() > 1 or bool(cfg.static_mode) or bool(cfg.fast_mode)
                   or bool(cfg.offload_activations))
-        return forced or os.environ.get("SMP_REPLAY", "1") != "0"
+        return forced or os.environ.get("SMP_REPLAY", "0") == "1"
 
     def after_step(self, step_fn, seconds):
         """Called on every rank after every pipelined step (symmetric collectives)."""
@@ -506,8 +509,12 @@ class PipelineEngine:
         pending = {}
         pos = 0  # index of decisions[0] in the replayed schedule
         step = self.state.step_count
+        owed = None  # replay: how many times each key is still expected this step
         if replay is not None:
             decisions = deque(replay)
+            owed = Counter(replay)
+            stall_s = float(os.environ.get("SMP_REPLAY_STALL_TIMEOUT_S", "600"))
+            last = time.monotonic()
         else:
             stash = getattr(self, "_dec_stash", deque())
             decisions = deque(k for st, k in stash if st == step)
@@ -525,13 +532,25 @@ class PipelineEngine:
                 elif stubbed[0] == "abort":
                     self._dispatch(src, stubbed, tensors)
                 else:
-                    pending[self._event_key(src, stubbed)] = m
+                    key = self._event_key(src, stubbed)
+                    if owed is not None and owed[key] <= sum(1 for k in pending if k == key):
+                        self._replay_mismatch(f"event {key} from rank {src} is not in the frozen schedule", decisions)
+                    pending[key] = m
                 m = self.state.transport.poll(0.0)
             if replay_mbs is not None:
                 self._lookahead_prefetch(replay, replay_mbs, pos)
+            pos0 = pos
             while decisions and not self._stop:
                 key = decisions[0]
                 pos += 1
+                if owed is not None and not (key[0] in ("act", "lres") or key in pending):
+                    pos -= 1
+                    break  # the decided message has not arrived yet
+                if owed is not None:
+                    owed[key] -= 1
+                    if key[:2] == ("act", "bwd") and ("bwd_start", key[2]) not in self.waiting:
+                        self._replay_mismatch(f"microbatch {key[2]}'s forward has not finished where the frozen "
+                                              "schedule starts its backward", decisions)
                 if key[0] == "act":
                     decisions.popleft()
                     self._do_action(key[1:])
@@ -548,8 +567,25 @@ class PipelineEngine:
                 else:
                     pos -= 1
                     break  # the decided message has not arrived yet
+            if owed is not None and not self._stop:
+                now = time.monotonic()
+                if pos != pos0:
+                    last = now
+                elif not decisions and not (leader and self.pipeline.is_done()):
+                    self._replay_mismatch("the frozen schedule is exhausted but the step has not finished", decisions)
+                elif now - last > stall_s:
+                    self._replay_mismatch(f"no event of the frozen schedule arrived for {stall_s:.0f} s "
+                                          f"(SMP_REPLAY_STALL_TIMEOUT_S)", decisions)
             if leader and self.pipeline.is_done() and not decisions:
                 self._stop = True
+
+    def _replay_mismatch(self, what, decisions):
+        nxt = list(decisions)[:3]
+        raise SMPRuntimeError(
+            f"rank {self.core.rank()} step {self.state.step_count}: {what}; next expected events {nxt}.  The "
+            "module graph changed after the pipeline schedule was frozen (record-and-replay runs for TP > 1, "
+            "static_mode, fast_mode and offload_activations, or SMP_REPLAY=1): keep the per-step module calls "
+            "identical, or run without those options / with SMP_REPLAY=0.")
 
     # ------------------------------------------------- activation prefetching
     def _offloader(self):

@@ -52,6 +52,8 @@ def _check_audit_fields(rec, world, dp, pp):
     assert rec["dist_backend"] == ("gloo" if world > 1 else rec["dist_backend"])
     assert rec["groups"]["world"] == world and rec["groups"]["dp"] == dp and rec["groups"]["pp"] == pp
     assert {"mode", "ipc_selfcheck"} <= set(rec["p2p"])
+    # one entry per rank (device index / GPU UUID on GPU boxes; distinct devices are asserted there)
+    assert [d["rank"] for d in rec["devices"]] == list(range(world))
     ex = rec["exposed_comm_ms"]
     assert set(ex) == {"dp", "p2p", "tp"} and all(v >= 0.0 for v in ex.values())
     if dp > 1:

@@ -234,10 +234,22 @@ def test_pp2_offload_alone_forces_replay_and_task_prefetch():
          env={"SMP_REPLAY_RECORD_STEPS": "2", "SMP_REPLAY": "0"})
 
 
-def test_pp2_default_replays_repeated_steps():
-    """A plain pipeline (no TP, no static / fast mode, no offload) records and replays by
-    default; results still match the unpartitioned model."""
-    _run(2, 2, 1, 3, steps=4, extra={"expect_replay": True}, env={"SMP_REPLAY_RECORD_STEPS": "2"})
+def test_pp2_replay_opt_in_repeated_steps():
+    """A plain pipeline (no TP, no static / fast mode, no offload) keeps the dynamic scheduler
+    unless SMP_REPLAY=1 opts into record-and-replay (reference `torch/server.py:57-65`); results
+    match the unpartitioned model either way."""
+    _run(2, 2, 1, 3, steps=4, extra={"expect_replay": True}, env={"SMP_REPLAY_RECORD_STEPS": "2", "SMP_REPLAY": "1"})
+
+
+@pytest.mark.parametrize("mode", ["dynamic", "static"])
+def test_pp2_step_varying_graph(mode):
+    """A module graph that changes from step to step: the default dynamic schedule
+    runs it past the record window and matches the unpartitioned model; under static_mode's
+    forced replay the changed step raises a clear mismatch error on both ranks, no hang."""
+    outs = run_workers("varying_graph", 2, [mode], timeout=120, env_extra={"SMP_REPLAY_RECORD_STEPS": "2"})
+    assert all("OK" in o for o in outs)
+    if mode == "static":
+        assert all("frozen schedule" in o for o in outs)
 
 
 def test_sharded_dp_fp16_overflow_skips_on_every_rank():
