@@ -44,8 +44,13 @@ namespace smprt_torch {
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 128;
-constexpr int kThreads = 256;
+// One wave per workgroup and at most 64 workgroups (a quarter of the CUs): the spinning waits
+// of a call hold no LDS and few wave slots, so they never keep a full-LDS GEMM workgroup off
+// the CUs they sit on (with 128 x 256-thread workgroups each taking an LDS
+// word, a TP rank's spinning one-shot kernel could starve a co-resident rank's GEMM when the
+// ranks share a GPU).
+constexpr int kMaxBlocks = 64;
+constexpr int kThreads = 64;
 constexpr int kAbortWord = kMaxRanks * kMaxBlocks;  // index of the abort word in a flag array
 constexpr int kFlagWords = kAbortWord + 64;          // the abort word on a line of its own
 
@@ -88,8 +93,6 @@ __global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(ArParams p)
   const int64_t hi = lo + p.chunk < p.n ? lo + p.chunk : p.n;
   constexpr int V = 16 / sizeof(T);  // elements per 16-byte vector
   const int64_t vlo = lo / V, vhi = hi / V;  // lo is a multiple of 8 >= V
-  __shared__ int s_fail;
-  if (tid == 0) s_fail = 0;
   // 1. input chunk -> own slot
   {
     const uint4* src = static_cast<const uint4*>(p.in);
@@ -99,19 +102,20 @@ __global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(ArParams p)
     T* d1 = reinterpret_cast<T*>(const_cast<char*>(p.slot[p.rank]));
     for (int64_t i = vhi * V + tid; i < hi; i += kThreads) d1[i] = s1[i];
   }
-  // 2. publish: every thread's stores visible at system scope, then push the epoch
+  // 2. publish: the wave's stores visible at system scope (one wave: the fence orders all of
+  // them before the pushes), then push the epoch
   __threadfence_system();
-  __syncthreads();
   if (tid < p.world && tid != p.rank) {
     __hip_atomic_store(p.peer_flags[tid] + p.rank * kMaxBlocks + b, p.epoch, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. wait for every peer's chunk (bounded; a peer's abort ends the wait too)
+  bool fail = false;
   if (tid < p.world && tid != p.rank) {
     const uint32_t* f = p.my_flags + tid * kMaxBlocks + b;
     const uint32_t* ab = p.my_flags + kAbortWord;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    bool fail = __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    fail = __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     while (!fail &&
            static_cast<int32_t>(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - p.epoch) < 0) {
       if (__hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
@@ -125,14 +129,12 @@ __global__ void __launch_bounds__(kThreads) oneshot_allreduce_kernel(ArParams p)
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    if (fail) {
-      __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      s_fail = 1;
-    }
+    if (fail) __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __syncthreads();
+  // the polling lanes' verdict reaches the whole wave by a vote (no LDS)
+  const bool any_fail = __any(fail);
   __atomic_thread_fence(__ATOMIC_ACQUIRE);  // (system-scope acquire by the polling lanes above)
-  if (s_fail) {  // never reduce stale slots: the output is poisoned, the host raises at step end
+  if (any_fail) {  // never reduce stale slots: the output is poisoned, the host raises at step end
     T* out = static_cast<T*>(p.out);
     const T nan = from_f<T>(__builtin_nanf(""));
     for (int64_t i = lo + tid; i < hi; i += kThreads) out[i] = nan;

@@ -168,7 +168,7 @@ def lm_return_hook(out):
 
 
 def encoder_forward_hook(hidden_states, attention_mask=None, encoder_hidden_states=None, encoder_attention_mask=None,
-                         past_key_values=None, use_cache=None, head_mask=None, output_attentions=False,
+                         past_key_values=None, use_cache=None, *, head_mask=None, output_attentions=False,
                          output_hidden_states=False, return_dict=None, error=None, family="encoder", **kwargs):
     """HF ``BertEncoder`` / ``RobertaEncoder`` call -> the DistributedTransformer input tuple:
     (hidden, mask) or, with encoder states for the cross-attention layers, (hidden, mask,
@@ -176,7 +176,13 @@ def encoder_forward_hook(hidden_states, attention_mask=None, encoder_hidden_stat
     refused instead of silently ignored, as the reference's hooks do
     (`nn/huggingface/bert.py:111-160`, `roberta.py:111-160`).  Pass-through kwargs of
     transformers 5.x (``position_ids``, ``cache_position``) are ignored: absolute positions
-    live in the embeddings, outside the encoder."""
+    live in the embeddings, outside the encoder.
+
+    The positional order is that of the installed transformers 5.x ``BertEncoder.forward``
+    (hidden_states, attention_mask, encoder_hidden_states, encoder_attention_mask,
+    past_key_values, use_cache); the 4.x-only arguments (head_mask, output_*, return_dict) are
+    keyword-only, so a 4.x-style positional head_mask cannot land in encoder_hidden_states
+    (the reference's hook, `nn/huggingface/bert.py:107-118`, has the 4.x order)."""
     from ...backend.exceptions import HFConfigError
 
     err = error or HFConfigError

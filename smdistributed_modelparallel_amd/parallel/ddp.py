@@ -34,7 +34,6 @@ from .comm_timer import timer as comm_timer
 logger = get_logger()
 
 
-
 def probe_premul_sum(group, dtype, device, group_size):
     """Whether RCCL's pre-multiplied sum gives the right average for this dtype on this group:
     one 8-element all-reduce, the same on every rank (so every rank reaches the same verdict),
@@ -71,6 +70,12 @@ class BucketReducer:
         self.group_rank = dist.get_rank(group) if (group is not None and dist.is_initialized()) else 0
         if overlap or flat.fp32_accumulation:
             self._install_hooks()
+        if group is not None and group_size > 1:
+            # the pre-multiplied-sum probe is a collective: run it here, at the same point of
+            # every rank's collective order (construction), not lazily inside the first bucket
+            # launch -- a rank that joins before its first backward would otherwise probe at a
+            # different position than the training ranks
+            self._premul_ok()
 
     # ------------------------------------------------------------------ hooks
     def _install_hooks(self):
@@ -154,6 +159,7 @@ class BucketReducer:
             b.work = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
     def _premul_ok(self):
+        """Whether this reducer averages inside RCCL (decided once, at construction)."""
         ok = getattr(self, "_premul", None)
         if ok is None:
             ok = (hasattr(dist, "_make_nccl_premul_sum") and self.flat.grad.is_cuda
@@ -161,7 +167,6 @@ class BucketReducer:
                   and probe_premul_sum(self.group, self.flat.grad.dtype, self.flat.grad.device, self.group_size))
             self._premul = ok
         return ok
-
 
     # ------------------------------------------------------------------ step
     def prepare_for_backward(self):

@@ -23,11 +23,11 @@ Failures after set-up are never silent: a kernel that waits longer than
 ``SMP_ONESHOT_ALLREDUCE_TIMEOUT_S`` (default 600 s, the RCCL process-group timeout) for a
 peer -- a rank skipped a call, died, or drifted away -- writes NaN instead of reducing stale
 slots, raises the instance's host-mapped error word and pushes an abort into every peer's
-flag array, so the peers' kernels fail too.  ``check_errors()`` (called by
-``DistributedModel`` at the end of every step: reads the error words behind the previous
-step's end event, then the TP ranks agree on the verdict) raises ``OneShotAllReduceError`` on
-every rank of the group in the same step, and the failed instance refuses all later calls;
-checkpoint saves check with a full synchronisation first.
+flag array, so the peers' kernels fail too.  At the end of every step ``DistributedModel``
+reads the error words behind the previous step's end event (``poll_failures``) and sends the
+verdict with its end-of-step model-parallel barrier, so every rank raises
+``OneShotAllReduceError`` in the same step; the failed instance refuses all later calls.
+Checkpoint saves check with a full synchronisation first (``check_errors(sync=True)``).
 """
 import os
 import socket
@@ -191,23 +191,18 @@ def all_reduce(x, op=dist.ReduceOp.SUM, group=None, async_op=False):
 _pending = []  # [event recorded at the end of the previous checked step]
 
 
-def check_errors(group=None, sync=False):
-    """Raise ``OneShotAllReduceError`` if a one-shot all-reduce of any group failed (own
-    timeout, or a peer's abort) -- on every rank of `group` (the TP group's gloo twin) in the
-    SAME step: the ranks agree on the verdict (a MAX over `group`), so a peer whose poisoned
-    kernel was still running cannot pass the check alone.
+def poll_failures(sync=False):
+    """This rank's verdict, no communication: True if a one-shot all-reduce of any of its
+    groups failed (own timeout, or a peer's abort).
 
     No full stream synchronisation per step: the error words are read after
     the event recorded at the end of the PREVIOUS checked step -- a step whose kernels have
     normally finished long ago, so the host does not stall and keeps at most one step of
-    run-ahead -- and a fresh event is recorded for the next check.  A failure is therefore
-    raised at the end of the step in which it happened or of the next one, on every rank of
-    the group at once.  ``sync=True`` (checkpoint saves, teardown) waits for the current
-    stream first, so nothing unchecked is persisted.  Costs one 4-byte gloo all-reduce per
-    step, only while one-shot instances exist.  The failed instance stays disabled."""
+    run-ahead -- and a fresh event is recorded for the next check.  ``sync=True`` (checkpoint
+    saves, teardown) waits for the current stream first."""
     active = [(k, inst) for k, inst in _instances.items() if inst is not None]
     if not active and not _failed:
-        return
+        return False
     if torch.cuda.is_available():
         if sync:
             torch.cuda.current_stream().synchronize()
@@ -219,16 +214,48 @@ def check_errors(group=None, sync=False):
     for k, inst in active:
         if k in _failed or inst.error(False):
             _failed.add(k)
-    failed = bool(_failed)
+    return bool(_failed)
+
+
+def active():
+    """Whether one-shot instances (or failures) exist on this rank.  All ranks of one TP group
+    agree (instances are created collectively)."""
+    return bool(_failed) or any(inst is not None for inst in _instances.values())
+
+
+def raise_if_failed(any_failed):
+    """Raise ``OneShotAllReduceError`` on every rank once the ranks agreed that one failed.
+
+    The failure of step N is seen at the end of step N or N + 1 (the check reads the error words
+    behind the previous step's event): by then the optimizer update of step N has run on the
+    NaN-poisoned outputs, so the in-memory parameters and optimizer state are corrupt.  Saved
+    checkpoints are not (saves check with a full synchronisation first): recover by resuming
+    from the last checkpoint."""
+    if any_failed and not _failed:
+        _failed.add("peer")
+    if any_failed:
+        raise OneShotAllReduceError(
+            f"one-shot all-reduce failed on {len(_failed)} TP group(s): a kernel timed out waiting for a peer rank (or "
+            "a peer aborted) and its outputs were poisoned with NaN.  The optimizer update of the failing step may "
+            "already have applied them: the in-memory model and optimizer state must not be used further -- resume "
+            "from the last checkpoint (checkpoint saves verify the one-shot state before writing)")
+
+
+def check_errors(group=None, sync=False):
+    """Raise ``OneShotAllReduceError`` if a one-shot all-reduce of any group failed -- on every
+    rank of `group` (the TP group's gloo twin) in the SAME call: the ranks agree on the verdict
+    (a MAX over `group`), so a peer whose poisoned kernel was still running cannot pass the
+    check alone.  Used where no other rendezvous is at hand (checkpoint saves, with
+    ``sync=True``); the training step folds the verdict into its end-of-step barrier instead
+    (``DistributedModel._step``: one model-parallel allgather, no separate all-reduce)."""
+    if not active():
+        return
+    failed = poll_failures(sync)
     if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
         flag = torch.tensor([1 if failed else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        if int(flag.item()) and not failed:
-            _failed.add("peer")
-            failed = True
-    if failed:
-        raise OneShotAllReduceError(f"one-shot all-reduce failed on {len(_failed)} TP group(s): a kernel timed out "
-                                    f"waiting for a peer rank (or a peer aborted); outputs were poisoned with NaN")
+        failed = bool(flag.item())
+    raise_if_failed(failed)
 
 
 def inject_failure(group=None):

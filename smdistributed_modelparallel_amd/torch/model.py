@@ -484,13 +484,17 @@ class DistributedModel(nn.Module):
             if name not in self._post_step_hooks_run:
                 self._post_step_hooks_run.add(name)
                 hook(self, state.optimizer)
-        # a one-shot TP all-reduce that timed out (or whose peer aborted) poisoned its output:
-        # surface it on every rank of the TP group in this step, before the optimizer update
+        # end-of-step rendezvous, carrying the one-shot TP all-reduce verdict (a kernel that
+        # timed out, or whose peer aborted, poisoned its output): every rank of the model-parallel
+        # group raises in the same step.  Pipelines: one allgather over PP x TP replaces the
+        # stage barrier and the TP agreement; TP alone: over the TP group, only while one-shot
+        # instances exist (all ranks of a TP group agree on that)
         from ..parallel import oneshot
 
-        oneshot.check_errors(state.pgs.cpu_tp if state.pgs is not None else None)
         if state.core.pp_size() > 1:
-            state.comm.barrier(CommGroup.PP_GROUP)
+            oneshot.raise_if_failed(any(state.comm.allgather(oneshot.poll_failures(), CommGroup.MP_GROUP)))
+        elif state.core.tp_size() > 1 and oneshot.active():
+            oneshot.raise_if_failed(any(state.comm.allgather(oneshot.poll_failures(), CommGroup.TP_GROUP)))
 
     # ============================================================ forward/backward
     def forward(self, *args, **kwargs):

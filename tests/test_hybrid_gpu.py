@@ -63,25 +63,29 @@ def test_gptneox20b_width_pp2_tp2_gpu():
     _run(4, 2, 2, 2, extra={"base": "gptneox-20b", "cfg": {"shard_optimizer_state": True}}, env={"SMP_P2P": "ipc"})
 
 
-# Reduced precision (reference `test_gpt_grad.py:121-154`, thresholds `model_zoo/gpt_models.py:51-61`):
-# the smp model (bf16 / fp16 compute, fp32 master weights) against the same architecture run in
-# that dtype without smp, flash attention and the HIP RoPE / LayerNorm / GeLU / CE kernels on both
-# sides.  Parameters: the reference's param_atol 5e-3.  Loss: 3e-2 absolute for bf16 (~0.4 % of
-# a ~7.0 loss = one bf16 rounding unit: TP splits change the rounding of every row-parallel
-# partial sum, where the reference's 1e-8 compares two runs of identical kernels); the
-# reference's fp16 loss_atol 1e-2 for fp16.
-_BF16 = {"dtype": "bf16", "loss_tol": 3e-2, "param_tol": 5e-3, "expect_flash": True}
+# Reduced precision (reference `test_gpt_grad.py:121-154`, thresholds `model_zoo/gpt_models.py:51-61`,
+# gradient comparison `smp_test_base.py:731-788`, batch 8 / seq 512 `gpt_models.py:34-35`): the smp
+# model (bf16 / fp16 compute, fp32 master weights) at seq 256 -- the d = 256 / 96 / 64 flash kernels
+# loop over >= 2 key tiles -- checked three ways:
+# * every local gradient of the first step, before the update, against the same architecture run
+#   unpartitioned in that dtype (flash attention and the HIP RoPE / LayerNorm / GeLU / CE kernels on
+#   both sides), as a relative norm: 1e-2 (bf16), 5e-3 (fp16);
+# * the same gradients against the independent plain-torch fp32 model of tests/torch_ref.py on the
+#   initial weights (no smp module, no HIP kernel): 5e-2 (bf16), 3e-2 (fp16) -- this bound also
+#   contains the reduced-precision rounding of the smp run itself;
+# * loss every step and parameters after 2 SGD steps (as before; the parameter check alone cannot
+#   see a wrong gradient: lr 0.05 x 2 steps puts param_tol 5e-3 at a gradient error of 0.05).
+# test_grad_check_catches_missing_tp_allreduce shows the gradient check fails when the column-
+# parallel input-gradient all-reduce is dropped.
+_BF16 = {"dtype": "bf16", "loss_tol": 3e-2, "param_tol": 5e-3, "expect_flash": True, "seq": 256,
+         "grad_tol": 1e-2, "fp32_ref_tol": 5e-2}
 
 
 def test_gptj6b_width_tp4_bf16_gpu():
-    """GPT-J 6B width (16 heads x 256: the d = 256 flash kernels, rotary 64) at TP=4 in bf16.
-    TP collectives on RCCL's path here, not the one-shot kernel: with four ranks SHARING this one
-    GPU, a rank's spinning one-shot kernel (waiting for a peer's call that is queued behind a
-    GEMM needing whole CUs) can starve that GEMM of CUs -- a cross-process co-residency deadlock
-    that distinct GPUs cannot have (measured: 60 s timeout on the 1 MiB bf16 all-reduces,
-    tools/gpu_r5d.sh; the same calls pass in order on every rank).  The one-shot kernel itself is
-    covered at four ranks and 1 MiB bf16 by tests/test_oneshot_gpu.py."""
-    _run(4, 1, 4, 2, extra=dict(_BF16, base="gptj-6b"), env={"SMP_ONESHOT_ALLREDUCE": "auto"})
+    """GPT-J 6B width (16 heads x 256: the d = 256 flash kernels, rotary 64) at TP=4 in bf16, TP
+    collectives on the one-shot IPC kernel (four ranks sharing this GPU: the kernel is one wave
+    per workgroup without LDS, so its spinning waits cannot keep a GEMM workgroup off a CU)."""
+    _run(4, 1, 4, 2, extra=dict(_BF16, base="gptj-6b"))
 
 
 def test_gptneox20b_width_pp2_tp2_bf16_gpu():
@@ -95,4 +99,11 @@ def test_gpt2xl_width_tp2_fp16_dynamic_loss_scale_gpu():
     """GPT-2 XL width (25 heads x 64, uneven 13 / 12 head split) at TP=2 in fp16 with dynamic
     loss scaling (fp16 flash kernels, scaled backward, unscale + overflow check before SGD)."""
     _run(2, 1, 2, 2, extra={"base": "gpt2-xl", "dtype": "fp16", "loss_tol": 1e-2, "param_tol": 5e-3,
-                            "expect_flash": True})
+                            "expect_flash": True, "seq": 256, "grad_tol": 5e-3, "fp32_ref_tol": 3e-2})
+
+
+def test_grad_check_catches_missing_tp_allreduce():
+    """Mutation: the column-parallel layers' input-gradient all-reduce dropped on every rank
+    (GPT-2 XL width, TP=2, bf16) -- the gradient check must fail."""
+    with pytest.raises(AssertionError, match="grad rel err"):
+        _run(2, 1, 2, 2, extra=dict(_BF16, base="gpt2-xl", break_tp_bwd=True, fp32_ref_tol=None))

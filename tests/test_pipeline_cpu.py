@@ -8,6 +8,11 @@ import pytest
 from tests.dist_utils import run_workers
 
 
+# per-parameter first-step gradients as relative norms, against the same model unpartitioned and
+# against the plain-torch fp32 model of tests/torch_ref.py (reference smp_test_base.py:731-788)
+_GRADS = {"grad_tol": 1e-4, "fp32_ref_tol": 1e-4}
+
+
 def _run(world, pp, tp, mbs, pipe="interleaved", auto=0, steps=2, extra=None, timeout=200, env=None):
     args = [pp, tp, mbs, pipe, auto, steps]
     if extra:
@@ -33,7 +38,7 @@ def test_pp4_auto_partition():
 
 
 def test_pp2_dp2():
-    _run(4, 2, 1, 2)
+    _run(4, 2, 1, 2, extra=_GRADS)
 
 
 @pytest.mark.parametrize("pipe", ["interleaved", "simple"])
@@ -48,7 +53,14 @@ def test_dp2():
 
 
 def test_tp2():
-    _run(2, 1, 2, 1)
+    _run(2, 1, 2, 1, extra=_GRADS)
+
+
+def test_tp2_grad_check_catches_missing_tp_allreduce():
+    """Mutation: drop the column-parallel input-gradient all-reduce on every rank; the
+    per-parameter gradient check (reference smp_test_base.py:731-788) must fail."""
+    with pytest.raises(AssertionError, match="grad rel err"):
+        _run(2, 1, 2, 1, extra=dict(_GRADS, break_tp_bwd=True))
 
 
 def test_tp2_dx_allreduce_overlaps_weight_gradient():
@@ -82,7 +94,7 @@ def test_tp2_distribute_embedding(prescaled):
 
 
 def test_pp2_tp2():
-    _run(4, 2, 2, 2)
+    _run(4, 2, 2, 2, extra=dict(_GRADS, seq=32))
 
 
 def test_pp2_activation_checkpointing():

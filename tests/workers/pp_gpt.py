@@ -3,6 +3,15 @@
 argv: pp tp microbatches pipeline(simple|interleaved) auto(0|1) steps [extra_json]
 Each rank trains the smp model and an identical plain-PyTorch model on the same global
 batch and checks loss and parameters after every step.
+
+Gradient checks (reference `test/torch/smp_test_base.py:731-788`), on the first step, before
+the optimizer update, per local (TP-sliced) parameter as a relative norm |g - g_ref| / |g_ref|:
+* ``grad_tol``: against the same architecture run unpartitioned in the same dtype;
+* ``fp32_ref_tol``: against the independent plain-torch fp32 model of tests/torch_ref.py on the
+  initial weights (no smp module, no HIP kernel) -- a looser bound, since it also measures the
+  reduced-precision rounding of the smp run.
+``seq`` sets the sequence length (default 16); ``break_tp_bwd`` drops the column-parallel
+input-gradient all-reduce on every rank (a mutation the gradient check must catch).
 """
 import json
 import sys
@@ -41,8 +50,14 @@ def main():
     smp.init(cfg)
     dev = smp.state.device  # GPU runs (tests/test_hybrid_gpu.py): every rank on the box's one GPU
     ref.to(dev)
+    fp32_tol = extra.get("fp32_ref_tol")
+    sd0 = {k: v.detach().float().clone() for k, v in ref.state_dict().items()} if fp32_tol else None
     if ldt is not None:
         ref.to(ldt)
+    if extra.get("break_tp_bwd"):
+        import smdistributed_modelparallel_amd.nn.transformer as tr
+
+        tr.dx_allreduce_async = lambda dx: None  # mutation: column-parallel dX never all-reduced
     delayed = bool(extra.get("delayed"))
     with smp.delay_param_initialization(enabled=delayed):
         with smp.model_creation(tensor_parallelism=tp > 1):
@@ -113,11 +128,19 @@ def main():
     dp = smp.rdp_size() if prescaled else smp.dp_size()
     my_dp = smp.rdp_rank() if prescaled else smp.dp_rank()
     local_bs = 2 * mbs
+    seq = int(extra.get("seq", 16))
+    grad_tol = extra.get("grad_tol")
     for it in range(steps):
-        ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, 16), generator=g).to(dev)
+        ids_all = torch.randint(0, kw["vocab_size"], (local_bs * dp, seq), generator=g).to(dev)
         ids = ids_all[my_dp * local_bs:(my_dp + 1) * local_bs]
         opt.zero_grad()
         out = train(model, ids, ids)
+        snap = None
+        if it == 0 and (grad_tol or fp32_tol):
+            # reduced gradients of the first step, before the update (fp16: loss-scaled)
+            inv = 1.0 / float(getattr(opt, "loss_scale", 1.0) or 1.0)
+            snap = {n: p.grad.detach().float() * inv for n, p in model.local_named_parameters()
+                    if p.grad is not None and p.numel() > 0}
         if extra.get("opt_clip"):
             opt.clip_master_grads(extra["opt_clip"])
         opt.step()
@@ -143,6 +166,8 @@ def main():
                 losses.append(l)
         ref_loss = torch.stack(losses).mean()
         ref_loss.backward()
+        if snap is not None:
+            _check_grads(model, snap, ref, sd0, ids_all, kw, base, grad_tol, fp32_tol)
         if extra.get("ref_clip") or extra.get("opt_clip"):
             torch.nn.utils.clip_grad_norm_(ref.parameters(), extra.get("ref_clip") or extra["opt_clip"])
         ropt.step()
@@ -229,6 +254,34 @@ def main():
         print(f"rank {smp.rank()} flash launches {ran}", flush=True)
     print(f"rank {smp.rank()} OK loss={ref_loss.item():.5f} worst_param_diff={worst:.2e}", flush=True)
     smp.barrier()
+
+
+def _check_grads(model, snap, ref, sd0, ids_all, kw, base, grad_tol, fp32_tol):
+    from smdistributed_modelparallel_amd.models import GPT_CONFIGS
+    from smdistributed_modelparallel_amd.torch.checkpoint_utils import slice_for_param
+
+    params = dict(model.local_named_parameters())
+    refs = []
+    if grad_tol:
+        refs.append(("same-dtype model", {n: p.grad for n, p in ref.named_parameters()}, float(grad_tol)))
+    if fp32_tol:
+        from tests.torch_ref import gpt_loss
+
+        leaves = {k: v.clone().requires_grad_(True) for k, v in sd0.items()}
+        gpt_loss(leaves, ids_all, ids_all, dict(GPT_CONFIGS[base], **kw)).backward()
+        refs.append(("plain-torch fp32", {n: t.grad for n, t in leaves.items()}, float(fp32_tol)))
+    for label, grads, tol in refs:
+        worst, name = 0.0, None
+        for n, g in snap.items():
+            r = grads.get(n)
+            assert r is not None, (label, n, "no reference gradient")
+            r = slice_for_param(r.detach().float(), params[n], smp.tp_rank(), smp.tp_size())
+            err = float((g - r).norm() / (r.norm() + 1e-12))
+            if err > worst:
+                worst, name = err, n
+        assert worst < tol, f"rank {smp.rank()}: grad rel err vs {label} {worst:.4f} > {tol} ({name})"
+        print(f"rank {smp.rank()} grads vs {label}: worst rel err {worst:.4f} ({name}) over {len(snap)} params",
+              flush=True)
 
 
 if __name__ == "__main__":
