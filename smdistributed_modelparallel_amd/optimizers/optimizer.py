@@ -255,11 +255,22 @@ class DistributedOptimizer:
         group = state.pgs.world if sharded else (self._model_parallel_group() if state.core.mp_size() > 1 else None)
         return any_overflow(grads, group)
 
+    @staticmethod
+    def _materialize_grads():
+        """Sharded data parallelism zeroes gradient shards lazily (``_ShardFlat.zero_grad``):
+        make sure no shard is read before its zero fill when a step ran no reduction."""
+        model = state.model
+        for flat in (model.flat_groups.values() if model is not None else ()):
+            fill = getattr(flat, "fill_fresh", None)
+            if fill is not None:
+                fill()
+
     def clip_master_grads(self, max_norm, norm_type=2):
         """Global L2 norm of the (unscaled) gradients across all ranks holding distinct
         gradients; records the clip coefficient applied inside the next step."""
         if norm_type != 2:
             raise SMPInvalidArgumentError("only L2 norm clipping is supported")
+        self._materialize_grads()
         dev = state.device
         acc = torch.zeros(1, dtype=torch.float32, device=dev)
         core = state.core
@@ -284,6 +295,7 @@ class DistributedOptimizer:
 
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        self._materialize_grads()
         if state.sdp is not None and self._clip_coef is None and state.cfg.sdp_gradient_clipping > 0:
             # sharded data parallelism clips to sdp_gradient_clipping on every step (the
             # DeepSpeed `gradient_clipping` the reference configures, zero_config.py)

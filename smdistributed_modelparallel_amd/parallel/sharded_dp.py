@@ -30,8 +30,9 @@ MI355X design:
   the whole step.
 * **Backward.**  A gradient hook on each unit's forward outputs re-gathers the unit before
   its backward runs; ``post_accumulate_grad`` hooks count finished gradients, and a
-  complete unit is pre-scaled by ``1/(microbatches x dp)`` and reduce-scattered into the
-  shard gradient buffer while the rest of backward proceeds.  Activation-checkpoint
+  complete unit is reduce-scattered straight into the shard gradient buffer, averaged by
+  ``1/(microbatches x dp)`` inside RCCL (pre-multiplied sum), while the rest of backward
+  proceeds.  Activation-checkpoint
   recomputation (forward hooks firing inside backward) keeps the unit gathered.
 """
 import os
@@ -59,6 +60,7 @@ def _in_backward():
 class _Unit:
     def __init__(self, index, modules, params, names, shard_size, dtype):
         self.index = index
+        self.fresh = False  # the shard's gradient was zeroed (lazily): the next reduction writes it
         self.modules = modules
         self.params = params
         self.names = names
@@ -91,6 +93,7 @@ class _ShardFlat:
 
     def __init__(self, units, device, dtype):
         total = sum(u.shard_numel for u in units)
+        self.units = units
         self.data = torch.zeros(total, dtype=dtype, device=device)
         self.grad = torch.zeros(total, dtype=dtype, device=device)
         self.buckets = []
@@ -109,7 +112,17 @@ class _ShardFlat:
         return self.grad[u.shard_start:u.shard_start + u.shard_numel]
 
     def zero_grad(self):
-        self.grad.zero_()
+        """Lazy: every shard is marked fresh, and the step's first reduce-scatter of a unit writes
+        its shard directly (no zero pass, no temporary + add); ``fill_fresh`` zeroes what no
+        reduction wrote by the end of the step."""
+        for u in self.units:
+            u.fresh = True
+
+    def fill_fresh(self):
+        for u in self.units:
+            if u.fresh:
+                self.grad_shard(u).zero_()
+                u.fresh = False
 
     def params(self):
         return [p for b in self.buckets for p in b.params]
@@ -263,6 +276,16 @@ class ShardedDataParallel:
         self.dtype = dtype
         self._group_of = {}
         self.flat = _ShardFlat(self.units, self.device, dtype)
+        # the average's 1 / (microbatches x S x R) applied inside RCCL's reduction (pre-multiplied
+        # sum, probed once here -- a collective at a fixed point of every rank's order -- like
+        # the DDP reducer) instead of a scaling pass over every gradient byte
+        from .ddp import probe_premul_sum
+
+        red = self.intra if self.hier else self.group
+        self._premul = (red is not None and self.device.type == "cuda" and hasattr(dist, "_make_nccl_premul_sum")
+                        and dist.get_backend(red) == "nccl" and os.environ.get("SMP_DDP_PREMUL_SUM", "1") != "0"
+                        and probe_premul_sum(red, dtype, self.device, dist.get_world_size(red)))
+        self._side = None  # hierarchical reduce-scatter: both stages ordered on a side stream
         # fill shards from the (broadcast-consistent) full parameters, then free them
         with torch.no_grad():
             for u in self.units:
@@ -496,6 +519,11 @@ class ShardedDataParallel:
 
     # ---------------------------------------------------------------- reduce
     def _reduce_unit(self, u):
+        """Reduce-scatter the unit's full gradient into this rank's shard: scaled inside RCCL
+        (pre-multiplied sum) and written straight into the shard when it is the step's first
+        contribution -- no scaling pass, no temporary, no add; later microbatches' contributions
+        land in a temporary and are added.  Hierarchical: the node-local and cross-node stages
+        are chained on a side stream, so the compute stream never waits for the first one."""
         fg = u.full_grad
         if fg is None:
             return
@@ -503,30 +531,50 @@ class ShardedDataParallel:
         u.ready = 0
         for p in u.params:
             p.grad = None
-        fg.mul_(1.0 / (self.num_mb * self.S * self.R))
+        scale = 1.0 / (self.num_mb * self.S * self.R)
+        fresh, u.fresh = u.fresh, False
+        shard = self.flat.grad_shard(u)
         if self.group is None:
-            self.flat.grad_shard(u).add_(fg)
-        elif self.hier:
-            # node-local reduce-scatter to this local rank's N-slice block, then the
-            # cross-node reduce-scatter of that block to slice l * N + n
-            mid = torch.empty(u.shard_numel * dist.get_world_size(self.inter), dtype=u.dtype, device=self.device)
-            dist.reduce_scatter_tensor(mid, fg, group=self.intra, async_op=True).wait()
-            out = torch.empty(u.shard_numel, dtype=u.dtype, device=self.device)
-            work = dist.reduce_scatter_tensor(out, mid, group=self.inter, async_op=True)
-            self._pending_rs.append((u, out, (fg, mid), work))
+            if fresh:
+                torch.mul(fg[:u.shard_numel], scale, out=shard)
+            else:
+                shard.add_(fg[:u.shard_numel], alpha=scale)
         else:
-            out = torch.empty(u.shard_numel, dtype=u.dtype, device=self.device)
-            work = dist.reduce_scatter_tensor(out, fg, group=self.group, async_op=True)
-            self._pending_rs.append((u, out, fg, work))
+            op = dist.ReduceOp.SUM
+            if self._premul:
+                op = dist._make_nccl_premul_sum(scale)
+            else:
+                fg.mul_(scale)
+            out = shard if fresh else torch.empty(u.shard_numel, dtype=u.dtype, device=self.device)
+            if self.hier:
+                # node-local reduce-scatter to this local rank's N-slice block, then the cross-node
+                # reduce-scatter of that block to slice l * N + n
+                mid = torch.empty(u.shard_numel * dist.get_world_size(self.inter), dtype=u.dtype, device=self.device)
+                if fg.is_cuda:
+                    if self._side is None:
+                        self._side = torch.cuda.Stream(device=self.device)
+                    self._side.wait_stream(torch.cuda.current_stream(self.device))
+                    with torch.cuda.stream(self._side):
+                        dist.reduce_scatter_tensor(mid, fg, op=op, group=self.intra, async_op=True).wait()
+                        work = dist.reduce_scatter_tensor(out, mid, group=self.inter, async_op=True)
+                else:  # gloo: collectives complete on the host anyway
+                    dist.reduce_scatter_tensor(mid, fg, op=op, group=self.intra)
+                    work = dist.reduce_scatter_tensor(out, mid, group=self.inter, async_op=True)
+                keep = (fg, mid)
+            else:
+                work = dist.reduce_scatter_tensor(out, fg, op=op, group=self.group, async_op=True)
+                keep = fg
+            self._pending_rs.append((u, None if fresh else out, keep, work))
             while len(self._pending_rs) > 2:
                 self._finish_one_rs()
         if not u.persistent:
             self._release(u)
 
     def _finish_one_rs(self):
-        u, out, fg, work = self._pending_rs.popleft()
+        u, out, keep, work = self._pending_rs.popleft()
         work.wait()
-        self.flat.grad_shard(u).add_(out)
+        if out is not None:  # a later microbatch's contribution: accumulate
+            self.flat.grad_shard(u).add_(out)
 
     def _end_of_backward(self):
         self._cb_queued = False
@@ -544,6 +592,7 @@ class ShardedDataParallel:
         """End of step: finish reductions, then average the shards across replicas."""
         while self._pending_rs:
             self._finish_one_rs()
+        self.flat.fill_fresh()  # shards no reduction wrote this step (no gradient reached them)
         if self.replica_group is not None and self.R > 1:
             dist.all_reduce(self.flat.grad, group=self.replica_group)
 
