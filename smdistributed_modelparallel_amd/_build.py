@@ -109,7 +109,7 @@ def build_runtime(jobs=8, verbose=False):
 
 
 # per-translation-unit extra flags (measured per kernel: profiles/r3/s3_rehearsal.md)
-_TU_FLAGS = {"attention_d64_dq.hip": ["-fno-slp-vectorize"]}
+_TU_FLAGS = {"attention_d64_dq.hip": ["-fno-slp-vectorize"], "attention_d64.hip": ["-fno-slp-vectorize"]}
 
 
 def build_kernels(jobs=8, verbose=False):

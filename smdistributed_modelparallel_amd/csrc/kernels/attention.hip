@@ -26,14 +26,9 @@ int attention_fwd(int dt, const AttnParams& p, hipStream_t s) {
   }
 }
 
-bool attention_bwd_fused_ok(const AttnBwdParams& p) {
-  return p.f.d == 64 && p.f.causal && p.f.sq == p.f.sk && p.f.kbias == nullptr && p.f.window <= 0;
-}
-
 int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s) {
   if (p.f.b * p.f.h == 0 || p.f.sq == 0) return 0;
   if (p.f.drop_on && p.f.drop_bits == nullptr) return -4;  // dropout backward reads the forward's keep bits
-  if (p.fused && attention_bwd_fused_ok(p)) return attention_bwd_fused_d64(dt, p, s);
   switch (p.f.d) {
     case 64: return attention_bwd_d64(dt, p, s);
     case 96: return attention_bwd_d96(dt, p, s);

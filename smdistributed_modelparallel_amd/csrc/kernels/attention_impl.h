@@ -432,6 +432,17 @@ __device__ __forceinline__ int64_t bits_index(int64_t bh, int ntiles, int tile, 
   return ((bh * ntiles + tile) * static_cast<int64_t>(sq) + q) * 2 + hh;
 }
 
+// The keep flags of the lane's tile from its stored word (the inverse of pack_keep): the flags
+// of register group g of half s sit at bits 8 i + 7 of w << (g + 4 s) -- the bits at other
+// positions are ignored by drop_packed's v_perm selectors, so no masking is needed.
+__device__ __forceinline__ void unpack_keep(uint32_t w, uint32_t (&f0)[4], uint32_t (&f1)[4]) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    f0[g] = w << g;
+    f1[g] = w << (4 + g);
+  }
+}
+
 // The lane's 32 keep bits of a tile from the 8 keep words of its two 32-key halves: word g of
 // half s keeps its flags at bits 7, 15, 23, 31 (element i at 8 i + 7); shifted right by g + 4 s
 // they interleave without overlap, so register reg = 4 g + i of half s is bit
@@ -508,10 +519,15 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
   constexpr bool QLDS = QInLds<D>::v;
   static_assert(!DMA || (!QLDS && !BIAS && DS == D && (D == 64 || D == 128)), "DMA variant: D 64 / 128, no bias");
   // K then V of each buffer (one array: a second LDS object beside DMA targets can make
-  // hipcc drain vmcnt before ds_reads)
-  __shared__ __attribute__((aligned(16))) uint16_t sKV[(DMA ? 4 : 2) * BN * DS];
+  // hipcc drain vmcnt before ds_reads); DMA + dropout: then the two buffers' keep words (the
+  // block's 128 queries x 2 halves = 256 words = 1 KB per tile, one LDS-DMA dword
+  // instruction per wave)
+  constexpr int KBW = BM * 2;  // keep words per block per tile
+  constexpr bool BITS_LDS = DMA && DROP;
+  __shared__ __attribute__((aligned(16))) uint16_t sKV[(DMA ? 4 : 2) * BN * DS + (BITS_LDS ? 2 * 2 * KBW : 0)];
   uint16_t* sK = sKV;
   uint16_t* sV = sKV + BN * DS;
+  const uint32_t* sBits = reinterpret_cast<const uint32_t*>(sKV + 4 * BN * DS);
   __shared__ __attribute__((aligned(16))) uint16_t sQ[QLDS ? BM * DS : 8];
   __shared__ __attribute__((aligned(16))) float sB[BIAS ? BN : 4];
   __shared__ int sFlag;
@@ -555,9 +571,6 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
   }
   const float sl2 = p.scale * kLog2e;
   const float inv_scale = 1.f / p.scale;
-  const uint32_t dkey = DROP ? drop_key(p, bh) : 0u;
-  const uint32_t bkey = DROP ? drop_block_key(dkey) : 0u;
-  const uint32_t qbase = static_cast<uint32_t>(qrow) * static_cast<uint32_t>((sk + 3) >> 2);
   // m_i: exponent offset (lazy running max, log2 units), l_i: this lane's partial row sum
   float m_i = -INFINITY, m_use = 0.f, l_i = 0.f;
   f32x16 o[D / 32];
@@ -596,6 +609,30 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
     // the loop and drains vmcnt(0) -- the in-flight K/V DMA included -- before the first MFMA
     __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
   }
+  // Dropout keep bits: generated before the forward by the keep-bits kernel (attention_bits.hip,
+  // the words the backward reads too) -- no hash in this kernel (it was ~110 VALU per tile per
+  // lane).  DMA: a tile's 1 KB of the block's words arrives by LDS-DMA with the tile's K / V
+  // (same vmcnt + barrier) and each lane reads its word from LDS; register staging: each lane
+  // loads its word one tile ahead, before that tile's K / V loads (as the dQ kernel does).
+  const bool bits_row_ok = DROP && qrow < sq;
+  const int64_t sq2 = 2 * static_cast<int64_t>(sq);
+  auto bits_ptr = [&](int t) {
+    return p.drop_bits + bits_index(bh, ntiles64, (kv_begin + t * BN) >> 6, sq, qrow, hh);
+  };
+  // word w of the block's tile-t slab (words [q][hh] are contiguous over the block's queries);
+  // rows past sq re-read the tile's last word (those queries are never stored)
+  auto dma_bits = [&](int t, int b) {
+    const int64_t w = static_cast<int64_t>(qb) * KBW + wave * 64 + lane;
+    const int64_t base = (bh * ntiles64 + ((kv_begin + t * BN) >> 6)) * sq2;
+    lds_dma4(p.drop_bits + base + (w < sq2 ? w : sq2 - 1), sKV + 4 * BN * DS + b * 2 * KBW + wave * 128);
+  };
+  const int kb_slot = wave * 64 + 2 * r + hh;  // this lane's word in a tile's slab
+  uint32_t kb_cur = 0u, kb_nxt = 0u;
+  if constexpr (BITS_LDS) {
+    if (nt > 0) dma_bits(0, 0);
+  } else {
+    if (nt > 0 && bits_row_ok) kb_nxt = *bits_ptr(0);
+  }
   if (nt > 0) {
     if constexpr (DMA) {
       dma_tile<D, BN>(sKV, K, p.k_ss, kv_begin, sk, wave, lane);
@@ -616,13 +653,16 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
       __syncthreads();  // ... everyone's; and every wave is done with the other buffer
       sK = sKV + buf * 2 * BN * DS;
       sV = sK + BN * DS;
+      if constexpr (BITS_LDS) sBits = reinterpret_cast<const uint32_t*>(sKV + 4 * BN * DS + buf * 2 * KBW);
       if (t + 1 < nt) {
+        if constexpr (BITS_LDS) dma_bits(t + 1, buf ^ 1);
         uint16_t* nb = sKV + (buf ^ 1) * 2 * BN * DS;
         dma_tile<D, BN>(nb, K, p.k_ss, kv0 + BN, sk, wave, lane);
         dma_tile<D, BN>(nb + BN * DS, V, p.v_ss, kv0 + BN, sk, wave, lane);
       }
       buf ^= 1;
     } else {
+      kb_cur = kb_nxt;
       __syncthreads();
       stK.store(sK);
       stV.store(sV);
@@ -633,6 +673,7 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
       __syncthreads();
       tile_bias = BIAS && sFlag != 0;
       if (t + 1 < nt) {
+        if (bits_row_ok) kb_nxt = *bits_ptr(t + 1);
         stK.load(K + static_cast<int64_t>(kv0 + BN) * p.k_ss, sk - kv0 - BN);
         stV.load(V + static_cast<int64_t>(kv0 + BN) * p.v_ss, sk - kv0 - BN);
         if (BIAS && threadIdx.x < BN) bstage = load_bias(p, b, kv0 + BN + threadIdx.x);
@@ -650,18 +691,9 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
       s0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qt, s0);
       s1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * DS), qt, s1);
     }
-    // While the S MFMAs run: the dropout hashes (independent of S) and, D = 64, the V operand
-    // fragments of this tile's PV MFMAs (their LDS latency then hides under the softmax
-    // instead of stalling each PV MFMA; +32 VGPRs, occupancy unchanged)
+    // the tile's dropout keep flags from its keep word
     uint32_t f0[4], f1[4];
-    if (DROP) {
-      const DropThr d0 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5));
-      const DropThr d1 = drop_block_thr(p, bkey, static_cast<uint32_t>(q0 >> 5), static_cast<uint32_t>(kv0 >> 5) + 1);
-      drop_words(f0, dkey, qbase, kv0, hh, d0.xr, d0.c);
-      drop_words(f1, dkey, qbase, kv0 + 32, hh, d1.xr, d1.c);
-      if (p.drop_bits != nullptr && qrow < sq)  // for the backward kernels
-        p.drop_bits[bits_index(bh, ntiles64, kv0 >> 6, sq, qrow, hh)] = pack_keep(f0, f1);
-    }
+    if (DROP) unpack_keep(BITS_LDS ? sBits[kb_slot] : kb_cur, f0, f1);
     if (BIAS && tile_bias) {
       add_from_keys(s0, sB, hh);
       add_from_keys(s1, sB + 32, hh);

@@ -657,6 +657,8 @@ void check_bshd(const at::Tensor& t, const char* n) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf, n, " must be bf16/fp16");
 }
 
+void set_dropout(smpk::AttnParams& p, double dropout_p, int64_t seed, int64_t offset);
+
 smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, double scale, bool causal,
                              int64_t window, const c10::optional<at::Tensor>& kbias,
                              double dropout_p, int64_t seed,
@@ -696,6 +698,13 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
     p.kbias = kb.data_ptr<float>();
     p.kbias_sb = kb.size(0) == 1 ? 0 : kb.stride(0);
   }
+  set_dropout(p, dropout_p, seed, offset);
+  return p;
+}
+
+// dropout fields of the attention parameters (the keep-bits kernel needs only these and the
+// sizes)
+void set_dropout(smpk::AttnParams& p, double dropout_p, int64_t seed, int64_t offset) {
   TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention: dropout_p must be in [0, 1)");
   if (dropout_p > 0.0) {
     // dropped iff the element's 8-bit uniform < thr, where each 32x32 block draws thr from
@@ -721,33 +730,58 @@ smpk::AttnParams attn_params(const at::Tensor& q, const at::Tensor& k, const at:
     p.seed = static_cast<uint64_t>(seed);
     p.offset = static_cast<uint64_t>(offset);
   }
-  return p;
 }
 
 std::vector<at::Tensor> attention_fwd(at::Tensor q, at::Tensor k, at::Tensor v, double scale, bool causal,
                                       int64_t window, c10::optional<at::Tensor> kbias,
                                       double dropout_p, int64_t seed,
-                                      int64_t offset, bool store_bits) {
+                                      int64_t offset, bool store_bits, c10::optional<at::Tensor> bits_in) {
   auto p = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   auto o = at::empty({p.b, p.sq, p.h, p.d}, q.options());
   auto lse = at::empty({p.b, p.h, p.sq}, q.options().dtype(at::kFloat));
   p.o = o.data_ptr();
   p.o_sb = o.stride(0), p.o_ss = o.stride(1), p.o_sh = o.stride(2);
   p.lse = lse.data_ptr<float>();
-  // dropout: the keep bits for the backward (1 bit per score: b h sq sk / 8 bytes)
+  // dropout: the keep bits (1 bit per score: b h sq sk / 8 bytes) are generated first by the
+  // keep-bits kernel and read by the forward (no hash in the MFMA loop); kept for the backward
+  // when store_bits, else dropped here and regenerated before the backward
+  // (bits_in: the same words, generated earlier by attention_keep_bits_for on a side stream)
   at::Tensor bits;
-  if (p.drop_on && store_bits) {
+  if (p.drop_on && bits_in.has_value() && bits_in->defined()) {
+    bits = *bits_in;
+    TORCH_CHECK(bits.is_cuda() && bits.scalar_type() == at::kInt && bits.is_contiguous() &&
+                    bits.numel() == p.b * p.h * ((p.sk + 63) / 64) * p.sq * 2,
+                "attention_fwd: bits_in must be the int32 [b h, ceil(sk / 64), sq, 2] keep bits");
+    p.drop_bits = reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>());
+  } else if (p.drop_on) {
     bits = at::empty({p.b * p.h, (p.sk + 63) / 64, p.sq, 2}, q.options().dtype(at::kInt));
     p.drop_bits = reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>());
-  } else {
-    bits = at::empty({0}, q.options().dtype(at::kInt));
+    check(smpk::attention_keep_bits(p, p.drop_bits, stream()), "attention_keep_bits");
   }
   check(smpk::attention_fwd(dt_code(q), p, stream()), "attention_fwd");
+  if (!p.drop_on || !store_bits) bits = at::empty({0}, q.options().dtype(at::kInt));
   return {o, lse, bits};
 }
 
 // The keep bits a dropout forward with these arguments stores, regenerated from the hash (for a
 // forward called with store_bits = false).
+// The keep bits of a (b, h, sq, sk) attention from the sizes alone, on the current stream (the
+// caller's side stream: launched before the QKV projection, the hash runs beside that GEMM)
+at::Tensor attention_keep_bits_for(int64_t b, int64_t h, int64_t sq, int64_t sk, bool causal, double dropout_p,
+                                   int64_t seed, int64_t offset, at::Tensor like) {
+  TORCH_CHECK(dropout_p > 0.0, "attention_keep_bits_for: dropout_p must be > 0");
+  TORCH_CHECK(like.is_cuda(), "attention_keep_bits_for: like must be a GPU tensor");
+  TORCH_CHECK(b >= 0 && h >= 0 && sq >= 0 && sk >= 0 && sq < (1 << 24) && sk < (1 << 24), "attention_keep_bits_for: sizes");
+  smpk::AttnParams p{};
+  p.b = b, p.h = h, p.sq = sq, p.sk = sk;
+  p.causal = causal ? 1 : 0;
+  set_dropout(p, dropout_p, seed, offset);
+  auto bits = at::empty({b * h, (sk + 63) / 64, sq, 2}, like.options().dtype(at::kInt));
+  check(smpk::attention_keep_bits(p, reinterpret_cast<uint32_t*>(bits.data_ptr<int32_t>()), stream()),
+        "attention_keep_bits");
+  return bits;
+}
+
 at::Tensor attention_keep_bits(at::Tensor q, at::Tensor k, at::Tensor v, bool causal, int64_t window,
                                double dropout_p, int64_t seed, int64_t offset) {
   TORCH_CHECK(dropout_p > 0.0, "attention_keep_bits: dropout_p must be > 0");
@@ -762,8 +796,7 @@ at::Tensor attention_keep_bits(at::Tensor q, at::Tensor k, at::Tensor v, bool ca
 void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
                         at::Tensor dq, at::Tensor dk, at::Tensor dv, double scale, bool causal, int64_t window,
                         c10::optional<at::Tensor> kbias, double dropout_p,
-                        int64_t seed, int64_t offset, c10::optional<at::Tensor> drop_bits, int64_t fused,
-                        c10::optional<at::Tensor> err_out) {
+                        int64_t seed, int64_t offset, c10::optional<at::Tensor> drop_bits) {
   smpk::AttnBwdParams P{};
   P.f = attn_params(q, k, v, scale, causal, window, kbias, dropout_p, seed, offset);
   if (P.f.drop_on) {
@@ -795,23 +828,7 @@ void attention_bwd_into(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor 
   P.dv_sb = dv.stride(0), P.dv_ss = dv.stride(1), P.dv_sh = dv.stride(2);
   auto delta = at::empty({P.f.b, P.f.h, P.f.sq}, q.options().dtype(at::kFloat));
   P.delta = delta.data_ptr<float>();
-  P.dq_acc = nullptr;
-  P.dq_flags = P.dq_err = nullptr;
-  P.fused = 0;
-  at::Tensor acc, flags;
-  if (fused != 0 && smpk::attention_bwd_fused_ok(P)) {
-    // fused backward: fp32 dQ partials (one 16 KB slot per (b h, 64-query tile)) and the
-    // hand-off flags + error word, zeroed on the stream ahead of the kernel
-    const int64_t ntq = (P.f.sq + 63) / 64;
-    acc = at::empty({P.f.b * P.f.h * ntq * 4096}, q.options().dtype(at::kFloat));
-    flags = at::zeros({P.f.b * P.f.h * ntq + 4}, q.options().dtype(at::kInt));
-    P.dq_acc = acc.data_ptr<float>();
-    P.dq_flags = flags.data_ptr<int32_t>();
-    P.dq_err = P.dq_flags + P.f.b * P.f.h * ntq;
-    P.fused = 1;
-  }
   check(smpk::attention_bwd(dt_code(q), P, stream()), "attention_bwd");
-  if (err_out.has_value() && err_out->defined() && flags.defined()) err_out->copy_(flags.narrow(0, flags.numel() - 4, 1));
 }
 
 }  // namespace
@@ -872,12 +889,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("vocab_start"), py::arg("ignore_index"), py::arg("vocab") = -1);
   m.def("attention_fwd", &attention_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
-        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("store_bits") = true);
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("store_bits") = true,
+        py::arg("bits_in") = py::none());
+  m.def("attention_keep_bits_for", &attention_keep_bits_for, py::arg("b"), py::arg("h"), py::arg("sq"), py::arg("sk"),
+        py::arg("causal"), py::arg("dropout_p"), py::arg("seed"), py::arg("offset"), py::arg("like"));
   m.def("attention_keep_bits", &attention_keep_bits, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("causal"),
         py::arg("window"), py::arg("dropout_p"), py::arg("seed"), py::arg("offset"));
   m.def("attention_bwd_into", &attention_bwd_into, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"),
         py::arg("o"), py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"),
         py::arg("causal"), py::arg("window"), py::arg("kbias") = py::none(),
-        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("drop_bits") = py::none(),
-        py::arg("fused") = 0, py::arg("err_out") = py::none());
+        py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("offset") = 0, py::arg("drop_bits") = py::none());
 }

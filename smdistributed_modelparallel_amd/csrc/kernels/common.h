@@ -138,6 +138,14 @@ __device__ __forceinline__ void lds_dma16(const void* src, const void* lds_wave_
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
 }
 
+// One dword per lane (a wave writes 256 consecutive LDS bytes at lds_wave_base): small slabs
+// that ride with a tile's 16-byte DMA pieces, e.g. the attention forward's dropout keep words.
+__device__ __forceinline__ void lds_dma4(const void* src, const void* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+
 // Same, saddr form: scalar 64-bit base + 32-bit per-lane byte offset.  Interior tiles use
 // this so the only per-lane address term is loop-invariant (no 64-bit row * stride multiply
 // and add per load per tile).

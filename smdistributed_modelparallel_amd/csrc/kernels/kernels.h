@@ -191,19 +191,10 @@ struct AttnBwdParams {
   int64_t dk_sb, dk_sh, dk_ss;
   int64_t dv_sb, dv_sh, dv_ss;
   float* delta;  // [b, h, sq] workspace
-  // fused backward (attention_d64_fused.hip): fp32 dQ partials [b h][ceil(sq / 64)][4096],
-  // per-(b h, query tile) hand-off flags and an error word, zeroed by the caller on the stream
-  float* dq_acc;
-  int* dq_flags;
-  int* dq_err;
-  int fused;  // 1: use the fused kernel (eligibility: attention_bwd_fused_ok)
 };
-// D = 64, causal self-attention without key bias / window: the fused single-kernel backward
-bool attention_bwd_fused_ok(const AttnBwdParams& p);
-int attention_bwd_fused_d64(int dt, const AttnBwdParams& p, hipStream_t s);
 int attention_fwd(int dt, const AttnParams& p, hipStream_t s);
-// the keep bits the dropout forward stores, regenerated from the hash into `bits`
-// ([b h, ceil(sk / 64), sq, 2] uint32) for a forward that stored none
+// the dropout keep bits from the hash into `bits` ([b h, ceil(sk / 64), sq, 2] uint32): before
+// every dropout forward (which reads them), and before a backward whose forward kept none
 int attention_keep_bits(const AttnParams& p, uint32_t* bits, hipStream_t s);
 bool attention_head_dim_supported(int64_t d);
 int attention_bwd(int dt, const AttnBwdParams& p, hipStream_t s);

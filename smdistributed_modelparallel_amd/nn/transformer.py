@@ -34,7 +34,7 @@ import torch.nn.functional as F
 from ..backend.exceptions import DistTransformerConfigError, SMPInvalidArgumentError
 from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
-from ..ops.attention import attention_packed
+from ..ops.attention import FLASH_HEAD_DIMS, attention_packed, prefetch_keep_bits
 from ..ops.cross_entropy import cross_entropy
 from ..ops.dropout import add3
 from ..ops.dropout import dropout_add as _dropout_add
@@ -415,6 +415,12 @@ class DistributedAttentionLayer(DistributedModule):
         else:
             causal = self.causal_mask_size is not None
             packed = not self.attention_in_fp32 and (_ROPE_PACKED or not self.rotary_dim)
+            pre = None
+            if (packed and mask is None and not self.window_size and self.training and self.attention_dropout_prob > 0.0
+                    and a.is_cuda and self.qkv_weight.dtype in (torch.bfloat16, torch.float16)
+                    and d in FLASH_HEAD_DIMS and ((not state.initialized) or state.cfg.amd_fused_attention)):
+                # dropout keep bits on a side stream beside the QKV projection GEMM
+                pre = prefetch_keep_bits(B, lh, s, s, causal, self.attention_dropout_prob, a.device, a)
             if packed and self.rotary_dim:
                 # rotary on the packed buffer, in place on the projection's 2-D (non-view) output:
                 # one dqkv buffer in the backward, no per-view zero-filled gradients to add up
@@ -429,7 +435,7 @@ class DistributedAttentionLayer(DistributedModule):
                     qkv, causal=causal, scale=self._scale(), dropout_p=self.attention_dropout_prob,
                     window=self.window_size, training=self.training,
                     use_flash=(not state.initialized) or state.cfg.amd_fused_attention,
-                    mask=mask, mask_value=getattr(self, "mask_value", -1e4),
+                    mask=mask, mask_value=getattr(self, "mask_value", -1e4), keep_bits=pre,
                 )
                 # row-parallel: the TP all-reduce runs per token chunk beside the next chunk's GEMM
                 return linear(ctx.reshape(B, s, lh * d), self.dense_weight, self.dense_bias,
@@ -899,6 +905,9 @@ class DistributedTransformerLMHead(DistributedModule):
             cross_states = cross_mask = None
         B, s = input_ids.shape[0], input_ids.shape[1]
         device = input_ids.device
+        if self.use_positional_embedding and position_ids is None and s > self.num_positions:
+            # host-side shape check: position ids past the table are an out-of-bounds gather
+            raise SMPInvalidArgumentError(f"sequence length {s} exceeds num_positions {self.num_positions}")
         if position_ids is None:
             position_ids = torch.arange(0, s, dtype=torch.long, device=device).unsqueeze(0).expand(B, -1)
         elif position_ids.shape[0] != B:

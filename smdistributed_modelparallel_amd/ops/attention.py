@@ -129,14 +129,6 @@ def flash_dropout_keep_mask(b, h, sq, sk, dropout_p, seed, offset, device="cpu")
     return (u >= thr).view(b, h, sq, sk)
 
 
-# Fused single-kernel backward for D = 64 causal self-attention (csrc/kernels/attention_d64_fused.hip:
-# dK, dV and dQ in one pass with a deterministic ordered dQ hand-off).  SMP_ATTN_FUSED_BWD=1 turns
-# it on; FUSED_BWD_ERR[0], when set to an int32 [1] GPU tensor, receives the hand-off's error word
-# (a timed-out wait) after every fused backward -- tests assert it stays 0.
-FUSED_BWD = [os.environ.get("SMP_ATTN_FUSED_BWD", "0") == "1"]
-FUSED_BWD_ERR = [None]
-
-
 # forward launches of the flash kernels by variant, for run reports (bench.py "attention_calls":
 # a pipeline stage whose padding masks were decided all-ones launches no key-bias variant)
 FLASH_CALLS = {"plain": 0, "key_bias": 0}
@@ -155,6 +147,46 @@ def _store_bits(q, k, dropout_p):
     b, sq, h = q.shape[0], q.shape[1], q.shape[2]
     sk = k.shape[1]
     return b * h * ((sk + 63) // 64) * sq * 8 <= KEEPBITS_MAX_BYTES[0]
+
+
+# Keep-bits prefetch (SMP_ATTN_BITS_PREFETCH, default on): the layer launches the dropout
+# keep-bits kernel on a side stream right before its QKV projection GEMM, so the hash (pure
+# VALU + stores) runs beside the MFMA-bound GEMM instead of in front of the attention forward.
+BITS_PREFETCH = [os.environ.get("SMP_ATTN_BITS_PREFETCH", "1") != "0"]
+_SIDE = {}
+
+
+class KeepBits:
+    """Dropout keep bits generated ahead of the flash forward: (seed, offset) drawn now, the
+    words produced on a side stream; ``consume`` makes the current stream wait for them."""
+
+    __slots__ = ("bits", "seed", "off", "event", "shape")
+
+    def consume(self):
+        torch.cuda.current_stream(self.bits.device).wait_event(self.event)
+        return self.bits
+
+
+def prefetch_keep_bits(b, h, sq, sk, causal, dropout_p, device, like):
+    """Launch the keep-bits kernel for a (b, h, sq, sk) dropout attention on a side stream
+    (ordered after the work already queued on the current stream).  Returns a KeepBits for
+    ``attention_packed(..., keep_bits=...)``, or None when prefetching does not apply."""
+    if not (BITS_PREFETCH[0] and dropout_p > 0.0 and device.type == "cuda"):
+        return None
+    seed, off = dropout_seed_offset(device)
+    cur = torch.cuda.current_stream(device)
+    side = _SIDE.get(device)
+    if side is None:
+        side = _SIDE[device] = torch.cuda.Stream(device=device)
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        bits = ext().attention_keep_bits_for(b, h, sq, sk, causal, dropout_p, seed, off, like)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    bits.record_stream(cur)  # read (and saved for the backward) on the compute stream
+    kb = KeepBits()
+    kb.bits, kb.seed, kb.off, kb.event, kb.shape = bits, seed, off, ev, (b, h, sq, sk, bool(causal), float(dropout_p))
+    return kb
 
 
 def _keep_bits(bits, q, k, v, causal, window, p, seed, off):
@@ -192,7 +224,7 @@ class _FlashAttention(torch.autograd.Function):
         bias = kb.bias if kb is not None else None
         bits = _keep_bits(bits, q, k, v, ctx.causal, ctx.window, p, seed, off)
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dq, dk, dv, ctx.scale, ctx.causal, ctx.window,
-                                 bias, p, seed, off, bits, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
+                                 bias, p, seed, off, bits)
         return dq, dk, dv, None, None, None, None, None
 
 
@@ -201,12 +233,18 @@ class _FlashAttentionPacked(torch.autograd.Function):
     the backward writes dQ/dK/dV into one packed gradient (no scatter/zero-fill copies)."""
 
     @staticmethod
-    def forward(ctx, qkv, scale, causal, window, kb, dropout_p):
+    def forward(ctx, qkv, scale, causal, window, kb, dropout_p, pre=None):
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
+        bits_in = None
+        if pre is not None and dropout_p > 0.0 and window <= 0 and \
+                pre.shape == (q.shape[0], q.shape[2], q.shape[1], k.shape[1], bool(causal), float(dropout_p)):
+            seed, off = pre.seed, pre.off
+            bits_in = pre.consume()
+        else:
+            seed, off = dropout_seed_offset(qkv.device) if dropout_p > 0.0 else (0, 0)
         bias = kb.bias if kb is not None else None
         o, lse, bits = ext().attention_fwd(q, k, v, scale, causal, window, bias, dropout_p, seed, off,
-                                           _store_bits(q, k, dropout_p))
+                                           _store_bits(q, k, dropout_p), bits_in)
         ctx.save_for_backward(qkv, o, lse, bits)
         ctx.kb = kb
         ctx.scale, ctx.causal, ctx.window = scale, causal, window
@@ -224,15 +262,16 @@ class _FlashAttentionPacked(torch.autograd.Function):
         bits = _keep_bits(bits, q, k, v, ctx.causal, ctx.window, p, seed, off)
         ext().attention_bwd_into(do.contiguous(), q, k, v, o, lse, dqkv[:, :, 0],
                                  dqkv[:, :, 1], dqkv[:, :, 2], ctx.scale, ctx.causal, ctx.window, bias, p, seed, off,
-                                 bits, int(FUSED_BWD[0]), FUSED_BWD_ERR[0])
+                                 bits)
         # a fresh buffer no one else holds: the packed rotary's backward may rotate it in place
         dqkv._smp_fresh_grad = True
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None
 
 
 def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, training=True, use_flash=True,
-                     mask=None, mask_value=-1e4):
-    """qkv: [b, s, 3, h, d] -> [b, s, h, d].  mask: optional [b|1, 1, s, s] bool (True = masked)."""
+                     mask=None, mask_value=-1e4, keep_bits=None):
+    """qkv: [b, s, 3, h, d] -> [b, s, h, d].  mask: optional [b|1, 1, s, s] bool (True = masked).
+    keep_bits: a ``prefetch_keep_bits`` result for this attention (used by the flash path)."""
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
     q = qkv[:, :, 0]
@@ -240,7 +279,8 @@ def attention_packed(qkv, causal=True, scale=None, dropout_p=0.0, window=None, t
     kbias = key_padding_bias(mask, q.shape[1], q.shape[1], mask_value) if mask is not None else None
     if use_flash and flash_supported(q, p, mask, kbias):
         _count_flash(kbias)
-        return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kbias, float(p))
+        return _FlashAttentionPacked.apply(qkv, float(scale), bool(causal), int(window or 0), kbias, float(p),
+                                           keep_bits)
     return attention(q, qkv[:, :, 1], qkv[:, :, 2], causal=causal, mask=mask, scale=scale, dropout_p=dropout_p,
                      window=window, training=training, use_flash=use_flash, mask_value=mask_value)
 

@@ -299,43 +299,35 @@ def test_materialised_chunked_d256(monkeypatch, causal):
     _check_grads((("dq", q.grad, qr.grad), ("dk", k.grad, kr.grad), ("dv", v.grad, vr.grad)), 3e-2)
 
 
-def _packed_grads(qkv, g, p, fused):
+def _packed_grads(qkv, g, p):
     from smdistributed_modelparallel_amd.ops import attention as A
 
-    old = A.FUSED_BWD[0]
-    err = torch.zeros(1, dtype=torch.int32, device="cuda")
-    A.FUSED_BWD[0], A.FUSED_BWD_ERR[0] = fused, err
-    try:
-        x = qkv.detach().clone().requires_grad_()
-        torch.manual_seed(1234)  # same dropout draw
-        o = A._FlashAttentionPacked.apply(x, 1.0 / math.sqrt(qkv.shape[-1]), True, 0, None, p)
-        o.backward(g)
-        torch.cuda.synchronize()
-    finally:
-        A.FUSED_BWD[0], A.FUSED_BWD_ERR[0] = old, None
-    return o.detach(), x.grad, int(err.item())
+    x = qkv.detach().clone().requires_grad_()
+    torch.manual_seed(1234)  # same dropout draw
+    o = A._FlashAttentionPacked.apply(x, 1.0 / math.sqrt(qkv.shape[-1]), True, 0, None, p)
+    o.backward(g)
+    torch.cuda.synchronize()
+    return o.detach(), x.grad
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("b,s,h", [(1, 64, 2), (2, 300, 3), (1, 520, 2), (2, 1024, 4), (1, 2048, 5)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_bwd_matches_fp32_and_is_deterministic(dt, b, s, h, p):
-    """csrc/kernels/attention_d64_fused.hip (one kernel: dK, dV and dQ with the ordered dQ
-    hand-off across key blocks) against the fp32 reference with the host-rebuilt keep mask,
-    against the split kernels, bitwise equal over two runs, error word 0.  Shapes cover one
-    key block (s 64), ragged tails (300, 520), and 4-8 key blocks (the hand-off chain)."""
+def test_packed_bwd_matches_fp32_and_is_deterministic(dt, b, s, h, p):
+    """Packed-QKV self-attention (d 64, causal) -- the forward reading the keep-bits kernel's
+    words, the dQ and dK/dV kernels -- against the fp32 reference with the host-rebuilt keep
+    mask, and bitwise equal over two runs.  Shapes cover one key block (s 64), ragged tails
+    (300, 520) and 4-32 key tiles.  (The single-kernel fused backward of round 5 was 4 % slower
+    than these split kernels and was removed.)"""
     from smdistributed_modelparallel_amd.ops.attention import flash_dropout_keep_mask
 
     torch.manual_seed(3)
     d = 64
     qkv = torch.randn(b, s, 3, h, d, device="cuda", dtype=dt)
     g = torch.randn(b, s, h, d, device="cuda", dtype=dt)
-    o1, g1, e1 = _packed_grads(qkv, g, p, True)
-    o2, g2, e2 = _packed_grads(qkv, g, p, True)
-    o3, g3, e3 = _packed_grads(qkv, g, p, False)
-    assert e1 == 0 and e2 == 0, (e1, e2)
-    assert torch.equal(o1, o3)
-    assert torch.equal(g1, g2), "fused backward must be bitwise reproducible"
+    o1, g1 = _packed_grads(qkv, g, p)
+    o2, g2 = _packed_grads(qkv, g, p)
+    assert torch.equal(o1, o2) and torch.equal(g1, g2), "flash attention must be bitwise reproducible"
     keep = None
     if p > 0.0:
         torch.manual_seed(1234)
@@ -345,9 +337,8 @@ def test_fused_bwd_matches_fp32_and_is_deterministic(dt, b, s, h, p):
         keep = flash_dropout_keep_mask(b, h, s, s, p, seed, off, device="cuda")
     qf = qkv.float().requires_grad_()
     orf = _ref(qf[:, :, 0], qf[:, :, 1], qf[:, :, 2], 1.0 / math.sqrt(d), True, keep=keep, p=p)
+    assert (o1.float() - orf).abs().max().item() < 3e-2
     orf.backward(g.float())
     gr = qf.grad
     names = ("dq", "dk", "dv")
     _check_grads([(names[i], g1[:, :, i], gr[:, :, i]) for i in range(3)], 3e-2)
-    # the split kernels agree to rounding (different fp32 summation orders)
-    _check_grads([(names[i], g1[:, :, i], g3[:, :, i].float()) for i in range(3)], 2e-2)

@@ -69,7 +69,8 @@ def test_gptneox20b_width_pp2_tp2_gpu():
 # loop over >= 2 key tiles -- checked three ways:
 # * every local gradient of the first step, before the update, against the same architecture run
 #   unpartitioned in that dtype (flash attention and the HIP RoPE / LayerNorm / GeLU / CE kernels on
-#   both sides), as a relative norm: 1e-2 (bf16), 5e-3 (fp16);
+#   both sides), as a relative norm: 1e-2 (bf16), 5e-3 (fp16) for the weights, 4x that for 1-D
+#   parameters (biases / LayerNorm: token sums with heavy cancellation);
 # * the same gradients against the independent plain-torch fp32 model of tests/torch_ref.py on the
 #   initial weights (no smp module, no HIP kernel): 5e-2 (bf16), 3e-2 (fp16) -- this bound also
 #   contains the reduced-precision rounding of the smp run itself;
@@ -90,9 +91,10 @@ def test_gptj6b_width_tp4_bf16_gpu():
 
 def test_gptneox20b_width_pp2_tp2_bf16_gpu():
     """GPT-NeoX 20B width (64 heads x 96: the d = 96 flash kernels, NeoX rotary 24) at PP2 x TP2
-    with optimizer-state sharding, in bf16, pipeline tensors over IPC."""
-    _run(4, 2, 2, 2, extra=dict(_BF16, base="gptneox-20b", cfg={"shard_optimizer_state": True}),
-         env={"SMP_P2P": "ipc"})
+    in bf16, pipeline tensors over IPC.  Without optimizer-state sharding, so that every rank
+    holds its full reduced gradients for the gradient check (the fp32 test above covers the
+    sharded optimizer at this architecture)."""
+    _run(4, 2, 2, 2, extra=dict(_BF16, base="gptneox-20b"), env={"SMP_P2P": "ipc"})
 
 
 def test_gpt2xl_width_tp2_fp16_dynamic_loss_scale_gpu():

