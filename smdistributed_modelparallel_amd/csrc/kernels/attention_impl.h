@@ -513,7 +513,7 @@ struct QInLds {
 // at GPT-2 XL shape); with dropout the same bound spills 35 registers and runs 2-3 % slower
 // (profiles/r5/dropout_hash_ab.md)
 template <typename T, int D, bool CAUSAL, bool DROP, bool BIAS, bool DMA = false>
-__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !DROP ? 4 : 2))
+__global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA ? 4 : 2))
     attn_fwd_kernel(AttnParams p) {
   constexpr int BM = 128, BN = 64, DS = LdsStride<D>::v;
   constexpr bool QLDS = QInLds<D>::v;
@@ -619,14 +619,15 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
   auto bits_ptr = [&](int t) {
     return p.drop_bits + bits_index(bh, ntiles64, (kv_begin + t * BN) >> 6, sq, qrow, hh);
   };
-  // word w of the block's tile-t slab (words [q][hh] are contiguous over the block's queries);
-  // rows past sq re-read the tile's last word (those queries are never stored)
+  // the block's tile-t slab (words [q][hh] are contiguous over the block's queries), gathered so
+  // that LDS slot wave * 64 + lane holds the word of (query wave * 32 + r, half hh): each lane then
+  // reads its own slot, conflict-free; rows past sq re-read the tile's last word (never stored)
   auto dma_bits = [&](int t, int b) {
-    const int64_t w = static_cast<int64_t>(qb) * KBW + wave * 64 + lane;
+    const int64_t w = static_cast<int64_t>(qb) * KBW + wave * 64 + 2 * r + hh;
     const int64_t base = (bh * ntiles64 + ((kv_begin + t * BN) >> 6)) * sq2;
     lds_dma4(p.drop_bits + base + (w < sq2 ? w : sq2 - 1), sKV + 4 * BN * DS + b * 2 * KBW + wave * 128);
   };
-  const int kb_slot = wave * 64 + 2 * r + hh;  // this lane's word in a tile's slab
+  const int kb_slot = wave * 64 + lane;  // this lane's word in a tile's slab
   uint32_t kb_cur = 0u, kb_nxt = 0u;
   if constexpr (BITS_LDS) {
     if (nt > 0) dma_bits(0, 0);
@@ -691,9 +692,6 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
       s0 = MF<T>::mma(ld8<T>(sK + ro.o[k]), qt, s0);
       s1 = MF<T>::mma(ld8<T>(sK + ro.o[k] + 32 * DS), qt, s1);
     }
-    // the tile's dropout keep flags from its keep word
-    uint32_t f0[4], f1[4];
-    if (DROP) unpack_keep(BITS_LDS ? sBits[kb_slot] : kb_cur, f0, f1);
     if (BIAS && tile_bias) {
       add_from_keys(s0, sB, hh);
       add_from_keys(s1, sB + 32, hh);
@@ -742,10 +740,13 @@ __global__ void __launch_bounds__(kThreads, D >= 256 ? 1 : (D == 64 && DMA && !D
     l_i += rs0 + rs1;
     typename MF<T>::e8 pf[4] = {pack8<T>(s0, 0), pack8<T>(s0, 1), pack8<T>(s1, 0), pack8<T>(s1, 1)};
     if (DROP) {  // the normaliser above used every p; only kept entries reach P.V
-      pf[0] = drop_packed(pf[0], f0[0], f0[1]);
-      pf[1] = drop_packed(pf[1], f0[2], f0[3]);
-      pf[2] = drop_packed(pf[2], f1[0], f1[1]);
-      pf[3] = drop_packed(pf[3], f1[2], f1[3]);
+      // the tile's keep word, read here so its flags are live only for these masks: register
+      // group g of half s has its flags at bits 8 i + 7 of w << (g + 4 s) (unpack_keep)
+      const uint32_t w = BITS_LDS ? sBits[kb_slot] : kb_cur;
+      pf[0] = drop_packed(pf[0], w, w << 1);
+      pf[1] = drop_packed(pf[1], w << 2, w << 3);
+      pf[2] = drop_packed(pf[2], w << 4, w << 5);
+      pf[3] = drop_packed(pf[3], w << 6, w << 7);
     }
 #pragma unroll
     for (int i = 0; i < D / 32; ++i) {

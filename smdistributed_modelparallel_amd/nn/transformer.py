@@ -415,12 +415,11 @@ class DistributedAttentionLayer(DistributedModule):
         else:
             causal = self.causal_mask_size is not None
             packed = not self.attention_in_fp32 and (_ROPE_PACKED or not self.rotary_dim)
-            pre = None
-            if (packed and mask is None and not self.window_size and self.training and self.attention_dropout_prob > 0.0
-                    and a.is_cuda and self.qkv_weight.dtype in (torch.bfloat16, torch.float16)
-                    and d in FLASH_HEAD_DIMS and ((not state.initialized) or state.cfg.amd_fused_attention)):
-                # dropout keep bits on a side stream beside the QKV projection GEMM
-                pre = prefetch_keep_bits(B, lh, s, s, causal, self.attention_dropout_prob, a.device, a)
+            # dropout keep bits on a side stream: launched by the enclosing layer before its
+            # first LayerNorm (early_keep_bits), else here, beside the QKV projection GEMM
+            pre, self._early_bits = self._early_bits, None
+            if pre is None and packed and mask is None:
+                pre = self.early_keep_bits(a)
             if packed and self.rotary_dim:
                 # rotary on the packed buffer, in place on the projection's 2-D (non-view) output:
                 # one dqkv buffer in the backward, no per-view zero-filled gradients to add up
@@ -456,6 +455,23 @@ class DistributedAttentionLayer(DistributedModule):
         ctx = ctx.reshape(B, s, lh * d)
         return linear(ctx, self.dense_weight, self.dense_bias,
                       fwd_ar=fwd_allreduce_async if self._tp > 1 and reduce else None)
+
+    _early_bits = None
+
+    def early_keep_bits(self, x):
+        """Start this layer's attention-dropout keep bits (ops.attention.prefetch_keep_bits) for
+        an input shaped like ``x`` [B, s, h] -- when the packed flash path with dropout will run
+        (self-attention, no padding mask, no window).  The enclosing layer calls it before its
+        LayerNorm, so the VALU-bound hash overlaps that HBM-bound kernel and the QKV GEMM."""
+        if not (self.training and self.attention_dropout_prob > 0.0 and x.is_cuda and not self.window_size
+                and not self.cross_attention and not self._mem and not self.attention_in_fp32
+                and self.qkv_weight.dtype in (torch.bfloat16, torch.float16)
+                and self.attention_head_size in FLASH_HEAD_DIMS
+                and ((not state.initialized) or state.cfg.amd_fused_attention)):
+            return None
+        B, s = x.shape[0], x.shape[1]
+        return prefetch_keep_bits(B, self.local_heads, s, s, self.causal_mask_size is not None,
+                                  self.attention_dropout_prob, x.device, x)
 
     def _core_memory(self, a, mask):
         """optimize='memory': a is [B, s, h/tp] (hidden-sharded).  Partial QKV products
@@ -638,6 +654,9 @@ class _Deferred:
 
 
 _FUSE_CROSS_LAYER = [os.environ.get("SMP_FUSE_CROSS_LAYER_RESIDUAL", "1") != "0"]
+# SMP_ATTN_BITS_PREFETCH=early (default): keep bits launched before the layer's first LayerNorm;
+# =1: before the QKV GEMM; =0: generated in front of the attention forward
+_EARLY_BITS = os.environ.get("SMP_ATTN_BITS_PREFETCH", "early") == "early"
 # rotary on the packed QKV buffer (SMP_ROPE_PACKED=0: per-view rotation, the A/B baseline)
 _ROPE_PACKED = os.environ.get("SMP_ROPE_PACKED", "1") != "0"
 
@@ -722,6 +741,8 @@ class DistributedTransformerLayer(DistributedModule):
             else:
                 hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:
+            if mask is None and _EARLY_BITS:
+                at._early_bits = at.early_keep_bits(hidden)
             if deferred is not None:
                 # the previous layer's MLP dropout + residual add, fused into this LN1
                 a, hidden = at.pre_layernorm_module.forward_add(deferred[0], hidden, deferred[1])
