@@ -65,9 +65,11 @@ def _check_audit_fields(rec, world, dp, pp):
 
 
 def test_bench_pp_layout_four_ranks():
-    """N = 4 defaults to BASELINE config 2's layout (PP=4 interleaved): the JSON line says so."""
+    """N = 4 defaults to BASELINE config 2's layout (PP=4 interleaved): the JSON line says so.
+    7 steps: the PP layout is static_mode, so the last two replay the frozen schedule (the
+    driver's multi-GPU runs take that path after their warmup)."""
     args = ["bench.py", "--gpus", "4", "--model", "gpt2-tiny", "--layers", "4", "--seq", "32", "--mbs", "1",
-            "--microbatches", "4", "--steps", "1", "--warmup", "1"]
+            "--microbatches", "4", "--steps", "4", "--warmup", "3"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=4",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
     env = dict(os.environ, OMP_NUM_THREADS="1")
@@ -76,12 +78,13 @@ def test_bench_pp_layout_four_ranks():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     rec = json.loads(lines[0])
+    assert "pipeline schedule frozen" in r.stdout + r.stderr, r.stdout[-3000:]
     _check_audit_fields(rec, world=4, dp=1, pp=4)
     assert rec["p2p"]["mode"] is not None
     cfg = rec["config"]
     assert cfg["parallelism"] == "pp4xtp1xdp1" and cfg["layout"] == "pp" and cfg["pipeline"] == "interleaved"
     assert cfg["microbatches"] == 4 and cfg["global_batch"] == 4 and sum(cfg["layer_split"]) == 4
-    assert rec["n_gpus"] == 4
+    assert rec["n_gpus"] == 4 and rec["steps"] == 4
 
 
 def test_bench_node_layout_eight_ranks():
