@@ -48,9 +48,9 @@ class FusedLayerNorm(nn.Module):
                 self.weight.fill_(1.0)
                 self.bias.zero_()
 
-    def forward_add(self, x, residual, dropout_p=0.0):
+    def forward_add(self, x, residual, dropout_p=0.0, drawn=None):
         """(LN(dropout(x) + residual), dropout(x) + residual) in one kernel."""
-        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout_p)
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout_p, drawn)
 
     def forward_passthrough(self, x):
         """(LN(x), x) where x's two gradient paths (LN input, residual branch) are summed

@@ -35,6 +35,7 @@ from ..backend.exceptions import DistTransformerConfigError, SMPInvalidArgumentE
 from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
 from ..ops.attention import FLASH_HEAD_DIMS, attention_packed, prefetch_keep_bits
+from ..ops.dropout import dropout_seed_offset
 from ..ops.cross_entropy import cross_entropy
 from ..ops.dropout import add3
 from ..ops.dropout import dropout_add as _dropout_add
@@ -743,11 +744,15 @@ class DistributedTransformerLayer(DistributedModule):
             else:
                 hidden = hidden + at.dropout(attn) + out.dropout(mlp)
         else:
+            drawn = None
             if mask is None and _EARLY_BITS:
+                if deferred is not None and deferred[1] > 0.0 and hidden.is_cuda:
+                    # the previous layer's MLP dropout draws first, as in the unfused order
+                    drawn = dropout_seed_offset(hidden.device)
                 at._early_bits = at.early_keep_bits(hidden)
             if deferred is not None:
                 # the previous layer's MLP dropout + residual add, fused into this LN1
-                a, hidden = at.pre_layernorm_module.forward_add(deferred[0], hidden, deferred[1])
+                a, hidden = at.pre_layernorm_module.forward_add(deferred[0], hidden, deferred[1], drawn)
             elif at.pre_layernorm and hasattr(at.pre_layernorm_module, "forward_passthrough"):
                 # hidden feeds LN1 and the residual add: its two gradients meet in the LN kernel
                 a, hidden = at.pre_layernorm_module.forward_passthrough(hidden)

@@ -89,9 +89,12 @@ class _FusedAddLayerNorm(torch.autograd.Function):
     backward; the x branch then gets dropout's backward (mask regenerated from the hash)."""
 
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, dropout_p):
+    def forward(ctx, x, residual, weight, bias, eps, dropout_p, drawn):
         x2, r2 = x.contiguous(), residual.contiguous()
-        seed, off = dropout_seed_offset(x.device) if dropout_p > 0.0 else (0, 0)
+        if dropout_p <= 0.0:
+            seed, off = 0, 0
+        else:
+            seed, off = drawn if drawn is not None else dropout_seed_offset(x.device)
         y, mean, rstd, s = ext().layernorm_fwd(x2, r2, weight, bias, eps, dropout_p, seed, off)
         ctx.save_for_backward(s, weight, mean, rstd)
         ctx.bias = bias
@@ -109,7 +112,7 @@ class _FusedAddLayerNorm(torch.autograd.Function):
         # the x branch's dropout backward comes out of the LN backward kernel itself (one pass
         # writing dx and dx * keep / (1 - p)) instead of a separate read of dx
         dx, dw, db, dxin = _ln_bwd(dy.contiguous(), s, w, ctx.bias, mean, rstd, need_w, need_b, dres, drop=ctx.drop)
-        return dxin, dx, dw, db, None, None
+        return dxin, dx, dw, db, None, None, None
 
 
 class _MixedLayerNorm(torch.autograd.Function):
@@ -156,10 +159,11 @@ def layer_norm_passthrough(x, weight, bias, eps=1e-5):
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps), x
 
 
-def add_layer_norm(x, residual, weight, bias, eps=1e-5, dropout_p=0.0):
-    """Returns (LN(dropout(x) + residual), dropout(x) + residual)."""
+def add_layer_norm(x, residual, weight, bias, eps=1e-5, dropout_p=0.0, drawn=None):
+    """Returns (LN(dropout(x) + residual), dropout(x) + residual).  ``drawn``: the dropout's
+    (seed, offset), drawn earlier with ``dropout_seed_offset`` to keep a generator order."""
     if x.is_cuda:
-        return _FusedAddLayerNorm.apply(x, residual, weight, bias, eps, float(dropout_p))
+        return _FusedAddLayerNorm.apply(x, residual, weight, bias, eps, float(dropout_p), drawn)
     if dropout_p > 0.0:
         x = torch.nn.functional.dropout(x, dropout_p, True)
     s = x + residual
