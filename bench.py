@@ -234,7 +234,7 @@ def main():
         cfg["pipeline"] = "interleaved"
         # the step's module graph is identical every step: freeze and replay its schedule
         # (engine record-and-replay; the dynamic scheduler is the default otherwise)
-        cfg["static_mode"] = True
+        cfg["static_mode"] = os.environ.get("SMP_BENCH_STATIC", "1") != "0"
         if os.environ.get("SMP_BENCH_AUTO_PARTITION", "0") == "1":
             cfg["auto_partition"] = True
         else:
@@ -324,8 +324,13 @@ def main():
     comm_timer.reset()
     comm_timer.enabled = True  # two HIP events around each communication wait (no sync)
     t0 = time.perf_counter()
+    step_times = os.environ.get("SMP_BENCH_STEP_TIMES") == "1"  # diagnostic: synchronises every step
     for i in range(args.steps):
         out = one(i)
+        if step_times:
+            torch.cuda.synchronize() if torch.cuda.is_available() else None
+            print(f"rank {smp.rank()} timed step {i} ends at {1e3 * (time.perf_counter() - t0):.1f} ms",
+                  file=sys.stderr, flush=True)
     sync()
     dt = time.perf_counter() - t0
     comm_timer.enabled = False
