@@ -28,3 +28,31 @@ tot = sum(v[0] for v in agg.values())
 print(f"step {(t1 - t0) / 1e6:.1f} ms wall, {tot / 1e3:.1f} ms kernels")
 for k, v in sorted(agg.items(), key=lambda x: -x[1][0])[:40]:
     print(f"{v[0] / 1e3:8.2f} ms {v[1]:4d} {v[0] / v[1]:8.1f} us  {k}")
+
+# concurrency: busy union of the step (wall - union = idle gaps) and, per side-stream kernel
+# family, how much of its time ran beside another kernel
+iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in last)
+union, cs, ce = 0, None, None
+for s, e, _ in iv:
+    if cs is None or s > ce:
+        if cs is not None:
+            union += ce - cs
+        cs, ce = s, e
+    else:
+        ce = max(ce, e)
+if cs is not None:
+    union += ce - cs
+print(f"busy union {union / 1e6:.1f} ms, idle gaps {(t1 - t0 - union) / 1e6:.1f} ms, "
+      f"overlapped kernel time {(tot * 1e3 - union) / 1e6:.1f} ms")
+for fam in ("keep_bits", "oneshot", "device_copy"):
+    mine = [(s, e) for s, e, n in iv if fam in n]
+    if not mine:
+        continue
+    others = [(s, e) for s, e, n in iv if fam not in n]
+    ov = 0
+    for s, e in mine:
+        for os_, oe in others:
+            if oe > s and os_ < e:
+                ov += min(e, oe) - max(s, os_)
+    dur = sum(e - s for s, e in mine)
+    print(f"{fam}: {dur / 1e6:.2f} ms, {100.0 * ov / max(dur, 1):.0f} % of it beside other kernels")
