@@ -432,6 +432,7 @@ typedef WMF16<bf16>::e8 e8b;
 template <typename T>
 struct Regs {
   f32x4 acc[2][2][4][2];                       // [qa][qb][i][j]
+  f32x4 accs[2];                               // CS 2: row sums of A, 16 rows (i = wn) per qa
   typename WMF16<T>::e8 fa[4][2];              // A fragments of the current qa: [i][k-step]
   typename WMF16<T>::e8 fb[2][2][2];           // B fragments: [qb][j][k-step]
 };
@@ -479,9 +480,31 @@ __device__ __forceinline__ void mfma_quadrant(Regs<T>& R, bool act, bool cs_quad
   }
 }
 
+// CS 2 (any K, e.g. K % 256 == 0 where no quadrant idles): in the last K tile's workgroups each
+// wave also multiplies ONE of its four A fragments of the phase's fresh A half (i = wave column)
+// by the ones fragment -- 2 extra MFMAs in phases 0 and 2, spread over the four wave columns.
+template <typename T, int QA>
+__device__ __forceinline__ void mfma_rowsum(Regs<T>& R, int wn, const typename WMF16<T>::e8& ones) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    // wn is wave-uniform (SGPR): a scalar branch selects the fragment, no dynamic register index
+    if (wn == 0)
+      R.accs[QA] = WMF16<T>::mma(R.fa[0][s], ones, R.accs[QA]);
+    else if (wn == 1)
+      R.accs[QA] = WMF16<T>::mma(R.fa[1][s], ones, R.accs[QA]);
+    else if (wn == 2)
+      R.accs[QA] = WMF16<T>::mma(R.fa[2][s], ones, R.accs[QA]);
+    else
+      R.accs[QA] = WMF16<T>::mma(R.fa[3][s], ones, R.accs[QA]);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
 // One phase P (0..3) of a tile whose slots are set PAR (0, 1).  ISSUE: stage half-tile P of
 // the next tile into set PAR ^ 1.  VM: the counted wait ending the load segment.
-template <typename T, bool CS, int P, int PAR, int VM_ISSUE, int VM_LAST>
+// CS: 0 no bias gradient, 1 idle-quadrant row sums (K % 256 in [1, 128]), 2 extra row-sum MFMAs.
+template <typename T, int CS, int P, int PAR, int VM_ISSUE, int VM_LAST>
 __device__ __forceinline__ void phase(Regs<T>& R, const Geo& G, const uint16_t* smem, const uint16_t* nxtA,
                                       const uint16_t* nxtB, bool issue, int wave, const bool (&act)[2][2],
                                       bool cs_q1, const typename WMF16<T>::e8& ones) {
@@ -517,12 +540,15 @@ __device__ __forceinline__ void phase(Regs<T>& R, const Geo& G, const uint16_t* 
     wait_vm<VM_LAST>();
   bar();
   // ---- MFMA segment
-  mfma_quadrant<T, QA, QB>(R, act[QA][QB], CS && QB == 1 && cs_q1 && act[QA][0], ones);
+  mfma_quadrant<T, QA, QB>(R, act[QA][QB], CS == 1 && QB == 1 && cs_q1 && act[QA][0], ones);
+  if constexpr (CS == 2 && (P == 0 || P == 2)) {
+    if (cs_q1 && act[QA][0]) mfma_rowsum<T, QA>(R, wave & 3, ones);
+  }
   bar();
 }
 
 // a whole tile; issue: there is a next tile to stage (else this is the last tile)
-template <typename T, bool CS, int PAR>
+template <typename T, int CS, int PAR>
 __device__ __forceinline__ void tile(Regs<T>& R, const Geo& G, const uint16_t* smem, const uint16_t* nxtA,
                                      const uint16_t* nxtB, bool issue, int wave, const bool (&act)[2][2],
                                      bool cs_q1, const typename WMF16<T>::e8& ones) {
@@ -535,7 +561,7 @@ __device__ __forceinline__ void tile(Regs<T>& R, const Geo& G, const uint16_t* s
 }
 }  // namespace pp
 
-template <typename T, bool CS>
+template <typename T, int CS>
 __global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __restrict__ A,
                                                           const uint16_t* __restrict__ B, float* __restrict__ ws,
                                                           int64_t Tn, int N, int K, int64_t lda, int64_t ldb,
@@ -585,7 +611,8 @@ __global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __rest
     for (int qb = 0; qb < 2; ++qb) act[qa][qb] = (n0 + qa * 128 + wm * 64 < N) && (k0 + qb * 128 + wn * 32 < K);
   // bias-gradient quadrant: the last K tile with no valid column past 128 -> wave column 0
   // turns its (qa, 1) quadrants into row sums of A
-  const bool cs_q1 = CS && wn == 0 && tk == tiles_k - 1 && K - k0 <= 128;
+  // (CS 2: every wave of the last K tile's workgroups sums its 16 rows i = wn of each A half)
+  const bool cs_q1 = CS == 1 ? (wn == 0 && tk == tiles_k - 1 && K - k0 <= 128) : (CS == 2 && tk == tiles_k - 1);
 
   Regs<T> R;
 #pragma unroll
@@ -596,6 +623,7 @@ __global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __rest
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) R.acc[a][b2][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  R.accs[0] = R.accs[1] = f32x4{0.f, 0.f, 0.f, 0.f};
   typename WMF16<T>::e8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = 1.0f;
@@ -648,7 +676,17 @@ __global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __rest
             if (nb + r < N) out[static_cast<int64_t>(nb + r) * K + k] = R.acc[qa][qb][i][j][r];
         }
       }
-  if (CS && cs_q1 && col_l == 0) {
+  if (CS == 2 && cs_q1 && col_l == 0) {
+    float* cso = cs + static_cast<int64_t>(split) * N;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+      const int nb = n0 + qa * 128 + wm * 64 + wn * 16 + rq;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nb + r < N) cso[nb + r] = R.accs[qa][r];
+    }
+  }
+  if (CS == 1 && cs_q1 && col_l == 0) {
     float* cso = cs + static_cast<int64_t>(split) * N;
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
@@ -662,7 +700,7 @@ __global__ __launch_bounds__(512, 2) void wgrad_pp_kernel(const uint16_t* __rest
   }
 }
 
-template <typename T, bool CS>
+template <typename T, int CS>
 int launch_pp(const uint16_t* pa, const uint16_t* pb, float* ws, int64_t tokens, int n, int k, int64_t lda,
               int64_t ldb, int64_t t_split, int grid, hipStream_t s, float* cs) {
   static bool attr_set = false;
@@ -761,14 +799,23 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
     return e != nullptr && strcmp(e, "glds") == 0;
   }();
   const bool use_glds = impl == 0 || (impl < 0 && env_glds);
-  const bool pp_ok = !use_glds && lda < (1 << 24) && ldb < (1 << 24) && (bias == nullptr || wgrad_pp_cs_ok(k));
+  // (a bias gradient: idle-quadrant sums where K % 256 leaves a quadrant idle, else the extra
+  // row-sum MFMAs; SMP_WGRAD_PP_CS=idle keeps the round-5 rule -- other K to the round-4 kernel)
+  static const bool cs_idle_only = [] {
+    const char* e = getenv("SMP_WGRAD_PP_CS");
+    return e != nullptr && strcmp(e, "idle") == 0;
+  }();
+  const bool pp_ok = !use_glds && lda < (1 << 24) && ldb < (1 << 24) &&
+                     (bias == nullptr || wgrad_pp_cs_ok(k) || !cs_idle_only);
   if (pp_ok) {
-    if (bias != nullptr)
-      launch_pp<bf16, true>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
+    if (bias != nullptr && wgrad_pp_cs_ok(k))
+      launch_pp<bf16, 1>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
+    else if (bias != nullptr)
+      launch_pp<bf16, 2>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);
     else if (dt == BF16)
-      launch_pp<bf16, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
+      launch_pp<bf16, 0>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
     else if (dt == F16)
-      launch_pp<f16, false>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
+      launch_pp<f16, 0>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, nullptr);
     else
       return -2;
   } else if (bias != nullptr || dt == BF16)

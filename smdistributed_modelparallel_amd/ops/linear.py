@@ -244,8 +244,18 @@ _WGRAD_DBIAS_MIN_N = 4096 if os.environ.get("SMP_WGRAD_DBIAS", "1") == "wide" el
 
 
 def _wgrad_dbias_free(k):
-    """The kernel's idle-wave column-sum mode applies to input width ``k``."""
+    """A wave column of the weight-gradient kernel idles in the last K tile for input width ``k``
+    and sums the bias gradient there at no cost: worth forcing the kernel over a faster library
+    pick (it saves the separate full read of dY)."""
     return 0 < k % 256 <= 192
+
+
+def _wgrad_dbias_rowsum(k):
+    """Any other ``k``: the ping-pong kernel sums the bias gradient with two extra MFMAs per wave
+    in two of each tile's four phases of the last K tile's workgroups -- taken when the kernel is
+    the pick anyway (GPT-2 XL fc2, K = 6400: -1 ms per step same box), not forced over a library
+    pick (the NeoX shard lost 3 % that way, `profiles/r6/wgrad_rowsum_bias.md`)."""
+    return os.environ.get("SMP_WGRAD_IMPL") != "glds" and os.environ.get("SMP_WGRAD_PP_CS") != "idle"
 
 
 def _wgrad_accumulate(g, dy2, x2, dbias=None):
@@ -254,8 +264,9 @@ def _wgrad_accumulate(g, dy2, x2, dbias=None):
     when that happened (False: the caller computes them)."""
     if _wgrad_native_ok(g, dy2, x2):
         s = _wgrad_kernel_splits(g, dy2, x2)
+        cheap = _wgrad_dbias_free(x2.shape[1]) or dy2.shape[1] >= _WGRAD_DBIAS_MIN_N
         fuse = (dbias is not None and _WGRAD_DBIAS and dy2.dtype == torch.bfloat16
-                and (_wgrad_dbias_free(x2.shape[1]) or dy2.shape[1] >= _WGRAD_DBIAS_MIN_N))
+                and (cheap or (s != 0 and _wgrad_dbias_rowsum(x2.shape[1]))))
         if fuse and s == 0:
             # the fused bias pass makes the kernel the cheaper choice (it saves a full read of dY)
             s = _wgrad_dbias_splits(dy2, x2)

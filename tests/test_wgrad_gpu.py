@@ -201,11 +201,13 @@ def test_wgrad_impls_match_fp32(shape, impl):
         assert rel < 1e-5, (splits, rel)
 
 
-@pytest.mark.parametrize("shape", [(4096, 1600, 1600), (8256, 4800, 1600), (5000, 392, 1048), (4160, 1040, 1000)])
+@pytest.mark.parametrize("shape", [(4096, 1600, 1600), (8256, 4800, 1600), (5000, 392, 1048), (4160, 1040, 1000),
+                                   (4096, 1600, 6400), (4096, 1536, 6144), (2048, 520, 512), (4096, 800, 1200)])
 def test_wgrad_pp_bias_quadrant(shape):
-    """The ping-pong kernel's bias-gradient quadrant (K % 256 in [1, 128]: B fragment = ones in
-    the idle qb = 1 quadrant of the last K tile) against fp32 column sums, beside the
-    round-4 kernel's modes (K % 256 > 128: LDS column sums) on the same call API."""
+    """The ping-pong kernel's bias-gradient sums against fp32 column sums: the idle-quadrant mode
+    (K % 256 in [1, 128]: B fragment = ones in the idle qb = 1 quadrant of the last K tile) and
+    the row-sum MFMA mode for every other K (K % 256 == 0 as in the GPT-J / NeoX shards, and
+    K % 256 > 128), beside the round-4 kernel's modes on the same call API."""
     from smdistributed_modelparallel_amd.ops._ext import ext
 
     T, N, K = shape
