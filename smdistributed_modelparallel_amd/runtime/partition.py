@@ -344,15 +344,22 @@ class ModulePartitioner:
 
 
 def auto_partition(model, step_fn, mb_inputs):
-    """Rank 0 traces + partitions; everyone receives {module_name: partition}."""
+    """Rank 0 traces + partitions; everyone receives {module_name: partition}.  With tensor
+    parallelism the traced forward runs TP collectives, so rank 0's TP peers (same pipeline stage
+    and replica) run the same trace beside it -- told by rank 0 whether it traces -- and discard
+    the results."""
     core = state.core
     mm = state.module_manager
     mm.name_modules_and_create_parent_map()
+    cfg = state.cfg
+    dev = state.device if (model.trace_device == "gpu" and state.use_gpu) else torch.device("cpu")
+    tp_peers = core.tp_size() > 1
     if core.rank() == 0:
-        cfg = state.cfg
         trace = None
-        if not cfg.skip_tracing and model.size() <= SKIP_TRACING_MODEL_SIZE_THRESHOLD_BYTES and mb_inputs:
-            dev = state.device if (model.trace_device == "gpu" and state.use_gpu) else torch.device("cpu")
+        do_trace = bool(not cfg.skip_tracing and model.size() <= SKIP_TRACING_MODEL_SIZE_THRESHOLD_BYTES and mb_inputs)
+        if tp_peers:
+            state.comm.broadcast(do_trace, CommGroup.TP_GROUP)
+        if do_trace:
             a, k = mb_inputs[0]
             try:
                 trace = trace_model(model, state.step_func[state.current_step_fn_id], a, k, dev)
@@ -370,6 +377,13 @@ def auto_partition(model, step_fn, mb_inputs):
             raise
         state.comm.broadcast(info, CommGroup.WORLD)
     else:
+        if tp_peers and 0 in core.get_group_ranks(CommGroup.TP_GROUP):
+            if state.comm.recv_broadcast(0, CommGroup.TP_GROUP) and mb_inputs:
+                a, k = mb_inputs[0]
+                try:
+                    trace_model(model, state.step_func[state.current_step_fn_id], a, k, dev)
+                except Exception:  # noqa: B902 - rank 0 reports; its partition still comes below
+                    pass
         info = state.comm.recv_broadcast(0, CommGroup.WORLD)
         if "__error__" in info:
             raise PartitionError(f"auto-partitioning failed on rank 0: {info['__error__']}")

@@ -117,6 +117,14 @@ class DistributedModel(nn.Module):
         mm.simplify_tensor_parallelism_modules(module)
         module = self._replace_tp_counterparts(module)
         self.module = module
+        hf_cfg = getattr(module, "config", None)
+        if state.core.pp_size() > 1 and getattr(hf_cfg, "use_cache", False) is True:
+            # a Hugging Face model's KV-cache object would be passed from block to block across
+            # pipeline stages (its key / value tensors then reach later blocks as inputs with no
+            # path to their outputs); training does not use it
+            hf_cfg.use_cache = False
+            logger.info("pipeline parallelism: the model config's use_cache turned off (KV caches do not cross "
+                        "pipeline stages)")
         mm.set_main_module(module)
         mm.name_modules_and_create_parent_map()
         state.engine = PipelineEngine(state)

@@ -13,3 +13,37 @@ def test_train_gpt_pp2_checkpoint_resume(tmp_path):
     outs = run_script("examples/train_gpt.py", 2, common + ["--steps", "6"], timeout=240)
     assert "resumed from" in outs[0] and "at step 4" in outs[0], outs[0][-2000:]
     assert "step 5 loss" in outs[0] and "step 1 loss" not in outs[0]
+
+
+def test_train_gpt_pp2_tp2_auto_partition():
+    """PP=2 x TP=2 with auto-partitioning: rank 0 traces the model, whose forward runs TP
+    collectives -- its TP peer must run the same trace (this deadlocked before round 6)."""
+    args = ["--cpu", "--model", "gpt2-tiny", "--layers", "4", "--seq", "32", "--mbs", "2", "--microbatches", "2",
+            "--pp", "2", "--tp", "2", "--steps", "3"]
+    outs = run_script("examples/train_gpt.py", 4, args, timeout=300)
+    assert "TRAIN_DONE" in outs[0] and "step 3 loss" in outs[0], outs[0][-2000:]
+
+
+_HF = ["--cpu", "--layers", "4", "--hidden", "64", "--heads", "4", "--vocab", "97", "--seq", "32", "--mbs", "2",
+       "--microbatches", "2"]
+
+
+def test_train_hf_gpt2_pp2_checkpoint_resume(tmp_path):
+    """examples/train_hf.py: a transformers GPT2LMHeadModel auto-partitioned over 2 pipeline
+    stages (its config's use_cache is turned off: a KV-cache object cannot cross stages), partial
+    checkpoints, and a resumed second launch."""
+    common = _HF + ["--family", "gpt2", "--pp", "2", "--ckpt-dir", str(tmp_path), "--ckpt-every", "2"]
+    outs = run_script("examples/train_hf.py", 2, common + ["--steps", "4"], timeout=300)
+    assert "TRAIN_DONE" in outs[0] and "step 4 loss" in outs[0], outs[0][-2000:]
+    outs = run_script("examples/train_hf.py", 2, common + ["--steps", "6"], timeout=300)
+    assert "resumed from" in outs[0] and "at step 4" in outs[0], outs[0][-2000:]
+    assert "step 5 loss" in outs[0] and "step 1 loss" not in outs[0]
+
+
+def test_train_hf_gptneox_pp2_tp2():
+    """A transformers GPTNeoXForCausalLM created under smp.model_creation(tensor_parallelism=True)
+    becomes smp.nn's DistributedTransformerLMHead (TP=2) and is pipelined over 2 stages: BASELINE
+    config 4's layout in miniature, through the HF entry point."""
+    outs = run_script("examples/train_hf.py", 4, _HF + ["--family", "gpt_neox", "--pp", "2", "--tp", "2",
+                                                         "--steps", "3"], timeout=300)
+    assert "TRAIN_DONE" in outs[0] and "step 3 loss" in outs[0], outs[0][-2000:]
