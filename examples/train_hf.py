@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--activation-checkpointing", action="store_true", help="checkpoint every transformer block")
+    ap.add_argument("--shard-optimizer-state", action="store_true")
+    ap.add_argument("--delayed-init", action="store_true")
     ap.add_argument("--ckpt-dir", default=None)
     ap.add_argument("--ckpt-every", type=int, default=0)
     ap.add_argument("--cpu", action="store_true")
@@ -78,11 +81,24 @@ def main():
         "auto_partition": True,
         "ddp": world > 1,
         "bf16": not args.cpu,
+        "shard_optimizer_state": args.shard_optimizer_state,
+        "delayed_parameter_initialization": args.delayed_init,
     })
     torch.manual_seed(1234)
-    with smp.model_creation(tensor_parallelism=args.tp > 1, dtype=torch.float32 if args.cpu else torch.bfloat16):
-        net = hf_model(args)
+    with smp.delay_param_initialization(enabled=args.delayed_init):
+        with smp.model_creation(tensor_parallelism=args.tp > 1,
+                                dtype=torch.float32 if args.cpu else torch.bfloat16):
+            net = hf_model(args)
     model = smp.DistributedModel(net)
+    if args.activation_checkpointing:
+        # the transformer blocks: HF ModuleList children, or smp.nn's layer stack after the TP swap
+        inner = model.get_module()
+        stack = getattr(getattr(inner, "transformer", None), "seq_layers", None)
+        if stack is None:
+            body = getattr(inner, "transformer", None) or getattr(inner, "gpt_neox", None)
+            stack = getattr(body, "h", None) or getattr(body, "layers", None)
+        for block in stack:
+            smp.set_activation_checkpointing(block)
     opt = smp.DistributedOptimizer(torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=0.01))
 
     start = 0

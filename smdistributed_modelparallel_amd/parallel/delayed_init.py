@@ -6,7 +6,7 @@ partitioning only the *local* ones are allocated (on the device) and initialised
 model larger than host memory can be built.  Implementation: construction happens on
 the ``meta`` device; at post-partition each local module with meta parameters is
 allocated with ``to_empty`` on the device and re-initialised by its own
-``reset_parameters`` (or the module's ``_init_weights`` for HF-style models), non-local
+``reset_parameters`` and then, for Hugging Face models, the model's ``_init_weights``; non-local
 meta parameters become empty tensors.
 """
 import os
@@ -126,13 +126,20 @@ def materialize_local(model, owner=None, me=None):
                     torch.empty(0, dtype=b.dtype, device=device)
         if fresh:
             to_init.append(m)
+    # a Hugging Face model's own initialiser wins over the torch module defaults (GPT-2's token
+    # embedding is N(0, 0.02) there, N(0, 1) by nn.Embedding.reset_parameters): the default runs
+    # first so module types the HF initialiser does not cover still get initialised
+    hf_init = getattr(root, "_init_weights", None) if hasattr(root, "config") else None
     for m in to_init:
         init = state.param_initializers.get(m)
         with torch.no_grad():
             if init is not None:
                 init(m)
-            elif hasattr(m, "reset_parameters") and callable(m.reset_parameters):
+                continue
+            if hasattr(m, "reset_parameters") and callable(m.reset_parameters):
                 m.reset_parameters()
+                if hf_init is not None:
+                    hf_init(m)
             elif hasattr(root, "_init_weights"):
                 root._init_weights(m)
     return mapping

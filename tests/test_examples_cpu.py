@@ -47,3 +47,16 @@ def test_train_hf_gptneox_pp2_tp2():
     outs = run_script("examples/train_hf.py", 4, _HF + ["--family", "gpt_neox", "--pp", "2", "--tp", "2",
                                                          "--steps", "3"], timeout=300)
     assert "TRAIN_DONE" in outs[0] and "step 3 loss" in outs[0], outs[0][-2000:]
+
+
+def test_train_hf_gpt2_delayed_init_uses_hf_initialiser():
+    """Delayed parameter initialisation of a transformers model materialises each stage's
+    parameters with the model's own initialiser (GPT-2: N(0, 0.02) embeddings), not the torch
+    module defaults (nn.Embedding: N(0, 1), which put the first loss near 40 instead of ln V)."""
+    import math
+    import re
+
+    outs = run_script("examples/train_hf.py", 2, _HF + ["--family", "gpt2", "--pp", "2", "--delayed-init",
+                                                         "--activation-checkpointing", "--steps", "2"], timeout=300)
+    first = float(re.search(r"step 1 loss ([0-9.]+)", outs[0]).group(1))
+    assert abs(first - math.log(97)) < 0.3, first
