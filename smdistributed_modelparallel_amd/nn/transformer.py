@@ -713,9 +713,17 @@ class DistributedTransformerLayer(DistributedModule):
         if isinstance(inputs[-1], _Deferred):
             deferred, inputs = (inputs[-2], inputs[-1].p), inputs[:-2]
         hidden, mask = inputs[0], inputs[1]
-        if self._tp > 1 and self.input_layer and not _prescaled():
+        # the tuple handed on: the TP input layer replaces the mask (and a cross-attention
+        # stack's encoder states / mask) by their TP-group batch forms for the layers after it
+        rest = list(inputs[1:])
+        tp_region = self._tp > 1 and not _prescaled()
+        if tp_region and self.input_layer:
             hidden = _enter_tp(hidden, self._mem, self.hidden_size)
             mask = _gather_mask(mask)
+            rest[0] = mask
+            if self.add_cross_attention and len(rest) >= 3 and torch.is_tensor(rest[1]):
+                rest[1] = _enter_tp(rest[1], self._mem, self.hidden_size)
+                rest[2] = _gather_mask(rest[2])
         if self.fp32_residual_addition:
             # fp32 residual stream from the first transformer layer on (reference
             # `torch/nn/transformer.py:890-894`; a no-op on the later layers and stages, which
@@ -772,21 +780,28 @@ class DistributedTransformerLayer(DistributedModule):
             if self.add_cross_attention:
                 ca = self.cross_attention
                 c_in = ca.pre_layernorm_module(hidden) if ca.pre_layernorm else hidden
-                hidden = ca.dropout(ca.core(c_in, None, inputs[2], inputs[3])) + hidden
+                hidden = ca.dropout(ca.core(c_in, None, rest[1], rest[2])) + hidden
                 if ca.post_layernorm:
                     hidden = ca.layernorm(hidden)
                 m = out.pre_layernorm_module(hidden) if out.pre_layernorm else hidden
             mlp = out.core(m)
             if self._defers():
-                return (hidden,) + tuple(inputs[1:]) + (mlp, _Deferred(out.dropout.active_p()))
+                return (hidden,) + tuple(rest) + (mlp, _Deferred(out.dropout.active_p()))
             hidden = out.dropout.add(mlp, hidden)
             if out.post_layernorm:
                 hidden = out.layernorm(hidden)
-        if self._tp > 1 and self.output_layer and not _prescaled():
+        if tp_region and self.output_layer:
             hidden = _leave_tp(hidden, self._mem, self.hidden_size)
+            # back to the rank's own batch: the mask / encoder states this stack gathered
+            if torch.is_tensor(rest[0]) and rest[0].dim() > 0 and rest[0].shape[0] > 1:
+                rest[0] = narrow_for_tp(rest[0], 0)
+            if self.add_cross_attention and len(rest) >= 3 and torch.is_tensor(rest[1]):
+                rest[1] = _leave_tp(rest[1], self._mem, self.hidden_size)
+                if torch.is_tensor(rest[2]) and rest[2].dim() > 0 and rest[2].shape[0] > 1:
+                    rest[2] = narrow_for_tp(rest[2], 0)
         elif self._tp > 1 and self._mem and getattr(self, "_full_batch_out", False):
             hidden = _leave_tp(hidden, True, self.hidden_size, full_batch=True)
-        return (hidden,) + tuple(inputs[1:])
+        return (hidden,) + tuple(rest)
 
 
 _CAUSAL_MASK_NOTED = [False]

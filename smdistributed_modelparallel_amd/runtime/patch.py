@@ -101,7 +101,11 @@ def _seq_forward(seq, inp):
 def patch_one(module):
     if "_smp_orig_forward" in module.__dict__:
         return
-    module.__dict__["_smp_orig_forward"] = type(module).forward.__get__(module)
+    # an instance-level forward (e.g. the argument-translating wrapper smp.tp_register's hooks
+    # install on a replaced Hugging Face module) is the original to call, not the class's
+    inst = module.__dict__.get("forward")
+    module.__dict__["_smp_inst_forward"] = inst
+    module.__dict__["_smp_orig_forward"] = inst if inst is not None else type(module).forward.__get__(module)
     if isinstance(module, nn.Sequential):
         module.__dict__["forward"] = functools.partial(_seq_forward, module)
     else:
@@ -110,7 +114,11 @@ def patch_one(module):
 
 def unpatch_one(module):
     module.__dict__.pop("_smp_orig_forward", None)
-    module.__dict__.pop("forward", None)
+    inst = module.__dict__.pop("_smp_inst_forward", None)
+    if inst is not None:
+        module.__dict__["forward"] = inst
+    else:
+        module.__dict__.pop("forward", None)
 
 
 def patch_module_forwards(model):
