@@ -483,3 +483,15 @@ def test_hf_bert_mlm_tp_pp_matches_hf(pp, tp):
 
     outs = run_workers("hf_bert_tp", pp * tp, [str(pp), str(tp)], timeout=300)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("family,pp,tp", [("gpt2", 1, 2), ("gpt2", 2, 1), ("gptj", 2, 2), ("gptneo", 2, 2),
+                                          ("gpt_neox", 2, 2), ("gpt_neox", 1, 2)])
+def test_hf_causal_lm_padding_mask_tp_pp_matches_hf(family, pp, tp):
+    """HF causal LMs (GPT-2, GPT-J, GPT-Neo with local layers, GPT-NeoX) through the smp entry
+    points -- TP swap to DistributedTransformerLMHead and / or auto-partitioning -- on right-padded
+    batches: the loss follows the plain HF model for 3 SGD steps (tests/workers/hf_lm_mask.py)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("hf_lm_mask", pp * tp, [family, str(pp), str(tp)], timeout=300)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
