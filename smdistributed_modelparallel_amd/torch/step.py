@@ -63,6 +63,22 @@ def _decide_all_ones(args, kwargs):
             pass
 
 
+
+def as_step_output(per_mb):
+    """Per-microbatch return values -> the step function's return structure with a StepOutput at
+    every tensor leaf (reference `torch/step.py:305-337`): a step returning ``(loss, logits)``
+    yields ``(StepOutput, StepOutput)``; lists and dicts (e.g. a Hugging Face ModelOutput) keep
+    their shape; other leaves come back as the list of per-microbatch values."""
+    first = per_mb[0]
+    if isinstance(first, dict):
+        return {k: as_step_output([o[k] for o in per_mb]) for k in first}
+    if isinstance(first, (list, tuple)):
+        parts = [as_step_output([o[i] for o in per_mb]) for i in range(len(first))]
+        return parts if isinstance(first, list) else tuple(parts)
+    if isinstance(first, torch.Tensor):
+        return StepOutput(per_mb)
+    return per_mb
+
 class PTTensorSplitter(TensorSplitter):
     def is_tensor(self, x):
         return isinstance(x, torch.Tensor)
@@ -156,7 +172,7 @@ class StepFunction:
         self.memory_metrics.record(state.step_count)
         if outputs is None:
             return None
-        return StepOutput(outputs)
+        return as_step_output(list(outputs))
 
     def _upload_metrics_once(self):
         """Partition metrics, published once per job from rank 0 (reference `step.py:295-311`)."""

@@ -495,3 +495,26 @@ def test_hf_causal_lm_padding_mask_tp_pp_matches_hf(family, pp, tp):
 
     outs = run_workers("hf_lm_mask", pp * tp, [family, str(pp), str(tp)], timeout=300)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("pp,tp", [(2, 1), (2, 2)])
+def test_hf_eval_step_returns_structure_of_step_outputs(pp, tp):
+    """Train / evaluate / train with an HF model under PP (x TP): the eval step returns
+    ``(loss, {"logits": ...})`` and gets a StepOutput at every tensor leaf (reference
+    `torch/step.py:305-337`), full-vocabulary logits included."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("hf_eval", pp * tp, [str(pp), str(tp)], timeout=300)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+def test_as_step_output_structure():
+    from smdistributed_modelparallel_amd.backend.split import StepOutput
+    from smdistributed_modelparallel_amd.torch.step import as_step_output
+
+    per_mb = [(torch.ones(2), [torch.zeros(1), "a"], {"x": torch.full((1,), 3.0)}) for _ in range(2)]
+    out = as_step_output(per_mb)
+    assert isinstance(out, tuple) and isinstance(out[0], StepOutput)
+    assert isinstance(out[1], list) and isinstance(out[1][0], StepOutput) and out[1][1] == ["a", "a"]
+    assert float(out[2]["x"].reduce_sum()) == 6.0
+    assert isinstance(as_step_output([torch.ones(1)] * 3), StepOutput)

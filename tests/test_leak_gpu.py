@@ -43,7 +43,8 @@ def run():
         opt.zero_grad()
         out = train(model, ids, labels)
         opt.step()
-        for loss, logits in out.outputs:
+        loss_o, logits_o = out  # a tuple of StepOutputs (one per returned tensor)
+        for loss, logits in zip(loss_o.outputs, logits_o.outputs):
             assert loss.grad_fn is None and logits.grad_fn is None, "step outputs not detached"
         del out
         torch.cuda.synchronize()
