@@ -80,7 +80,13 @@ def _pinned_full(n, fill):
     return t
 
 
-class DistributedOptimizer:
+class DistributedOptimizer(torch.optim.Optimizer):
+    """The wrapped optimizer.  A ``torch.optim.Optimizer`` by type (the base class's ``__init__``
+    is not run: param_groups / defaults / state are the inner optimizer's), so code that checks
+    the type -- ``torch.optim.lr_scheduler`` schedulers, Hugging Face / accelerate training loops --
+    takes it; the reference returns the user's optimizer object itself with patched methods
+    (`torch/optimizers/optimizer.py:437-520`)."""
+
     def __init__(self, optimizer, static_loss_scale=1.0, dynamic_loss_scale=False, dynamic_loss_args=None):
         if state.model is None:
             raise SMPInvalidArgumentError("create smp.DistributedModel before smp.DistributedOptimizer")

@@ -28,3 +28,14 @@ def test_reference_format_optimizer_state_import():
     for kind, prec in (("adamw", "fp32"), ("sgd", "fp32"), ("adamw", "bf16")):
         outs = run_workers("ref_opt_import", 1, [kind, prec], timeout=120)
         assert f"OK {kind} {prec}" in outs[0], outs
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("pp,tp", [(2, 1), (1, 2)])
+def test_lr_scheduler_on_distributed_optimizer(pp, tp):
+    """smp.DistributedOptimizer is a torch.optim.Optimizer by type: torch's LR schedulers drive
+    it (they refused the wrapper before round 6), with gradient accumulation across steps."""
+    outs = run_workers("lr_sched", pp * tp, [str(pp), str(tp)], timeout=300)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
