@@ -111,3 +111,20 @@ def smp_to_hf(sd):
     rest = RULES.smp_to_hf(rest, out)
     out.update(rest)
     return out
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/bert.py` of the reference): the hook
+# triple for smp.tp_register_with_module and the state-dict translators under their names
+def get_hf_bert_transformer_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_bert(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_bert(state_dict):
+    return smp_to_hf(state_dict)
+
+
+translate_hf_state_dict_to_smdistributed = translate_hf_state_dict_to_smdistributed_bert

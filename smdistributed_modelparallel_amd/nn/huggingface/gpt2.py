@@ -217,3 +217,31 @@ class _LayerFamily:
 
 
 LAYER = _LayerFamily
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/gpt2.py:27-34,205,291,344,455` of the
+# reference): hook triples for smp.tp_register_with_module and the state-dict translators
+def get_hf_gpt2_transformer_lm_head_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def get_hf_gpt2_transformer_layer_hooks():
+    return layer_init_hook, layer_forward_hook, layer_return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_gpt2(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_gpt2(state_dict, max_seq_len=None):
+    """(max_seq_len: the reference re-creates HF attention-mask buffers of that length; the
+    installed transformers keeps none in its state dicts, so it is accepted and unused.)"""
+    return smp_to_hf(state_dict)
+
+
+def translate_hf_state_dict_to_smdistributed_gpt2_layer(state_dict):
+    return layer_hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_gpt2_layer(state_dict, max_seq_len=None):
+    return layer_smp_to_hf(state_dict)

@@ -84,3 +84,19 @@ def smp_to_hf(sd):
     out.update(rest)
     add_tied(out, "transformer.wte.weight", "lm_head.weight")
     return out
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/gptneo.py` of the reference): the hook
+# triple for smp.tp_register_with_module and the state-dict translators under their names
+def get_hf_gptneo_transformer_lm_head_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_gptneo(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_gptneo(state_dict, max_seq_len=None):
+    """(max_seq_len: the reference re-creates HF attention-mask buffers of that length; the
+    installed transformers keeps none in its state dicts, so it is accepted and unused.)"""
+    return smp_to_hf(state_dict)

@@ -121,3 +121,19 @@ def smp_to_hf(sd, num_heads=None):
     rest = RULES.smp_to_hf(rest, out)  # LM head: `lm_head` in transformers 5.x (older: `embed_out`)
     out.update(rest)
     return out
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/gptneox.py` of the reference): the hook
+# triple for smp.tp_register_with_module and the state-dict translators under their names
+def get_hf_gptneox_transformer_lm_head_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_gptneox(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_gptneox(state_dict, max_seq_len=None):
+    """(max_seq_len: the reference re-creates HF attention-mask buffers of that length; the
+    installed transformers keeps none in its state dicts, so it is accepted and unused.)"""
+    return smp_to_hf(state_dict)

@@ -26,3 +26,20 @@ def init_hook(config, *args, **kwargs):
 
 forward_hook = partial(encoder_forward_hook, error=HFRobertaConfigError, family="RoBERTa")
 return_hook = encoder_return_hook
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/roberta.py` of the reference): the hook
+# triple for smp.tp_register_with_module and the state-dict translators under their names
+def get_hf_roberta_transformer_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_roberta(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_roberta(state_dict):
+    return smp_to_hf(state_dict)
+
+
+translate_hf_state_dict_to_smdistributed = translate_hf_state_dict_to_smdistributed_roberta

@@ -105,3 +105,20 @@ def register_vit(registry):
 
     registry.register(ViTLayer, DistributedTransformerLayer, init_hook=init_hook, forward_hook=forward_hook,
                       return_hook=return_hook, translate_functions=(smp_to_hf, hf_to_smp))
+
+
+# ---- reference-named entry points (`torch/nn/huggingface/vit.py` of the reference): the hook
+# triple for smp.tp_register_with_module and the state-dict translators under their names
+def get_hf_vit_encoder_hooks():
+    return init_hook, forward_hook, return_hook
+
+
+def translate_hf_state_dict_to_smdistributed_vit(state_dict):
+    return hf_to_smp(state_dict)
+
+
+def translate_state_dict_to_hf_vit(state_dict):
+    return smp_to_hf(state_dict)
+
+
+translate_hf_state_dict_to_smdistributed = translate_hf_state_dict_to_smdistributed_vit

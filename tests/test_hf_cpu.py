@@ -518,3 +518,25 @@ def test_as_step_output_structure():
     assert isinstance(out[1], list) and isinstance(out[1][0], StepOutput) and out[1][1] == ["a", "a"]
     assert float(out[2]["x"].reduce_sum()) == 6.0
     assert isinstance(as_step_output([torch.ones(1)] * 3), StepOutput)
+
+
+def test_reference_named_translators_round_trip():
+    """The reference's entry-point names (translate_hf_state_dict_to_smdistributed_<family>,
+    translate_state_dict_to_hf_<family>, get_hf_<family>_..._hooks) exist and round-trip."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    from smdistributed_modelparallel_amd.nn.huggingface import bert, gpt2, gptj, gptneo, gptneox, roberta, vit
+
+    hf = GPT2LMHeadModel(GPT2Config(n_layer=2, n_embd=32, n_head=4, vocab_size=50, n_positions=16))
+    sd = {k: v for k, v in hf.state_dict().items()}
+    back = gpt2.translate_state_dict_to_hf_gpt2(gpt2.translate_hf_state_dict_to_smdistributed_gpt2(sd), 16)
+    for k, v in sd.items():
+        if k in back:
+            assert torch.equal(back[k], v), k
+    assert {k for k in sd if not k.endswith(".attn.bias")} <= set(back) | {"lm_head.weight"}
+    assert len(gpt2.get_hf_gpt2_transformer_lm_head_hooks()) == 3 and len(gpt2.get_hf_gpt2_transformer_layer_hooks()) == 3
+    for mod, name in ((gptj, "gptj"), (gptneo, "gptneo"), (gptneox, "gptneox"), (bert, "bert"), (roberta, "roberta"),
+                      (vit, "vit")):
+        assert callable(getattr(mod, f"translate_hf_state_dict_to_smdistributed_{name}"))
+        assert callable(getattr(mod, f"translate_state_dict_to_hf_{name}"))
+    assert len(gptj.get_hf_gptj_transformer_hooks()) == 3 and len(vit.get_hf_vit_encoder_hooks()) == 3
