@@ -28,6 +28,26 @@ class SMPConfigError(SMPValidationError):
     pass
 
 
+class DDPNotEnabledError(SMPValidationError):
+    """A torch.distributed process group was requested but none exists (reference
+    `torch/exceptions.py:24-27`)."""
+
+    def __str__(self):
+        return "torch.distributed is not initialized for this group: enable ddp in the smp config"
+
+
+class InvalidCommGroupError(SMPValidationError):
+    """A barrier / collective was given something that is not a CommGroup (reference
+    `torch/exceptions.py:29-35`)."""
+
+    def __init__(self, group):
+        super().__init__(group)
+        self.group = group
+
+    def __str__(self):
+        return f"invalid communication group {self.group!r}: expected a smp.CommGroup"
+
+
 class DistTransformerConfigError(SMPInvalidArgumentError):
     """An smp.nn transformer module was given an unsupported combination of options
     (reference `torch/exceptions.py:53`)."""

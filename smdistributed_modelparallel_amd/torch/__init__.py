@@ -159,6 +159,7 @@ def reset():
     from ..parallel import oneshot
 
     oneshot.reset()  # IPC buffers belong to the process groups being torn down
+    _SINGLETON_GROUPS.clear()
     state.reset()
 
 
@@ -291,6 +292,10 @@ from .collectives import allgatherv_tensor, scatter_and_merge_tensor  # noqa: E4
 
 
 def barrier(group=CommGroup.WORLD):
+    if not isinstance(group, CommGroup):
+        from ..backend.exceptions import InvalidCommGroupError
+
+        raise InvalidCommGroupError(group)
     state.comm.barrier(group, is_user_api=True)
 
 
@@ -314,28 +319,56 @@ def mp_barrier():
     barrier(CommGroup.MP_GROUP)
 
 
+_SINGLETON_GROUPS = {}
+
+
+def _process_group(name):
+    """The torch.distributed group of this rank.  A degree-1 group has no internal group object;
+    handing back None would make torch.distributed collectives run over WORLD, so a one-member
+    group is created for it (only this rank takes part: use_local_synchronization)."""
+    import torch.distributed as dist
+
+    pg = getattr(state.pgs, name, None) if state.pgs is not None else None
+    if pg is not None:
+        return pg
+    if not dist.is_available() or not dist.is_initialized():
+        from ..backend.exceptions import DDPNotEnabledError
+
+        raise DDPNotEnabledError()
+    if name not in _SINGLETON_GROUPS:
+        _SINGLETON_GROUPS[name] = dist.new_group([dist.get_rank()], use_local_synchronization=True)
+    return _SINGLETON_GROUPS[name]
+
+
 def get_world_process_group():
-    return state.pgs.world
+    return _process_group("world")
 
 
 def get_pp_process_group():
-    return state.pgs.pp
+    return _process_group("pp")
 
 
 def get_tp_process_group():
-    return state.pgs.tp
+    return _process_group("tp")
 
 
 def get_dp_process_group():
-    return state.pgs.dp
+    return _process_group("dp")
 
 
 def get_rdp_process_group():
-    return state.pgs.rdp
+    return _process_group("rdp")
 
 
 def get_mp_process_group():
-    return state.pgs.mp
+    return _process_group("mp")
+
+
+def shutdown():
+    """Flush and stop the native runtime of this process (reference `torch/core.py`); runs at
+    exit on its own."""
+    if state.core is not None:
+        state.core.shutdown()
 
 
 # ------------------------------------------------------------- model building
@@ -396,3 +429,10 @@ def _maybe_auto_init():
 
 
 _maybe_auto_init()
+
+
+def __getattr__(name):
+    # smp.core: the process topology / native runtime object (reference `torch/core.py`)
+    if name == "core":
+        return state.core
+    raise AttributeError(name)

@@ -563,3 +563,14 @@ def test_all_ones_mask_decided_before_split(monkeypatch):
     assert not T._all_ones(torch.ones(2, 16))  # no decision under PP: kept, no sync
     ones.add_(0)  # a write invalidates the decision
     assert not T._all_ones(ones[:2])
+
+
+def test_process_group_getters_and_barrier_validation():
+    """smp.get_*_process_group() never hands back None (a degree-1 group becomes a one-member
+    group: None would make torch.distributed collectives run over WORLD); smp.barrier refuses a
+    non-CommGroup with InvalidCommGroupError; smp.core is the topology object (reference
+    `torch/comm.py:56-104`, `torch/exceptions.py:24-35`)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("process_groups", 2, [], timeout=120)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
