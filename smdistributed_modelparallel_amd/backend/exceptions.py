@@ -202,6 +202,264 @@ class HFViTConfigError(HFConfigError):
     pass
 
 
+# ------------------------------------------------- reference exception names
+# Every exception class the reference defines (`backend/exceptions.py`, `torch/exceptions.py`)
+# exists here under its name, placed in this hierarchy, so user code catching them keeps
+# working; the ones this framework raises for the same condition are raised under these names
+# (split, step outputs, checkpoints, a second DistributedModel).
+class CommGroupConfigError(SMPValidationError):
+    pass
+
+
+class LoggingConfigError(SMPValidationError):
+    pass
+
+
+class InvalidTransactionIDError(SMPValidationError):
+    pass
+
+
+class InvalidLinkIDError(SMPValidationError):
+    pass
+
+
+class InvalidStepOutputError(SMPInvalidArgumentError):
+    """A StepOutput was built from something other than a list / tuple, or reduced over
+    non-tensor outputs."""
+
+
+class TensorSplitError(SMPRuntimeError, SMPInvalidArgumentError):
+    """A step input cannot be split into the configured number of microbatches."""
+
+
+class InitializationError(SMPRuntimeError):
+    pass
+
+
+class SMPSegFault(SMPRuntimeError):
+    pass
+
+
+class DDPConfigError(SMPValidationError):
+    pass
+
+
+class HorovodConfigError(SMPValidationError):
+    pass
+
+
+class CheckpointingConfigError(SMPValidationError):
+    pass
+
+
+class DistEmbeddingConfigError(SMPValidationError):
+    pass
+
+
+class ModelTooSmallError(SMPValidationError):
+    pass
+
+
+class InvalidSeqLenPrescaledBatchError(SMPValidationError):
+    pass
+
+
+class MemoryWeightError(SMPValidationError):
+    pass
+
+
+class CostListError(SMPValidationError):
+    pass
+
+
+class MultipleDistributedModelError(SMPValidationError, SMPRuntimeError):
+    """More than one smp.DistributedModel in a process."""
+
+
+class BwdExecutionNotInStepFnError(SMPValidationError):
+    pass
+
+
+class FwdExecutionNotInStepFnError(SMPValidationError):
+    pass
+
+
+class ModelNotPartitionedError(SMPValidationError):
+    pass
+
+
+class HiddenDimError(SMPValidationError):
+    pass
+
+
+class SplitShapeLenError(SMPValidationError):
+    pass
+
+
+class SplitShapeMismatchError(SMPValidationError):
+    pass
+
+
+class ShiftValueError(SMPValidationError):
+    pass
+
+
+class PaddingSizeError(SMPValidationError):
+    pass
+
+
+class DistributedModelWrappedError(SMPValidationError):
+    pass
+
+
+class InvalidPartitionIDError(SMPValidationError):
+    pass
+
+
+class HFNotAvailableError(SMPValidationError):
+    pass
+
+
+class SMPCheckpointError(CheckpointingError, SMPValidationError):
+    """Base of the checkpoint-content errors (a CheckpointingError too)."""
+
+
+class MissingCheckpointFilesError(SMPCheckpointError):
+    pass
+
+
+class IncompatibleCheckpointRankFoundError(SMPCheckpointError):
+    pass
+
+
+class IncompatibleCheckpointFoundError(SMPCheckpointError):
+    pass
+
+
+class MissingKeysInCheckpointError(SMPCheckpointError):
+    pass
+
+
+class RemoteBufferShouldNotExistError(SMPCheckpointError):
+    pass
+
+
+class RemoteBufferShouldExistError(SMPCheckpointError):
+    pass
+
+
+class InvalidReturnTypeFromCheckpointedModuleError(SMPCheckpointError):
+    pass
+
+
+class FusedLAMBError(SMPUnsupportedError):
+    pass
+
+
+class DelayedParamDeviceError(SMPUnsupportedError):
+    pass
+
+
+class UnsupportedTorchVersionError(SMPUnsupportedError):
+    pass
+
+
+class UnsupportedReducerTypeError(SMPUnsupportedError):
+    pass
+
+
+class UnsupportedTPModuleError(SMPUnsupportedError):
+    pass
+
+
+class TPModuleRegisterError(SMPUnsupportedError):
+    pass
+
+
+class MultipleDtypeOptShardingError(SMPUnsupportedError):
+    pass
+
+
+class SequentialBackwardBrokenError(SMPUnsupportedError):
+    pass
+
+
+class RecursionDepthExceededDuringSerializationError(SMPUnsupportedError):
+    pass
+
+
+class UnsupportedMessageError(SMPUnsupportedError):
+    pass
+
+
+class UnsupportedShardedConfigError(SMPUnsupportedError, RuntimeError):
+    pass
+
+
+class ScaledBatchBufNotInDistModuleError(SMPRuntimeError):
+    pass
+
+
+class InvalidHandleError(SMPRuntimeError):
+    pass
+
+
+class MissingParentModuleError(SMPRuntimeError):
+    pass
+
+
+class MissingModuleError(SMPRuntimeError):
+    pass
+
+
+class ParentNodeExistingError(SMPRuntimeError):
+    pass
+
+
+class ChildNodeExistingError(SMPRuntimeError):
+    pass
+
+
+class UnrecognizedHFKeyError(SMPRuntimeError):
+    pass
+
+
+class CustomSoftmaxKernelDtypeError(SMPRuntimeError):
+    pass
+
+
+class MissingGradientError(SMPRuntimeError):
+    pass
+
+
+class GradRequireGradError(SMPRuntimeError):
+    pass
+
+
+class SMPAMPError(SMPRuntimeError):
+    pass
+
+
+class InvalidRequestError(SMPRuntimeError):
+    pass
+
+
+class InvalidExecutorError(SMPRuntimeError):
+    pass
+
+
+class NonDummyTensorError(SMPRuntimeError):
+    pass
+
+
+class InvalidParentModuleError(SMPRuntimeError):
+    pass
+
+
+class NumParametersNotMatchError(SMPRuntimeError):
+    pass
+
+
 class TracingEnd(Exception):
     """Internal control-flow signal: stop the step function once the traced forward ends
     (reference `patches/tracing.py:41-86`)."""

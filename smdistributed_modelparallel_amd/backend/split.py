@@ -10,7 +10,7 @@ Behavioural parity with `smp/backend/split.py:13-228` and `smp/torch/step.py:53-
 """
 import inspect
 
-from .exceptions import SMPInvalidArgumentError
+from .exceptions import InvalidStepOutputError, SMPInvalidArgumentError, TensorSplitError
 
 
 class StepOutput:
@@ -36,7 +36,7 @@ class StepOutput:
 
         for o in self.outputs:
             if not isinstance(o, torch.Tensor):
-                raise SMPInvalidArgumentError("StepOutput reductions require tensor outputs")
+                raise InvalidStepOutputError("StepOutput reductions require tensor outputs")
 
     def reduce_mean(self):
         import torch
@@ -113,7 +113,7 @@ class TensorSplitter:
         if self.is_tensor(obj):
             size = self.tensor_size(obj, axis)
             if size % num_mb != 0:
-                raise SMPInvalidArgumentError(
+                raise TensorSplitError(
                     f"Batch size {size} along axis {axis} is not divisible by the number of microbatches "
                     f"{num_mb}."
                 )

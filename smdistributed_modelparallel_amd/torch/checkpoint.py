@@ -26,7 +26,8 @@ import torch
 
 from .. import __version__ as smp_version
 from ..backend.collectives import CommGroup
-from ..backend.exceptions import CheckpointingError, SMPInvalidArgumentError
+from ..backend.exceptions import (CheckpointingError, IncompatibleCheckpointFoundError, IncompatibleCheckpointRankFoundError,
+                                  MissingCheckpointFilesError, SMPInvalidArgumentError)
 from ..backend.logger import get_logger
 from .state_mod import state
 
@@ -40,7 +41,7 @@ def _c():
 def _parts(prefix):
     files = [f for f in glob.glob(f"{prefix}_*") if ".sagemaker-" not in f]
     if not files:
-        raise CheckpointingError(f"no checkpoint files found with prefix {prefix}")
+        raise MissingCheckpointFilesError(f"no checkpoint files found with prefix {prefix}")
     return files
 
 
@@ -60,7 +61,7 @@ def _validate_num_parts(prefix):
             kind = kind or "v1"
     expected = {"v3": core.size(), "v2": core.mp_size(), "v1": core.pp_size()}[kind]
     if n != expected:
-        raise CheckpointingError(
+        raise IncompatibleCheckpointRankFoundError(
             f"checkpoint {prefix} has {n} parts, expected {expected} for the current pp/tp/rdp layout ({kind})")
     return kind
 
@@ -198,7 +199,7 @@ def verify_smp_config(saved, partial=True, load_optimizer=True):
         hard = {"pipeline_parallel_degree", "tensor_parallel_degree", "shard_optimizer_state",
                 "sharded_data_parallel_degree"} & set(mismatch)
         if hard:
-            raise CheckpointingError(
+            raise IncompatibleCheckpointFoundError(
                 "changes not allowed when loading a partial checkpoint with optimizer state: "
                 + ", ".join(f"{k}: saved {mismatch[k][0]} current {mismatch[k][1]}" for k in sorted(hard)))
     if mismatch:
@@ -227,7 +228,7 @@ def resume_from_checkpoint(path, tag=None, partial=True, strict=True, load_optim
             tag = f"{tag}_partial"
     ckpt = os.path.join(path, tag)
     if not os.path.exists(ckpt):
-        raise CheckpointingError(f"checkpoint {ckpt} does not exist")
+        raise MissingCheckpointFilesError(f"checkpoint {ckpt} does not exist")
     logger.info(f"resuming from {'partial' if partial else 'full'} checkpoint {user_tag} at {path}")
     if partial and core.rank() == 0 and os.environ.get("SMP_VERIFY_CHECKPOINT_CONFIG", "1") not in ("0", "false"):
         verify_smp_config(load(os.path.join(ckpt, "smp_config.pt"), partial=False), partial, load_optimizer)

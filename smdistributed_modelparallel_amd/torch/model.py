@@ -79,7 +79,9 @@ class DistributedModel(nn.Module):
         if not state.initialized:
             raise SMPRuntimeError("smp.init() must be called before smp.DistributedModel")
         if state.model is not None:
-            raise SMPRuntimeError("only one smp.DistributedModel per process is supported")
+            from ..backend.exceptions import MultipleDistributedModelError
+
+            raise MultipleDistributedModelError("only one smp.DistributedModel per process is supported")
         cfg = state.cfg
         self.trace_device = trace_device
         self.trace_execution_times = trace_execution_times

@@ -574,3 +574,20 @@ def test_process_group_getters_and_barrier_validation():
 
     outs = run_workers("process_groups", 2, [], timeout=120)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+def test_reference_exception_names():
+    """Every exception class of the reference (`backend/exceptions.py`, `torch/exceptions.py`) is
+    importable from the smp namespace, and the split / checkpoint errors keep both their
+    reference name and the broader class earlier code caught."""
+    import smdistributed_modelparallel_amd.torch as smp
+    from smdistributed_modelparallel_amd.backend import exceptions as E
+
+    names = ["TensorSplitError", "InvalidStepOutputError", "SMPCheckpointError", "MissingCheckpointFilesError",
+             "IncompatibleCheckpointFoundError", "IncompatibleCheckpointRankFoundError", "MultipleDistributedModelError",
+             "DDPNotEnabledError", "InvalidCommGroupError", "HFT5ConfigError", "FusedLAMBError", "SMPSegFault",
+             "MissingPathFromModuleInputToModuleOutputError", "NotSupportedByFastModeError"]
+    for n in names:
+        assert isinstance(getattr(smp, n), type), n
+    assert issubclass(E.TensorSplitError, E.SMPInvalidArgumentError) and issubclass(E.TensorSplitError, RuntimeError)
+    assert issubclass(E.MissingCheckpointFilesError, E.CheckpointingError)
