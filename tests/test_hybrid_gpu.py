@@ -111,3 +111,14 @@ def test_grad_check_catches_missing_tp_allreduce():
     (GPT-2 XL width, TP=2, bf16) -- the gradient check must fail."""
     with pytest.raises(AssertionError, match="grad rel err"):
         _run(2, 1, 2, 2, extra=dict(_BF16, base="gpt2-xl", break_tp_bwd=True, fp32_ref_tol=None))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family,pp,tp", [("gpt2", 1, 2), ("gpt_neox", 2, 2)])
+def test_hf_causal_lm_padding_mask_bf16_gpu(family, pp, tp):
+    """HF causal LMs through smp on the GPU in bf16 (TP swap to DistributedTransformerLMHead, the
+    flash kernels' key-bias path for right padding, ranks sharing the card over gloo) against the
+    plain fp32 HF model on the CPU: loss within 3 % for 3 SGD steps (tests/workers/hf_lm_mask.py)."""
+    env = dict(_ENV, HF_MASK_BF16="1")
+    outs = run_workers("hf_lm_mask", pp * tp, [family, str(pp), str(tp)], timeout=240, env_extra=env)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
