@@ -9,7 +9,6 @@
 import numbers
 
 import torch
-import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.layernorm import add_layer_norm, layer_norm, layer_norm_passthrough

@@ -15,7 +15,6 @@ import functools
 
 import torch
 import torch.nn as nn
-from torch.utils.checkpoint import checkpoint as _torch_ckpt
 
 from ..torch.state_mod import state
 

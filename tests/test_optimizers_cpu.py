@@ -1,6 +1,7 @@
 """Fused optimizers on CPU: DistributedOptimizer(FusedLAMB) updates every domain with
 per-parameter trust ratios in two segmented launches (reference apex FusedLAMB semantics),
 FusedNovoGrad keeps its per-tensor second moments on the device (no host sync)."""
+import pytest
 import torch
 
 from smdistributed_modelparallel_amd.ops import multi_tensor as mt
@@ -29,8 +30,6 @@ def test_reference_format_optimizer_state_import():
         outs = run_workers("ref_opt_import", 1, [kind, prec], timeout=120)
         assert f"OK {kind} {prec}" in outs[0], outs
 
-
-import pytest  # noqa: E402
 
 
 @pytest.mark.parametrize("pp,tp", [(2, 1), (1, 2)])

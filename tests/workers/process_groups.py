@@ -1,6 +1,7 @@
 """Worker: smp process-group getters and barrier validation (PP=2, TP=1, 2 ranks)."""
-import os, sys
-import torch, torch.distributed as dist
+import torch
+import torch.distributed as dist
+
 import smdistributed_modelparallel_amd.torch as smp
 from smdistributed_modelparallel_amd.backend.exceptions import InvalidCommGroupError
 smp.init({"pipeline_parallel_degree": 2, "tensor_parallel_degree": 1, "ddp": True})
