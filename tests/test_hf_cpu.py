@@ -540,3 +540,12 @@ def test_reference_named_translators_round_trip():
         assert callable(getattr(mod, f"translate_hf_state_dict_to_smdistributed_{name}"))
         assert callable(getattr(mod, f"translate_state_dict_to_hf_{name}"))
     assert len(gptj.get_hf_gptj_transformer_hooks()) == 3 and len(vit.get_hf_vit_encoder_hooks()) == 3
+
+
+def test_tp_register_with_module_custom_block():
+    """smp.tp_register_with_module: a user-defined block mapped to DistributedTransformerLayer by
+    init / forward / return hooks is replaced at creation under TP=2 and trains."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("tp_register", 2, [], timeout=180)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
