@@ -549,3 +549,13 @@ def test_tp_register_with_module_custom_block():
 
     outs = run_workers("tp_register", 2, [], timeout=180)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("family,pp", [("gpt2", 1), ("gpt_neox", 2)])
+def test_hf_causal_lm_padding_mask_memory_mode_matches_hf(family, pp):
+    """The same HF parity with optimize="memory" (hidden-dimension-sharded TP stack)."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("hf_lm_mask", pp * 2, [family, str(pp), "2"], timeout=300,
+                       env_extra={"HF_MASK_CFG": "optimize=memory"})
+    assert all("OK" in o for o in outs), outs[0][-3000:]

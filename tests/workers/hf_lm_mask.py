@@ -35,8 +35,12 @@ def main():
     torch.manual_seed(0)
     ref, mod = build(family)
     bf16 = os.environ.get("HF_MASK_BF16") == "1"  # GPU variant: bf16 smp model (flash key-bias path)
-    smp.init({"pipeline_parallel_degree": pp, "tensor_parallel_degree": tp, "microbatches": 2,
-              "auto_partition": True, "ddp": True, "bf16": bf16})
+    extra = {}
+    for kv in filter(None, os.environ.get("HF_MASK_CFG", "").split(",")):  # e.g. optimize=memory
+        k, v = kv.split("=")
+        extra[k] = {"true": True, "false": False}.get(v.lower(), v)
+    smp.init(dict({"pipeline_parallel_degree": pp, "tensor_parallel_degree": tp, "microbatches": 2,
+                   "auto_partition": True, "ddp": True, "bf16": bf16}, **extra))
     torch.manual_seed(0)
     with smp.model_creation(tensor_parallelism=tp > 1):
         net, _ = build(family)
