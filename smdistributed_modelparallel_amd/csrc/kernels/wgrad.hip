@@ -799,14 +799,16 @@ int wgrad(int dt, const void* a, const void* b, int c_dt, void* c, float* ws, in
     return e != nullptr && strcmp(e, "glds") == 0;
   }();
   const bool use_glds = impl == 0 || (impl < 0 && env_glds);
-  // (a bias gradient: idle-quadrant sums where K % 256 leaves a quadrant idle, else the extra
-  // row-sum MFMAs; SMP_WGRAD_PP_CS=idle keeps the round-5 rule -- other K to the round-4 kernel)
-  static const bool cs_idle_only = [] {
+  // a bias gradient: idle-quadrant sums where K % 256 leaves a quadrant idle; the row-sum MFMA
+  // mode for other K only on request (impl 2, or SMP_WGRAD_PP_CS=rowsum: it slows every
+  // workgroup of the kernel, profiles/r6/wgrad_rowsum_bias.md), else the round-4 kernel
+  static const bool env_rowsum = [] {
     const char* e = getenv("SMP_WGRAD_PP_CS");
-    return e != nullptr && strcmp(e, "idle") == 0;
+    return e != nullptr && strcmp(e, "rowsum") == 0;
   }();
+  const bool rowsum_ok = impl == 2 || env_rowsum;
   const bool pp_ok = !use_glds && lda < (1 << 24) && ldb < (1 << 24) &&
-                     (bias == nullptr || wgrad_pp_cs_ok(k) || !cs_idle_only);
+                     (bias == nullptr || wgrad_pp_cs_ok(k) || rowsum_ok);
   if (pp_ok) {
     if (bias != nullptr && wgrad_pp_cs_ok(k))
       launch_pp<bf16, 1>(pa, pb, ws, tokens, n, k, lda, ldb, t_split, grid, s, cs);

@@ -251,11 +251,11 @@ def _wgrad_dbias_free(k):
 
 
 def _wgrad_dbias_rowsum(k):
-    """Any other ``k``: the ping-pong kernel sums the bias gradient with two extra MFMAs per wave
-    in two of each tile's four phases of the last K tile's workgroups -- taken when the kernel is
-    the pick anyway (GPT-2 XL fc2, K = 6400: -1 ms per step same box), not forced over a library
-    pick (the NeoX shard lost 3 % that way, `profiles/r6/wgrad_rowsum_bias.md`)."""
-    return os.environ.get("SMP_WGRAD_IMPL") != "glds" and os.environ.get("SMP_WGRAD_PP_CS") != "idle"
+    """Any other ``k``: the ping-pong kernel can sum the bias gradient with two extra MFMAs per
+    wave in two of each tile's four phases of the last K tile's workgroups (CS mode 2).  Opt-in
+    (SMP_WGRAD_PP_CS=rowsum): in the GPT-2 XL step its fc2 weight gradient (K = 6400) ran 1369.9 us
+    against 1275 us + a 40 us column-sum pass without it (`profiles/r6/wgrad_rowsum_bias.md`)."""
+    return os.environ.get("SMP_WGRAD_PP_CS") == "rowsum" and os.environ.get("SMP_WGRAD_IMPL") != "glds"
 
 
 def _wgrad_accumulate(g, dy2, x2, dbias=None):

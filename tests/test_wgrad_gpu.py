@@ -216,7 +216,8 @@ def test_wgrad_pp_bias_quadrant(shape):
     x = torch.randn(T, K, device="cuda", dtype=torch.bfloat16, generator=g0)
     ref_g = dy.float().t() @ x.float()
     ref_b = dy.float().sum(0)
-    for impl in (1, 0):
+    # impl 2: the ping-pong kernel with the row-sum mode allowed (K % 256 == 0 or > 128)
+    for impl in (2, 1, 0):
         for splits in (1, 4):
             g = torch.zeros(N, K, device="cuda", dtype=torch.float32)
             b = torch.zeros(N, device="cuda", dtype=torch.float32)
