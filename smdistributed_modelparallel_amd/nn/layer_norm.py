@@ -15,6 +15,7 @@ from ..ops.layernorm import add_layer_norm, layer_norm, layer_norm_passthrough
 from ..parallel.throttle import throttler
 from .utils import get_local_channels, get_start_pos_for_slicing, tp_group, tp_size
 from ..parallel import oneshot
+from ..ops._ext import fused_ok
 
 
 class FusedLayerNorm(nn.Module):
@@ -187,7 +188,7 @@ class DistributedLayerNorm(nn.Module):
 
     def forward(self, x):
         group = tp_group() if tp_size() > 1 else None
-        if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32):
+        if fused_ok(x) and x.dtype in (torch.bfloat16, torch.float16, torch.float32):
             return _DistLayerNormHIP.apply(x, self.weight, self.bias, self.eps, self.full_dim, group)
         mean, var = _DistLNStats.apply(x, self.full_dim, group)
         y = (x.float() - mean) * torch.rsqrt(var + self.eps)

@@ -36,6 +36,7 @@ from ..backend.logger import get_logger
 from ..ops.attention import attention as attention_op
 from ..ops.attention import FLASH_HEAD_DIMS, attention_packed, prefetch_keep_bits
 from ..ops.dropout import dropout_seed_offset
+from ..ops._ext import fused_ok
 from ..ops.cross_entropy import cross_entropy
 from ..ops.dropout import add3
 from ..ops.dropout import dropout_add as _dropout_add
@@ -464,7 +465,7 @@ class DistributedAttentionLayer(DistributedModule):
         an input shaped like ``x`` [B, s, h] -- when the packed flash path with dropout will run
         (self-attention, no padding mask, no window).  The enclosing layer calls it before its
         LayerNorm, so the VALU-bound hash overlaps that HBM-bound kernel and the QKV GEMM."""
-        if not (self.training and self.attention_dropout_prob > 0.0 and x.is_cuda and not self.window_size
+        if not (self.training and self.attention_dropout_prob > 0.0 and fused_ok(x) and not self.window_size
                 and not self.cross_attention and not self._mem and not self.attention_in_fp32
                 and self.qkv_weight.dtype in (torch.bfloat16, torch.float16)
                 and self.attention_head_size in FLASH_HEAD_DIMS
@@ -617,7 +618,7 @@ class DistributedTransformerOutputLayer(DistributedModule):
         # dense1's backward all-reduces dX asynchronously behind its weight-gradient GEMM; on
         # GPU it also takes dense1_bias's gradient (summed by its weight-gradient kernel from
         # the dY it reads anyway), so the bias-GeLU backward is a pure elementwise pass
-        fuse_db = (self.dense1_bias is not None and m.is_cuda and m.dtype == torch.bfloat16 and _lin._WGRAD_DBIAS
+        fuse_db = (self.dense1_bias is not None and fused_ok(m) and m.dtype == torch.bfloat16 and _lin._WGRAD_DBIAS
                    and self.activation in ("gelu", "gelu_exact"))
         x = linear(m, self.dense1_weight, dx_allreduce=dx_allreduce_async if self._tp > 1 else None,
                    dbias_of=self.dense1_bias if fuse_db else None)

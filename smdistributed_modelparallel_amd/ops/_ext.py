@@ -75,3 +75,12 @@ def available():
         return True
     except HIPExtensionMissingError:
         return False
+
+
+def fused_ok(t):
+    """The HIP kernels take this tensor: on the GPU and outside torch.autocast (under autocast the
+    inputs of one op arrive in mixed dtypes -- autocast GEMM outputs beside fp32 parameters -- and
+    the PyTorch reference path, which autocast handles, runs instead)."""
+    import torch
+
+    return t.is_cuda and not torch.is_autocast_enabled("cuda")

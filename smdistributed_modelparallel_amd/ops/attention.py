@@ -17,7 +17,7 @@ import os
 import torch
 
 from . import softmax as _sm
-from ._ext import ext
+from ._ext import ext, fused_ok
 from .dropout import dropout_seed_offset  # noqa: F401  (re-exported)
 
 _FLASH_OK = None
@@ -67,7 +67,7 @@ def flash_supported(q, dropout_p=0.0, mask=None, kbias=None):
     """Flash kernel covers bf16/fp16, head dims 64/96/128/256, in-kernel dropout, causal /
     sliding-window masks and per-key additive masks (padding)."""
     global _FLASH_OK
-    if not q.is_cuda or q.dtype not in (torch.bfloat16, torch.float16):
+    if not fused_ok(q) or q.dtype not in (torch.bfloat16, torch.float16):
         return False
     if q.shape[-1] not in FLASH_HEAD_DIMS:
         return False
@@ -351,7 +351,7 @@ def _materialised_chunk(q, k, v, scale, causal, mask, dropout_p, window, trainin
             local = local | (j > i)
         mask = local.view(1, 1, sq, sk) if mask is None else (mask.bool() | local.view(1, 1, sq, sk))
         causal = False
-    if scores.is_cuda and scores.dtype in (torch.float16, torch.bfloat16):
+    if fused_ok(scores) and scores.dtype in (torch.float16, torch.bfloat16):
         if causal and mask is None:
             probs = _sm.scaled_causal_softmax(scores, scale)
         else:
@@ -378,7 +378,7 @@ def attention(q, k, v, causal=True, mask=None, scale=None, dropout_p=0.0, window
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
     p = dropout_p if training else 0.0
-    if use_flash and not attention_in_fp32 and q.is_cuda:
+    if use_flash and not attention_in_fp32 and fused_ok(q):
         kbias = key_padding_bias(mask, q.shape[1], k.shape[1], mask_value) if mask is not None else None
         if flash_supported(q, p, mask, kbias):
             _count_flash(kbias)

@@ -9,7 +9,7 @@ rescaled SUM), matching Megatron-style vocab-parallel CE semantics of the refere
 import torch
 import torch.distributed as dist
 
-from ._ext import ext
+from ._ext import ext, fused_ok
 from ..parallel import oneshot
 
 
@@ -76,7 +76,7 @@ class _AllreduceSum(torch.autograd.Function):
 
 def cross_entropy_rows(logits, target, vocab_start=0, ignore_index=-100, group=None):
     """Per-token loss (fp32) for [..., V_local] logits and [...] int64 targets."""
-    if logits.is_cuda:
+    if fused_ok(logits):
         return _FusedCrossEntropy.apply(logits, target, vocab_start, ignore_index, group)
     return _ref_vocab_parallel_ce(logits, target, vocab_start, ignore_index, group)
 

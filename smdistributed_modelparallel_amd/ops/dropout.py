@@ -16,9 +16,7 @@ CPU tensors use ``torch.nn.functional.dropout``.
 """
 import torch
 
-from ._ext import ext
-
-
+from ._ext import ext, fused_ok
 def dropout_seed_offset(device, increment=4):
     """(seed, offset) for the in-kernel dropout hash, advanced like a philox consumer; no
     device synchronisation."""
@@ -63,7 +61,7 @@ def dropout_add(x, residual, p, training=True):
     """residual + dropout(x, p) (residual may be None)."""
     if not training or p == 0.0:
         return x if residual is None else x + residual
-    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
+    if not fused_ok(x) or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
         y = torch.nn.functional.dropout(x, p, True)
         return y if residual is None else y + residual
     return _DropoutAdd.apply(x, residual, float(p))
@@ -85,7 +83,7 @@ def add3(a, b, c):
     reference `smp/torch/nn/transformer.py` parallel_attention path).  Falls back to two adds
     for CPU tensors, mixed dtypes/shapes or non-contiguous / unaligned inputs."""
     ts = (a, b, c)
-    if (a.is_cuda and a.dtype in (torch.bfloat16, torch.float16, torch.float32)
+    if (fused_ok(a) and a.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and all(t.dtype == a.dtype and t.shape == a.shape and t.is_contiguous() and _aligned(t) for t in ts)):
         return _Add3.apply(a, b, c)
     return a + b + c

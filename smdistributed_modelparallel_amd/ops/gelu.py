@@ -3,7 +3,7 @@ import math
 
 import torch
 
-from ._ext import ext
+from ._ext import ext, fused_ok
 from .linear import _fusable
 
 
@@ -47,7 +47,7 @@ def bias_gelu(x, bias=None, exact=False, bias_grad=True):
     ``bias_grad=False``: the backward leaves the bias gradient to the linear layer that produced
     x (``ops.linear.linear(..., dbias_of=bias)``), whose weight-gradient kernel sums the same
     dx over tokens in its pass over it -- the GeLU backward is then a pure elementwise pass."""
-    if x.is_cuda:
+    if fused_ok(x):
         return _BiasGeLU.apply(x, bias, bool(exact), bool(bias_grad))
     v = x + bias if bias is not None else x
     return _gelu_erf_ref(v) if exact else _gelu_tanh_ref(v)

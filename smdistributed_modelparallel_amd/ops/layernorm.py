@@ -7,7 +7,7 @@ input / weight dtypes.
 """
 import torch
 
-from ._ext import ext
+from ._ext import ext, fused_ok
 from .dropout import dropout_seed_offset
 from .linear import _fusable
 
@@ -137,7 +137,7 @@ class _MixedLayerNorm(torch.autograd.Function):
 
 def mixed_layer_norm(x, weight, bias, eps=1e-5):
     """LayerNorm whose output takes the affine parameters' dtype (input any dtype)."""
-    if x.is_cuda and weight is not None and bias is not None:
+    if fused_ok(x) and weight is not None and bias is not None:
         return _MixedLayerNorm.apply(x, weight, bias, eps)
     # statistics and affine in fp32 from the unrounded input, one rounding into the parameters' dtype
     w = weight.float() if weight is not None else None
@@ -147,14 +147,14 @@ def mixed_layer_norm(x, weight, bias, eps=1e-5):
 
 
 def layer_norm(x, weight, bias, eps=1e-5):
-    if x.is_cuda:
+    if fused_ok(x):
         return _FusedLayerNorm.apply(x, weight, bias, eps)
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps)
 
 
 def layer_norm_passthrough(x, weight, bias, eps=1e-5):
     """Returns (LN(x), x) with the two backward paths of x summed inside the LN kernel."""
-    if x.is_cuda:
+    if fused_ok(x):
         return _FusedLayerNormPassthrough.apply(x, weight, bias, eps)
     return torch.nn.functional.layer_norm(x, (x.shape[-1],), weight, bias, eps), x
 
@@ -162,7 +162,7 @@ def layer_norm_passthrough(x, weight, bias, eps=1e-5):
 def add_layer_norm(x, residual, weight, bias, eps=1e-5, dropout_p=0.0, drawn=None):
     """Returns (LN(dropout(x) + residual), dropout(x) + residual).  ``drawn``: the dropout's
     (seed, offset), drawn earlier with ``dropout_seed_offset`` to keep a generator order."""
-    if x.is_cuda:
+    if fused_ok(x):
         return _FusedAddLayerNorm.apply(x, residual, weight, bias, eps, float(dropout_p), drawn)
     if dropout_p > 0.0:
         x = torch.nn.functional.dropout(x, dropout_p, True)

@@ -382,6 +382,11 @@ class _LinearWGradAccum(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        if dy.dtype != w.dtype or x.dtype != w.dtype:
+            # forward under torch.autocast (the GEMM ran in the autocast dtype, the inputs were
+            # saved as given): the backward runs in the parameters' dtype, and autograd casts dX
+            # back to the input's dtype
+            dy, x = dy.to(w.dtype), x.to(w.dtype)
         dx = dw = None
         grads = {2: None, 4: None}  # input index -> gradient returned to autograd
         dy2 = dy.reshape(-1, dy.shape[-1])

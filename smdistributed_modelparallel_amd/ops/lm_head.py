@@ -32,7 +32,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from ._ext import ext
+from ._ext import ext, fused_ok
 from .linear import _WT_EPOCH, _fusable
 
 # LM-head weight gradient on the MFMA weight-gradient kernel (bf16 operands)
@@ -64,7 +64,7 @@ def _padded(w, vp):
 def usable(weight, hidden):
     """The padded path applies to an odd-sized bf16/fp16 CUDA LM head inside a step (the
     cached copies are refreshed per step)."""
-    if not (_ENABLED and hidden.is_cuda and weight.is_cuda and weight.dim() == 2):
+    if not (_ENABLED and fused_ok(hidden) and weight.is_cuda and weight.dim() == 2):
         return False
     if weight.shape[0] % _ALIGN == 0 or weight.dtype not in (torch.bfloat16, torch.float16):
         return False

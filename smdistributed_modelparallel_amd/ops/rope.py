@@ -6,6 +6,7 @@ tables are built once per (seq, dim, base, device) in fp32 (precomputed tables r
 than on-device trig, per the elementwise guidance for CDNA).
 """
 import torch
+from ._ext import fused_ok
 
 _cache = {}
 PACKED_CALLS = [0]  # GPU in-place packed-QKV rotations (tests check the fast path engaged)
@@ -61,7 +62,7 @@ def apply_rotary(x, rotary_dim, base=10000, neox_style=False, offset=0):
     """Returns a new tensor with rotary applied (autograd-friendly)."""
     if rotary_dim is None or rotary_dim == 0:
         return x
-    if x.is_cuda and x.dtype in (torch.float16, torch.bfloat16, torch.float32) and x.stride(-1) == 1 \
+    if fused_ok(x) and x.dtype in (torch.float16, torch.bfloat16, torch.float32) and x.stride(-1) == 1 \
             and rotary_dim % 2 == 0:
         s = x.shape[1]
         cos, sin = rope_tables(s + offset, rotary_dim, base, x.device, 0)
@@ -120,7 +121,7 @@ def apply_rotary_qkv(y, batch, seq, heads, head_dim, rotary_dim, base=10000, neo
     result) -- otherwise the out-of-place torch path runs."""
     if rotary_dim is None or rotary_dim == 0:
         return y.view(batch, seq, 3, heads, head_dim)
-    if y.is_cuda and y.dtype in (torch.float16, torch.bfloat16, torch.float32) and y.is_contiguous() \
+    if fused_ok(y) and y.dtype in (torch.float16, torch.bfloat16, torch.float32) and y.is_contiguous() \
             and rotary_dim % 2 == 0 and y._base is None:
         cos, sin = rope_tables(seq + offset, rotary_dim, base, y.device, 0)
         PACKED_CALLS[0] += 1

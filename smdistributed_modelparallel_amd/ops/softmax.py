@@ -4,9 +4,7 @@ mask convention (reference): uint8/bool ``[b, 1, sq, sk]``, 1 = masked out.
 """
 import torch
 
-from ._ext import ext
-
-
+from ._ext import ext, fused_ok
 class _ScaledMaskedSoftmax(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, mask, scale):
@@ -52,13 +50,13 @@ def _ref_softmax(x, mask, scale, causal):
 
 
 def scaled_masked_softmax(x, mask, scale=1.0):
-    if x.is_cuda:
+    if fused_ok(x):
         return _ScaledMaskedSoftmax.apply(x, mask, scale)
     return _ref_softmax(x, mask, scale, False)
 
 
 def scaled_causal_softmax(x, scale=1.0):
-    if x.is_cuda:
+    if fused_ok(x):
         return _ScaledUpperTriangSoftmax.apply(x, scale)
     return _ref_softmax(x, None, scale, True)
 

@@ -130,6 +130,8 @@ class DistributedModel(nn.Module):
         mm.set_main_module(module)
         mm.name_modules_and_create_parent_map()
         state.engine = PipelineEngine(state)
+        if state.core.pp_size() > 1:
+            self._adopt_hf_gradient_checkpointing(module)
 
         if state.loaded_model_state is not None:
             self._deferred_load = state.loaded_model_state
@@ -151,6 +153,27 @@ class DistributedModel(nn.Module):
             self._partitions_assigned = True
 
     # ============================================================ TP replace
+
+    def _adopt_hf_gradient_checkpointing(self, module):
+        """Hugging Face gradient checkpointing (``model.gradient_checkpointing_enable()``) wraps
+        each block's call in torch.utils.checkpoint on the CALLER's stage; under pipeline
+        parallelism that block may live on another stage, and recomputing it in the backward
+        would re-issue the remote call.  Each such block is switched to smp activation
+        checkpointing instead (recomputed on the stage that owns it), as
+        ``smp.set_activation_checkpointing(block)`` would."""
+        try:
+            from transformers.modeling_layers import GradientCheckpointingLayer
+        except ImportError:  # older transformers: no per-layer flag to take over
+            return
+        n = 0
+        for m in module.modules():
+            if isinstance(m, GradientCheckpointingLayer) and getattr(m, "gradient_checkpointing", False):
+                m.gradient_checkpointing = False
+                state.module_manager.set_activation_checkpointing(m, True, False, "each", model=self)
+                n += 1
+        if n:
+            logger.info(f"pipeline parallelism: {n} Hugging Face gradient-checkpointing layers run smp activation "
+                        "checkpointing instead")
     def _replace_tp_counterparts(self, module):
         mm = state.module_manager
         reg = state.tp_registry

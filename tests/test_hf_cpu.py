@@ -559,3 +559,14 @@ def test_hf_causal_lm_padding_mask_memory_mode_matches_hf(family, pp):
     outs = run_workers("hf_lm_mask", pp * 2, [family, str(pp), "2"], timeout=300,
                        env_extra={"HF_MASK_CFG": "optimize=memory"})
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("pp,tp,mode", [(2, 1, "gc"), (2, 2, "autocast"), (1, 2, "autocast")])
+def test_hf_gradient_checkpointing_and_autocast(pp, tp, mode):
+    """HF gradient checkpointing under PP (each GradientCheckpointingLayer becomes an smp
+    activation-checkpointed module: HF's own wrapper would recompute a remote block on the
+    caller's stage) and a torch.autocast(bf16) step over fp32 parameters under TP."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("hf_gc_autocast", pp * tp, [str(pp), str(tp), mode], timeout=300)
+    assert all("OK" in o for o in outs), outs[0][-3000:]

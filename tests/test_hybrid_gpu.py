@@ -122,3 +122,12 @@ def test_hf_causal_lm_padding_mask_bf16_gpu(family, pp, tp):
     env = dict(_ENV, HF_MASK_BF16="1")
     outs = run_workers("hf_lm_mask", pp * tp, [family, str(pp), str(tp)], timeout=240, env_extra=env)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pp,tp,mode", [(1, 2, "autocast"), (2, 1, "gc")])
+def test_hf_autocast_and_gradient_checkpointing_gpu(pp, tp, mode):
+    """On the GPU: a torch.autocast(bf16) step over fp32 parameters through the TP stack's HIP
+    kernels, and HF gradient checkpointing under PP (tests/workers/hf_gc_autocast.py)."""
+    outs = run_workers("hf_gc_autocast", pp * tp, [str(pp), str(tp), mode], timeout=240, env_extra=_ENV)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
