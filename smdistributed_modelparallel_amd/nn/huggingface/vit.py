@@ -8,8 +8,8 @@ layer: each ``ViTLayer`` becomes a pre-LayerNorm, bidirectional
 ``DistributedTransformerLayer`` (exact-erf GeLU for ``hidden_act="gelu"``, q/k/v fused
 into one projection).  Keys: ``layers.{i}.attention.{q,k,v}_proj`` <->
 ``layers.{i}.attention.qkv_*``; embeddings, final LayerNorm, pooler and classifier stay HF.
-Like the reference's, this mapping is opt-in: ``register_vit(smp.tp_registry())`` (the
-predefined set covers the GPT/BERT families).
+Like the reference's, this mapping is opt-in: ``register_vit()`` (the process's registry,
+``smp.state.tp_registry``; the predefined set covers the GPT/BERT families).
 """
 from ._common import KeyMap, masked_from_hf, pack_qkv, unpack_qkv
 
@@ -96,10 +96,17 @@ def smp_to_hf(sd):
     return out
 
 
-def register_vit(registry):
+def register_vit(registry=None):
     """Opt-in registration of ViTLayer -> DistributedTransformerLayer (reference tests
-    register their ViT translation by hand the same way)."""
+    register their ViT translation by hand the same way); default: the process's registry
+    (``smp.state.tp_registry``), so ViT models created under ``smp.model_creation(
+    tensor_parallelism=True)`` afterwards get distributed layers."""
     from transformers.models.vit.modeling_vit import ViTLayer
+
+    if registry is None:
+        from ...torch.state_mod import state
+
+        registry = state.tp_registry
 
     from ..transformer import DistributedTransformerLayer
 

@@ -570,3 +570,14 @@ def test_hf_gradient_checkpointing_and_autocast(pp, tp, mode):
 
     outs = run_workers("hf_gc_autocast", pp * tp, [str(pp), str(tp), mode], timeout=300)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("pp", [1, 2])
+def test_hf_vit_opt_in_tp_matches_hf(pp):
+    """register_vit() then smp.model_creation(tensor_parallelism=True): every ViTLayer of an HF
+    ViTForImageClassification becomes a DistributedTransformerLayer; TP=2 (x PP=2) training
+    follows the plain HF model's loss for 3 SGD steps."""
+    from tests.dist_utils import run_workers
+
+    outs = run_workers("hf_vit_tp", 2 * pp, [str(pp)], timeout=300)
+    assert all("OK" in o for o in outs), outs[0][-3000:]
