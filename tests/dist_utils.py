@@ -15,9 +15,24 @@ def free_port():
     return p
 
 
+def _port_race(err):
+    # free_port() releases the port before rank 0 binds it: under pytest-xdist another test's
+    # launcher can take it in between (EADDRINUSE) -- a harness race, retried once
+    return "EADDRINUSE" in str(err)
+
+
 def run_workers(module, world, args=(), timeout=240, env_extra=None):
     """Run `python -m tests.workers.<module> args...` on `world` ranks; returns outputs.
     Raises AssertionError with the logs if any rank fails."""
+    try:
+        return _run_workers(module, world, args, timeout, env_extra)
+    except AssertionError as e:
+        if not _port_race(e):
+            raise
+        return _run_workers(module, world, args, timeout, env_extra)
+
+
+def _run_workers(module, world, args=(), timeout=240, env_extra=None):
     port = free_port()
     procs = []
     for r in range(world):
@@ -52,6 +67,15 @@ def run_workers(module, world, args=(), timeout=240, env_extra=None):
 
 def run_script(path, world, args=(), timeout=240, env_extra=None):
     """Run a repository script on `world` ranks (same env contract as run_workers)."""
+    try:
+        return _run_script(path, world, args, timeout, env_extra)
+    except AssertionError as e:
+        if not _port_race(e):
+            raise
+        return _run_script(path, world, args, timeout, env_extra)
+
+
+def _run_script(path, world, args=(), timeout=240, env_extra=None):
     port = free_port()
     procs = []
     for r in range(world):
