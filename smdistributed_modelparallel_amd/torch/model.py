@@ -609,6 +609,25 @@ class DistributedModel(nn.Module):
                 for bn, b in m.named_buffers(recurse=False):
                     yield (f"{mn}.{bn}" if mn else bn), b
 
+    def get_module_for_param(self, param):
+        """The module that directly owns ``param`` (reference torch/model.py:348)."""
+        for m in self.module.modules():
+            for p in m.parameters(recurse=False):
+                if p is param:
+                    return m
+        raise KeyError("parameter does not belong to this DistributedModel")
+
+    def load_partition(self, partitioning_and_trace_results=None):
+        """Adopt a module->partition assignment made elsewhere (reference torch/model.py:846):
+        the {module name: pp rank} dict of ``partition_dict()`` / the ``partition_file``; must cover
+        every module and come before the first step."""
+        if partitioning_and_trace_results is None:
+            return
+        if self.partitioned:
+            raise StepFunctionCalledError("load_partition must be called before the first step")
+        state.module_manager.load_partition(dict(partitioning_and_trace_results))
+        self._partitions_assigned = True
+
     def virtual_named_parameters(self):
         opt = state.optimizer
         if opt is None:

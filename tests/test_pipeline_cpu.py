@@ -293,6 +293,9 @@ def test_partition_file_save_and_load(tmp_path):
     assert all("OK save" in o for o in outs)
     outs = run_workers("partition_file", 2, ["load", path], timeout=120)
     assert all("OK load" in o for o in outs)
+    # the same assignment through DistributedModel.load_partition (reference torch/model.py:846)
+    outs = run_workers("partition_file", 2, ["api", path], timeout=120)
+    assert all("OK api" in o for o in outs)
 
 
 def test_pp2_auto_partition_metrics_published(tmp_path):

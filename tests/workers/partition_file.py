@@ -1,5 +1,6 @@
 """Worker: auto-partition result written to ``partition_file`` and reused with
-``load_partition`` (argv: save|load path)."""
+``load_partition`` (argv: save|load|api path); ``api`` hands the saved assignment to
+``DistributedModel.load_partition`` instead of the config key."""
 import json
 import sys
 
@@ -20,6 +21,11 @@ def main():
     model = smp.DistributedModel(net)
     mm = smp.state.module_manager
     assert mm.partition_loaded == (mode == "load")
+    if mode == "api":
+        with open(path) as f:
+            model.load_partition(json.load(f)["partition"])
+        assert mm.partition_loaded
+    assert model.get_module_for_param(net[3][0].weight) is net[3][0]
 
     @smp.step
     def train(model, x):
@@ -30,7 +36,7 @@ def main():
     train(model, torch.randn(8, 32))
     parts = mm.partition_dict()
     assert set(parts.values()) == {0, 1}, parts
-    if mode == "load":
+    if mode in ("load", "api"):
         with open(path) as f:
             saved = json.load(f)["partition"]
         assert parts == saved, (parts, saved)
