@@ -122,6 +122,15 @@ def model_load_state_dict(model, sd, strict=True, translate_function=None, same_
     sd = dict(sd)
     if translate_function is not None:
         sd = translate_function(sd)
+    elif "_smp_is_partial" not in sd and state.tp_registry is not None and state.tp_registry.translate_functions:
+        # an HF-keyed full dict (save_checkpoint(partial=False) of a swapped HF model, or an HF
+        # model's own state_dict): the swapped modules' hf_to_smp translators apply
+        # (reference torch/model.py:1059-1065); a dict already in this model's keys is left alone
+        own = {n for n, _ in model.module.named_parameters()}
+        if not own & set(sd):
+            for _, hf_to_smp in state.tp_registry.translate_functions:
+                if hf_to_smp is not None:
+                    sd = hf_to_smp(sd)
     from .checkpoint_compat import from_reference_state_dict, is_reference_state_dict
 
     if is_reference_state_dict(sd):

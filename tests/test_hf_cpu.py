@@ -243,9 +243,11 @@ def test_encoder_hooks_refuse_what_they_cannot_honour():
     assert issubclass(HFBertConfigError, NotImplementedError)
 
 
-def test_hf_gpt2_auto_tp2_matches_hf():
-    outs = run_workers("hf_gpt2_tp", 2, [], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
+def test_hf_gpt2_auto_tp2_matches_hf(tmp_path):
+    # after training, save_checkpoint(partial=False) writes HF keys a plain GPT2LMHeadModel loads
+    outs = run_workers("hf_gpt2_tp", 2, ["", str(tmp_path)], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
     assert all("OK" in o for o in outs)
+    assert "full HF checkpoint OK" in outs[0]
     # _match_weights: no explicit load -- the replaced modules start from the HF weights
     outs = run_workers("hf_gpt2_tp", 2, ["match"], timeout=240, env_extra={"SMP_USE_HF_GELU": "1"})
     assert all("OK" in o for o in outs)

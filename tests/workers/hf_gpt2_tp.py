@@ -62,6 +62,30 @@ def main():
     hf_sd = gpt2.layer_smp_to_hf(sd) if mode == "layer" else gpt2.smp_to_hf(sd)
     worst = max((hf_sd[k].float() - v.detach().float()).abs().max().item() for k, v in ref.state_dict().items())
     assert worst < 2e-4, worst
+    if len(sys.argv) > 2:
+        # full checkpoint in HF key space (translate_if_full): a plain transformers model loads
+        # it strictly and computes the trained model's loss
+        import os
+
+        ckpt = sys.argv[2]
+        smp.save_checkpoint(ckpt, tag="hf", partial=False, model=model, translate_if_full=True)
+        if smp.rank() == 0:
+            saved = torch.load(os.path.join(ckpt, "hf"), weights_only=True)
+            fresh = GPT2LMHeadModel(cfg)
+            fresh.load_state_dict(saved, strict=True)
+            ids = torch.randint(0, 97, (2, 16), generator=g)
+            with torch.no_grad():
+                a, b = fresh(input_ids=ids, labels=ids).loss.item(), ref(input_ids=ids, labels=ids).loss.item()
+            assert abs(a - b) < 1e-4, (a, b)
+            print("full HF checkpoint OK", flush=True)
+        # and it resumes into the TP model: HF keys go back through hf_to_smp
+        with torch.no_grad():
+            for p in model.parameters():
+                p.zero_()
+        smp.resume_from_checkpoint(ckpt, tag="hf", partial=False, load_optimizer=False)
+        back = gpt2.smp_to_hf(model.state_dict(gather_to_rank0=False))
+        worst = max((back[k].float() - v.detach().float()).abs().max().item() for k, v in ref.state_dict().items())
+        assert worst < 2e-4, worst
     print(f"rank {smp.rank()} OK", flush=True)
     smp.barrier()
 
