@@ -117,20 +117,29 @@ def model_full_state_dict(model, gather_to_rank0=True, cast_to_cpu=True):
     return out
 
 
+def translate_for_load(model, sd, translate_function=None):
+    """``translate_function`` when given; otherwise an HF-keyed full dict (save_checkpoint(
+    partial=False) of a swapped HF model, or an HF model's own state_dict) goes through the
+    swapped modules' hf_to_smp translators (reference torch/model.py:1059-1065).  A dict
+    already in this model's keys, or tagged by smp, is left alone."""
+    if translate_function is not None:
+        return translate_function(sd)
+    reg = state.tp_registry
+    if "_smp_is_partial" in sd or reg is None or not reg.translate_functions:
+        return sd
+    own = {n for n, _ in model.module.named_parameters()}
+    if own & set(sd):
+        return sd
+    for _, hf_to_smp in reg.translate_functions:
+        if hf_to_smp is not None:
+            sd = hf_to_smp(sd)
+    return sd
+
+
 def model_load_state_dict(model, sd, strict=True, translate_function=None, same_partition_load=False):
     core = state.core
     sd = dict(sd)
-    if translate_function is not None:
-        sd = translate_function(sd)
-    elif "_smp_is_partial" not in sd and state.tp_registry is not None and state.tp_registry.translate_functions:
-        # an HF-keyed full dict (save_checkpoint(partial=False) of a swapped HF model, or an HF
-        # model's own state_dict): the swapped modules' hf_to_smp translators apply
-        # (reference torch/model.py:1059-1065); a dict already in this model's keys is left alone
-        own = {n for n, _ in model.module.named_parameters()}
-        if not own & set(sd):
-            for _, hf_to_smp in state.tp_registry.translate_functions:
-                if hf_to_smp is not None:
-                    sd = hf_to_smp(sd)
+    sd = translate_for_load(model, sd, translate_function)
     from .checkpoint_compat import from_reference_state_dict, is_reference_state_dict
 
     if is_reference_state_dict(sd):

@@ -174,6 +174,7 @@ class DistributedModel(nn.Module):
         if n:
             logger.info(f"pipeline parallelism: {n} Hugging Face gradient-checkpointing layers run smp activation "
                         "checkpointing instead")
+
     def _replace_tp_counterparts(self, module):
         mm = state.module_manager
         reg = state.tp_registry
@@ -827,9 +828,10 @@ class DistributedModel(nn.Module):
 
             if is_zero_state_dict(state_dict):
                 return state.sdp.load_shard_state_dict(state_dict)
-            if translate_function is not None:
-                state_dict = translate_function(state_dict)
-            return state.sdp.load_full_state_dict(state_dict, strict=strict)
+            from .checkpoint_utils import translate_for_load
+
+            return state.sdp.load_full_state_dict(translate_for_load(self, dict(state_dict), translate_function),
+                                                  strict=strict)
         return model_load_state_dict(self, state_dict, strict=strict, translate_function=translate_function,
                                      same_partition_load=same_partition_load)
 
