@@ -121,14 +121,14 @@ def translate_for_load(model, sd, translate_function=None):
     """``translate_function`` when given; otherwise an HF-keyed full dict (save_checkpoint(
     partial=False) of a swapped HF model, or an HF model's own state_dict) goes through the
     swapped modules' hf_to_smp translators (reference torch/model.py:1059-1065).  A dict
-    already in this model's keys, or tagged by smp, is left alone."""
+    mostly in this model's keys, or tagged by smp, is left alone."""
     if translate_function is not None:
         return translate_function(sd)
     reg = state.tp_registry
     if "_smp_is_partial" in sd or reg is None or not reg.translate_functions:
         return sd
     own = {n for n, _ in model.module.named_parameters()}
-    if own & set(sd):
+    if 2 * len(own & set(sd)) > len(own):  # mostly this model's own keys (an untied lm_head may match)
         return sd
     for _, hf_to_smp in reg.translate_functions:
         if hf_to_smp is not None:

@@ -583,3 +583,14 @@ def test_hf_vit_opt_in_tp_matches_hf(pp):
 
     outs = run_workers("hf_vit_tp", 2 * pp, [str(pp)], timeout=300)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("family,how", [("gpt2", "explicit"), ("gpt2", "auto"), ("gptj", "auto"),
+                                        ("gpt_neox", "explicit")])
+def test_hf_from_pretrained_translate_tp2(tmp_path, family, how):
+    """The reference's pretrained-load flow (test_translate_state_dict.py:103-160): save_pretrained,
+    from_pretrained under smp.tensor_parallelism, load_state_dict of the saved weights with the
+    family translator (or none: the registered one applies) -> TP=2 logits equal HF's."""
+    outs = run_workers("hf_from_pretrained", 2, [family, str(tmp_path / "hf"), how], timeout=240,
+                       env_extra={"SMP_USE_HF_GELU": "1"})
+    assert all(f"OK {family} {how}" in o for o in outs)

@@ -1,0 +1,63 @@
+"""Worker: the reference's pretrained-load flow (`test/torch/mpi/test_translate_state_dict.py:
+103-160`): rank 0 writes an HF model with save_pretrained, every rank re-creates it with
+from_pretrained under smp.tensor_parallelism (swapped for smp.nn at DistributedModel), the
+saved weights are loaded with the family's translator (argv[3] "auto": no translate_function,
+the registered one applies), and the TP=2 model's logits equal the HF model's.
+argv: family(gpt2|gptj|gpt_neox) dir auto|explicit"""
+import os
+import sys
+
+import torch
+import transformers as tf
+from safetensors.torch import load_file
+
+import smdistributed_modelparallel_amd.torch as smp
+from smdistributed_modelparallel_amd.nn import DistributedTransformerLMHead
+from smdistributed_modelparallel_amd.nn.huggingface import gpt2, gptj, gptneox
+
+FAMILIES = {
+    "gpt2": (tf.GPT2Config, tf.GPT2LMHeadModel, gpt2.translate_hf_state_dict_to_smdistributed_gpt2,
+             dict(n_layer=2, n_embd=64, n_head=4, n_positions=32, resid_pdrop=0.0, embd_pdrop=0.0, attn_pdrop=0.0)),
+    "gptj": (tf.GPTJConfig, tf.GPTJForCausalLM, gptj.translate_hf_state_dict_to_smdistributed_gptj,
+             dict(n_layer=2, n_embd=64, n_head=4, n_positions=32, rotary_dim=8, resid_pdrop=0.0, embd_pdrop=0.0,
+                  attn_pdrop=0.0)),
+    "gpt_neox": (tf.GPTNeoXConfig, tf.GPTNeoXForCausalLM, gptneox.translate_hf_state_dict_to_smdistributed_gptneox,
+                 dict(num_hidden_layers=2, hidden_size=64, num_attention_heads=4, intermediate_size=256,
+                      max_position_embeddings=32)),
+}
+
+
+def main():
+    fam, d, how = sys.argv[1], sys.argv[2], sys.argv[3]
+    cfg_cls, model_cls, translate, kw = FAMILIES[fam]
+    cfg = cfg_cls(vocab_size=97, bos_token_id=0, eos_token_id=0, **kw)
+    smp.init({"tensor_parallel_degree": 2, "ddp": True})
+    torch.manual_seed(0)
+    hf = model_cls(cfg).eval()
+    if smp.rank() == 0:
+        hf.save_pretrained(d)
+    smp.barrier()
+    with smp.tensor_parallelism(enabled=True):
+        net = model_cls.from_pretrained(d)
+    model = smp.DistributedModel(net)
+    assert isinstance(model.get_module(), DistributedTransformerLMHead), type(model.get_module())
+    sd = load_file(os.path.join(d, "model.safetensors"))
+    model.load_state_dict(sd, strict=True, translate_function=translate if how == "explicit" else None)
+
+    @smp.step
+    def logits(model, ids):
+        return model(input_ids=ids)["logits"]
+
+    model.eval()
+    ids = torch.randint(0, 97, (2, 16), generator=torch.Generator().manual_seed(1))
+    out = logits(model, ids).concat()
+    with torch.no_grad():
+        ref = hf(input_ids=ids).logits
+    err = (out.float() - ref.float()).abs().max().item()
+    assert err < 1e-4, err
+    print(f"rank {smp.rank()} OK {fam} {how} err={err:.2e}", flush=True)
+    smp.barrier()
+
+
+if __name__ == "__main__":
+    main()
