@@ -586,7 +586,7 @@ def test_hf_vit_opt_in_tp_matches_hf(pp):
 
 
 @pytest.mark.parametrize("family,how", [("gpt2", "explicit"), ("gpt2", "auto"), ("gptj", "auto"),
-                                        ("gpt_neox", "explicit")])
+                                        ("gpt_neo", "auto"), ("gpt_neox", "explicit")])
 def test_hf_from_pretrained_translate_tp2(tmp_path, family, how):
     """The reference's pretrained-load flow (test_translate_state_dict.py:103-160): save_pretrained,
     from_pretrained under smp.tensor_parallelism, load_state_dict of the saved weights with the

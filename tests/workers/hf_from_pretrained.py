@@ -3,7 +3,7 @@
 from_pretrained under smp.tensor_parallelism (swapped for smp.nn at DistributedModel), the
 saved weights are loaded with the family's translator (argv[3] "auto": no translate_function,
 the registered one applies), and the TP=2 model's logits equal the HF model's.
-argv: family(gpt2|gptj|gpt_neox) dir auto|explicit"""
+argv: family(gpt2|gptj|gpt_neo|gpt_neox) dir auto|explicit"""
 import os
 import sys
 
@@ -13,7 +13,7 @@ from safetensors.torch import load_file
 
 import smdistributed_modelparallel_amd.torch as smp
 from smdistributed_modelparallel_amd.nn import DistributedTransformerLMHead
-from smdistributed_modelparallel_amd.nn.huggingface import gpt2, gptj, gptneox
+from smdistributed_modelparallel_amd.nn.huggingface import gpt2, gptj, gptneo, gptneox
 
 FAMILIES = {
     "gpt2": (tf.GPT2Config, tf.GPT2LMHeadModel, gpt2.translate_hf_state_dict_to_smdistributed_gpt2,
@@ -21,6 +21,10 @@ FAMILIES = {
     "gptj": (tf.GPTJConfig, tf.GPTJForCausalLM, gptj.translate_hf_state_dict_to_smdistributed_gptj,
              dict(n_layer=2, n_embd=64, n_head=4, n_positions=32, rotary_dim=8, resid_pdrop=0.0, embd_pdrop=0.0,
                   attn_pdrop=0.0)),
+    "gpt_neo": (tf.GPTNeoConfig, tf.GPTNeoForCausalLM, gptneo.translate_hf_state_dict_to_smdistributed_gptneo,
+                dict(num_layers=2, hidden_size=64, num_heads=4, max_position_embeddings=32,
+                     attention_types=[[["global", "local"], 1]], window_size=8, resid_dropout=0.0,
+                     embed_dropout=0.0, attention_dropout=0.0)),
     "gpt_neox": (tf.GPTNeoXConfig, tf.GPTNeoXForCausalLM, gptneox.translate_hf_state_dict_to_smdistributed_gptneox,
                  dict(num_hidden_layers=2, hidden_size=64, num_attention_heads=4, intermediate_size=256,
                       max_position_embeddings=32)),
