@@ -30,6 +30,8 @@ FAMILIES = {
                       max_position_embeddings=32)),
 }
 
+TRANSLATOR_MODULES = {"gpt2": gpt2, "gptj": gptj, "gpt_neo": gptneo, "gpt_neox": gptneox}
+
 
 def main():
     fam, d, how = sys.argv[1], sys.argv[2], sys.argv[3]
@@ -59,6 +61,16 @@ def main():
         ref = hf(input_ids=ids).logits
     err = (out.float() - ref.float()).abs().max().item()
     assert err < 1e-4, err
+    # and back out (reference test_translate_state_dict_to_hf_*): the gathered state dict through
+    # translate_state_dict_to_hf_<family> loads strictly into a fresh HF model with equal logits
+    to_hf = getattr(TRANSLATOR_MODULES[fam], "translate_state_dict_to_hf_" + TRANSLATOR_MODULES[fam].__name__.rsplit(".", 1)[1])
+    full = model.state_dict(gather_to_rank0=False)
+    fresh = model_cls(cfg).eval()
+    fresh.load_state_dict(to_hf(full, cfg.max_position_embeddings if hasattr(cfg, "max_position_embeddings") else 32),
+                          strict=True)
+    with torch.no_grad():
+        err2 = (fresh(input_ids=ids).logits.float() - ref.float()).abs().max().item()
+    assert err2 < 1e-5, err2
     print(f"rank {smp.rank()} OK {fam} {how} err={err:.2e}", flush=True)
     smp.barrier()
 
