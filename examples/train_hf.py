@@ -116,10 +116,10 @@ def main():
 
     dev = smp.state.device
     g = torch.Generator(device=dev)
-    g.manual_seed(7 + smp.dp_rank())
     batch = args.mbs * args.microbatches
     t0 = time.time()
     for step in range(start, args.steps):
+        g.manual_seed(7 + smp.dp_rank() + 1000 * step)  # per-step batches: a resumed run sees the same data
         ids = torch.randint(0, args.vocab, (batch, args.seq), device=dev, generator=g)
         opt.zero_grad()
         out = train_step(model, ids)

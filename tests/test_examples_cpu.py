@@ -60,3 +60,23 @@ def test_train_hf_gpt2_delayed_init_uses_hf_initialiser():
                                                          "--activation-checkpointing", "--steps", "2"], timeout=300)
     first = float(re.search(r"step 1 loss ([0-9.]+)", outs[0]).group(1))
     assert abs(first - math.log(97)) < 0.3, first
+
+
+def test_train_hf_gptj_tp2_sharded_optimizer_resume_is_exact(tmp_path):
+    """GPT-J swapped for smp.nn at TP=2 x DP=2 with sharded optimizer state: a run checkpointed at
+    step 4 and resumed reproduces steps 5-6 of an uninterrupted run exactly (model weights and every
+    rank's optimizer shard come back; the example draws each step's batch from the step index)."""
+    import re
+
+    common = _HF + ["--family", "gptj", "--tp", "2", "--shard-optimizer-state"]
+    ck = ["--ckpt-dir", str(tmp_path / "ck"), "--ckpt-every", "2"]
+    run_script("examples/train_hf.py", 4, common + ck + ["--steps", "4"], timeout=300)
+    resumed = run_script("examples/train_hf.py", 4, common + ck + ["--steps", "6"], timeout=300)[0]
+    assert "at step 4" in resumed, resumed[-2000:]
+    straight = run_script("examples/train_hf.py", 4, common + ["--steps", "6"], timeout=300)[0]
+
+    def losses(out):
+        return {int(s): l for s, l in re.findall(r"step (\d+) loss ([0-9.]+)", out)}
+
+    a, b = losses(resumed), losses(straight)
+    assert a[5] == b[5] and a[6] == b[6], (a, b)
