@@ -1,3 +1,4 @@
+import pytest
 """examples/train_gpt.py runs as documented (gloo, 2 ranks): pipeline-parallel training with
 gradient clipping, partial checkpoints every 2 steps, and a second launch that resumes from
 the newest checkpoint."""
@@ -62,18 +63,22 @@ def test_train_hf_gpt2_delayed_init_uses_hf_initialiser():
     assert abs(first - math.log(97)) < 0.3, first
 
 
-def test_train_hf_gptj_tp2_sharded_optimizer_resume_is_exact(tmp_path):
-    """GPT-J swapped for smp.nn at TP=2 x DP=2 with sharded optimizer state: a run checkpointed at
-    step 4 and resumed reproduces steps 5-6 of an uninterrupted run exactly (model weights and every
-    rank's optimizer shard come back; the example draws each step's batch from the step index)."""
+@pytest.mark.parametrize("world,layout", [
+    (4, ["--family", "gptj", "--tp", "2", "--shard-optimizer-state"]),  # TP=2 x DP=2, sharded optimizer
+    (2, ["--family", "gpt_neox", "--pp", "2"]),  # 2 pipeline stages, per-stage partial files
+])
+def test_train_hf_resume_is_exact(tmp_path, world, layout):
+    """A run checkpointed at step 4 and resumed reproduces steps 5-6 of an uninterrupted run
+    exactly (model weights and every rank's optimizer state come back; the example draws each
+    step's batch from the step index; these families have no dropout by default)."""
     import re
 
-    common = _HF + ["--family", "gptj", "--tp", "2", "--shard-optimizer-state"]
+    common = _HF + layout
     ck = ["--ckpt-dir", str(tmp_path / "ck"), "--ckpt-every", "2"]
-    run_script("examples/train_hf.py", 4, common + ck + ["--steps", "4"], timeout=300)
-    resumed = run_script("examples/train_hf.py", 4, common + ck + ["--steps", "6"], timeout=300)[0]
+    run_script("examples/train_hf.py", world, common + ck + ["--steps", "4"], timeout=300)
+    resumed = run_script("examples/train_hf.py", world, common + ck + ["--steps", "6"], timeout=300)[0]
     assert "at step 4" in resumed, resumed[-2000:]
-    straight = run_script("examples/train_hf.py", 4, common + ["--steps", "6"], timeout=300)[0]
+    straight = run_script("examples/train_hf.py", world, common + ["--steps", "6"], timeout=300)[0]
 
     def losses(out):
         return {int(s): l for s, l in re.findall(r"step (\d+) loss ([0-9.]+)", out)}
