@@ -1,7 +1,8 @@
-import pytest
 """examples/train_gpt.py runs as documented (gloo, 2 ranks): pipeline-parallel training with
 gradient clipping, partial checkpoints every 2 steps, and a second launch that resumes from
 the newest checkpoint."""
+import pytest
+
 from tests.dist_utils import run_script
 
 
