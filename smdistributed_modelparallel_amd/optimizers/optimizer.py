@@ -145,9 +145,38 @@ class DistributedOptimizer(torch.optim.Optimizer):
     def defaults(self):
         return self.optimizer.defaults
 
+    # torch names of the fused kernels' per-parameter moments
+    _TORCH_STATE_NAMES = {"adam": {"m": "exp_avg", "v": "exp_avg_sq"}, "adamw": {"m": "exp_avg", "v": "exp_avg_sq"},
+                          "lamb": {"m": "exp_avg", "v": "exp_avg_sq"}, "sgd": {"m": "momentum_buffer"},
+                          "adagrad": {"v": "sum"}}
+
     @property
     def state(self):
-        return self.optimizer.state
+        """``optimizer.state[param]`` as torch names it (``exp_avg`` / ``exp_avg_sq`` / ``step``,
+        ``momentum_buffer``, ``sum``): views of the flat fp32 state for every parameter held whole
+        by this rank, so reads and in-place edits reach the fused optimizer.  Parameters split
+        across shards (shard_optimizer_state) are absent; the generic path keeps the inner
+        optimizer's own state."""
+        names = self._TORCH_STATE_NAMES.get(self.kind)
+        if names is None or state.model is None:
+            return self.optimizer.state
+        from collections import defaultdict
+
+        out = defaultdict(dict)
+        for d in self.domains:
+            flat = state.model.flat_groups[d.key]
+            for p in d.params:
+                off, n = flat.offsets[p], p.numel()
+                if off < d.start or off + n > d.end:
+                    continue
+                lo = off - d.start
+                entry = {"step": torch.tensor(float(self._step_count[d.group_index]))}
+                for k, tname in names.items():
+                    t = getattr(d, k)
+                    if t is not None:
+                        entry[tname] = t[lo:lo + n].view(p.shape)
+                out[p] = entry
+        return out
 
     # ----------------------------------------------------------------- build
     def _on_model_partitioned(self):

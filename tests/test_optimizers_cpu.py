@@ -38,3 +38,11 @@ def test_lr_scheduler_on_distributed_optimizer(pp, tp):
     it (they refused the wrapper before round 6), with gradient accumulation across steps."""
     outs = run_workers("lr_sched", pp * tp, [str(pp), str(tp)], timeout=300)
     assert all("OK" in o for o in outs), outs[0][-3000:]
+
+
+@pytest.mark.parametrize("kind", ["adamw", "sgd", "adagrad"])
+def test_optimizer_state_views_match_torch(kind):
+    """optimizer.state[param] (exp_avg / exp_avg_sq / step, momentum_buffer, sum) reads and writes
+    the fused flat-buffer state, equal to a plain torch optimizer's."""
+    outs = run_workers("opt_state_view", 1, [kind], timeout=120)
+    assert f"OK {kind}" in outs[0]
